@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""mxllm headline benchmark: fine-tune tokens/sec (whole node), Llama-3.1-70B DDP.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched by torchrun, one rank per GPU over RCCL.  W untimed warm-up
+steps, then EXACTLY K timed optimizer steps bracketed by barrier +
+device synchronize, wall time MAX over ranks; rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json metric/config): Llama-3.1-70B architecture (80 layers,
+h 8192, 64/8 heads, ffn 28672, vocab 128256), random-init bf16 weights
+created on device, synthetic token batches of seq_len 2048.  Each GPU holds a
+FULL 141 GB bf16 replica of the model (288 GB HBM3E per MI355X) and the
+fine-tune is LoRA (r=16 on q,k,v,o,gate,up,down; frozen base), so plain
+data-parallel DDP runs at every N from 1 to 8 — weak scaling, per-GPU micro
+batch fixed.  Every timed step is a complete step: forward through all 80
+layers, fused LM-head + CE over the 128k vocab, full backward (activation
+gradients through every layer + adapter gradients), bucketed RCCL all-reduce
+of the adapter gradients, grad-norm clip and fused AdamW.
+
+``--finetune full`` (e.g. with ``--model llama3.1-8b``) trains every weight
+(bf16 params/grads, fp32 master + Adam moments) — BASELINE config 2/3.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "fine-tune tokens/sec (whole node) Llama-3.1-70B DDP at 1/2/4/8 MI355X"
+PRETTY = {"llama3.1-70b": "Llama-3.1-70B", "llama3.1-8b": "Llama-3.1-8B", "llama3.2-1b": "Llama-3.2-1B",
+          "tiny": "tiny", "tiny-d128": "tiny-d128"}
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="llama3.1-70b")
+    ap.add_argument("--finetune", choices=["lora", "full"], default="lora")
+    ap.add_argument("--lora-r", type=int, default=16)
+    ap.add_argument("--lora-alpha", type=float, default=32.0)
+    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--act-ckpt", action="store_true", help="activation checkpointing per layer")
+    ap.add_argument("--bucket-mb", type=float, default=128.0)
+    ap.add_argument("--device", default=None, help="force 'cpu' for a plumbing run")
+    ap.add_argument("--layers", type=int, default=None, help="override n_layers (NOT valid for the headline)")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    if a.device == "cpu":
+        os.environ["MXLLM_FORCE_CPU"] = "1"
+    from mxllm.models import Llama, get_config
+    from mxllm.parallel import runtime
+    from mxllm.train.trainer import OptimConfig, Trainer
+    from mxllm.data import SyntheticTokens
+
+    env = runtime.init()
+    dev = env.device
+    cfg = get_config(a.model)
+    if a.layers:
+        cfg = cfg.replace(n_layers=a.layers)
+    torch.manual_seed(0)
+    lora_r = a.lora_r if a.finetune == "lora" else 0
+    t0 = time.perf_counter()
+    model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
+                  activation_checkpointing=a.act_ckpt)
+    trainer = Trainer(model, env, OptimConfig(lr=1e-4, weight_decay=0.0, grad_clip=1.0), bucket_mb=a.bucket_mb)
+    data = SyntheticTokens(cfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1, rank=env.rank)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+
+    def step():
+        mbs = [data.next() for _ in range(a.grad_accum)]
+        return trainer.train_step(mbs)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(a.warmup):
+        loss = step()
+    sync()
+    runtime.barrier()
+    sync()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    sync()
+    runtime.barrier()
+    sync()
+    elapsed = time.perf_counter() - t_start
+    elapsed = runtime.all_reduce_scalars([elapsed], op="max")[0]
+    loss_v = float(loss.float().item()) if a.steps or a.warmup else float("nan")
+    tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size
+    tps = tokens_per_step * a.steps / elapsed if a.steps else 0.0
+    ms = 1e3 * elapsed / max(1, a.steps)
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else 0.0
+    flops_tok = cfg.train_flops_per_token(a.seq_len, lora=(a.finetune == "lora"))
+    mfu = tps * flops_tok / (env.world_size * 2.5e15) if dev.type == "cuda" else 0.0
+    out = {
+        "metric": METRIC,
+        "value": round(tps, 2),
+        "unit": "tokens/s",
+        "n_gpus": env.world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random token ids, random-init weights)",
+        "config": {
+            "model": PRETTY.get(cfg.name, cfg.name) + (f" ({cfg.n_layers} layers)" if a.layers else ""),
+            "global_batch": a.micro_batch * a.grad_accum * env.world_size,
+            "seq_len": a.seq_len,
+            "parallelism": f"dp{env.world_size}",
+            "finetune": (f"lora r={lora_r} alpha={a.lora_alpha} on q,k,v,o,gate,up,down; frozen bf16 base"
+                         if a.finetune == "lora" else "full (bf16 params+grads, fp32 master/Adam)"),
+            "micro_batch": a.micro_batch,
+            "grad_accum": a.grad_accum,
+            "activation_checkpointing": a.act_ckpt,
+            "optimizer": "fused AdamW (HIP), grad clip 1.0",
+        },
+        "tokens_per_sec_per_gpu": round(tps / env.world_size, 2),
+        "model_tflops_per_gpu": round(tps * flops_tok / env.world_size / 1e12, 1),
+        "mfu_vs_2.5PF_dense": round(mfu, 4),
+        "peak_hbm_gb": round(peak_gb, 1),
+        "init_s": round(init_s, 1),
+        "final_loss": round(loss_v, 4),
+        "trainable_params": model.num_params(trainable_only=True),
+    }
+    if env.is_main:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    runtime.cleanup()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,60 @@
+// Small utility kernels:
+//  * segmented_mean_i32: SURVEY §2.4 K16 — the batched replacement for the
+//    reference's per-prompt `torch.tensor([ord(c)...]).mean().item()`
+//    (reference src/utils.py:25-28).  One wave per segment, shuffle reduce.
+//  * scale/accumulate helpers used by the trainer (grad scaling, sq-norm).
+#include "common.h"
+
+namespace mx {
+
+__global__ void __launch_bounds__(256) segmented_mean_kernel(const int32_t* __restrict__ codes,
+                                                             const int64_t* __restrict__ offs,
+                                                             float* __restrict__ out, int nseg) {
+  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (seg >= nseg) return;
+  const int64_t b = offs[seg], e = offs[seg + 1];
+  // accumulate in f64 per lane: exact for code points (< 2^21) over any length
+  double s = 0.0;
+  for (int64_t i = b + lane; i < e; i += 64) s += (double)codes[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[seg] = (e > b) ? (float)(s / (double)(e - b)) : NAN;
+}
+
+// sum of squares of an f32 vector into out[slot] (atomic, one per block).
+__global__ void __launch_bounds__(256) sqnorm_f32_kernel(const float* __restrict__ x, int64_t n,
+                                                         float* __restrict__ out) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+      s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    } else {
+      for (int64_t j = i; j < n; ++j) s += x[j] * x[j];
+    }
+  }
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+extern "C" int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, float* out, int nseg,
+                                     hipStream_t stream) {
+  if (nseg <= 0) return 0;
+  segmented_mean_kernel<<<(nseg + 3) / 4, 256, 0, stream>>>(codes, offs, out, nseg);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_sqnorm_f32(const float* x, int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  sqnorm_f32_kernel<<<(int)blocks, 256, 0, stream>>>(x, n, out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,133 @@
+"""In-tree build of the mxllm native extension for gfx950 (MI355X).
+
+No JIT cache and no hipify: every ``csrc/kernels/*.hip`` file is compiled
+with ``hipcc --offload-arch=gfx950`` into an object, ``csrc/*.cpp`` (the torch
+op bindings and the C++ runtime) with the host compiler, and everything is
+linked into ``mxllm/_C.so`` next to this file, so the built library travels
+with the repo snapshot to the GPU box.
+
+The HIP runtime is taken from torch's own ``torch/lib/libamdhip64.so``
+(same SONAME ``libamdhip64.so.7`` as /opt/rocm's), so the extension and torch
+share one runtime instance in-process.
+
+Usage: ``python -m mxllm._build [--force] [-j N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shlex
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OUT_DIR = os.path.join(ROOT, "build", "obj")
+LIB_PATH = os.path.join(ROOT, "mxllm", "_C.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("MXLLM_ARCH", "gfx950")
+
+
+def _torch_paths():
+    import torch  # noqa: F401  (only for its install location)
+
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    lib = os.path.join(tdir, "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _hash(paths, extra: str) -> str:
+    h = hashlib.sha1(extra.encode())
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(shlex.quote(c) for c in cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    inc, tlib, abi = _torch_paths()
+    os.makedirs(OUT_DIR, exist_ok=True)
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    cpp_srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")) + glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    py_inc = sysconfig.get_paths()["include"]
+
+    hip_flags = [
+        "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+        "-ffp-contract=fast", "-Wno-unused-result", f"-I{CSRC}", f"-I{os.path.join(CSRC, 'kernels')}",
+    ]
+    cxx_flags = [
+        "-O3", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
+        "-DTORCH_EXTENSION_NAME=_C", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}", f"-I{ROCM}/include",
+        f"-I{py_inc}", "-Wno-deprecated-declarations", "-Wno-unused-parameter",
+    ] + [f"-I{p}" for p in inc]
+
+    jobs_list = []
+    for src in hip_srcs:
+        key = _hash([src] + hdrs, " ".join(hip_flags))
+        obj = os.path.join(OUT_DIR, os.path.basename(src) + f".{key}.o")
+        cmd = [os.path.join(ROCM, "bin", "hipcc")] + hip_flags + ["-c", src, "-o", obj]
+        jobs_list.append((src, obj, cmd))
+    for src in cpp_srcs:
+        key = _hash([src] + hdrs, " ".join(cxx_flags))
+        obj = os.path.join(OUT_DIR, os.path.basename(src) + f".{key}.o")
+        cmd = ["g++"] + cxx_flags + ["-c", src, "-o", obj]
+        jobs_list.append((src, obj, cmd))
+
+    todo = [(s, o, c) for (s, o, c) in jobs_list if force or not os.path.exists(o)]
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            futs = {ex.submit(_run, c): s for (s, o, c) in todo}
+            for f in cf.as_completed(futs):
+                f.result()
+                if verbose:
+                    print(f"[mxllm build] compiled {os.path.relpath(futs[f], ROOT)}", flush=True)
+    objs = [o for (_, o, _) in jobs_list]
+    link_key = _hash([], "|".join(objs))
+    stamp = LIB_PATH + ".stamp"
+    if force or not os.path.exists(LIB_PATH) or not os.path.exists(stamp) or open(stamp).read() != link_key:
+        tmp = LIB_PATH + ".tmp"
+        cmd = (["g++", "-shared", "-o", tmp] + objs + [
+            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+            f"{tlib}/libamdhip64.so", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed",
+        ])
+        _run(cmd)
+        os.replace(tmp, LIB_PATH)
+        with open(stamp, "w") as f:
+            f.write(link_key)
+        if verbose:
+            print(f"[mxllm build] linked {os.path.relpath(LIB_PATH, ROOT)}", flush=True)
+    # drop stale objects from older source versions
+    keep = set(objs)
+    for o in glob.glob(os.path.join(OUT_DIR, "*.o")):
+        if o not in keep:
+            try:
+                os.remove(o)
+            except OSError:
+                pass
+    return LIB_PATH
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 8))
+    a = ap.parse_args(argv)
+    print(build(force=a.force, jobs=a.j, verbose=True))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

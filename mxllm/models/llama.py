@@ -1,0 +1,167 @@
+"""Llama-3.1 decoder built from mxllm ops (MI355X-first layout).
+
+Design choices:
+  * Fused projections: Wqkv = [Wq; Wk; Wv] and Wgu = [Wgate; Wup], so every
+    transformer sub-block issues one large hipBLASLt GEMM per projection.
+  * Residual adds are fused into the following RMSNorm (``add_rms_norm``),
+    including across the layer boundary, so the residual stream is touched
+    once per sub-block.
+  * The attention segment (split + RoPE + flash attention) is one autograd
+    node, the LM head + CE is another (``linear_cross_entropy``).
+  * Weights are created directly on the target device in bf16 with a seeded
+    RNG — a 70B model initialises on one MI355X in seconds, never on the host.
+  * LoRA (``lora_r > 0``): base weights frozen (no weight-gradient GEMMs), one
+    adapter per projection split on q, k, v, o, gate, up, down.
+
+Reference parity: the reference repo advertises "fine-tuning of Meta Llama 3.1
+70B" (reference README.md:1-3) but contains no model; this module is that model.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.utils.checkpoint as ckpt
+
+from .. import ops
+from ..ops import reference as ref
+from .config import LlamaConfig
+
+
+class FusedLinear(nn.Module):
+    """y = x @ W^T with W = concat(splits) [sum(splits), in]; optional per-split LoRA."""
+
+    def __init__(self, in_features: int, splits: list[int], *, dtype, device, lora_r: int = 0,
+                 lora_alpha: float = 16.0, train_base: bool = True):
+        super().__init__()
+        self.in_features = in_features
+        self.splits = list(splits)
+        self.weight = nn.Parameter(torch.empty(sum(splits), in_features, dtype=dtype, device=device),
+                                   requires_grad=train_base)
+        self.lora_r = lora_r
+        if lora_r > 0:
+            self.scaling = lora_alpha / lora_r
+            self.lora_a = nn.Parameter(torch.empty(len(splits) * lora_r, in_features, dtype=torch.float32,
+                                                   device=device))
+            self.lora_b = nn.ParameterList([
+                nn.Parameter(torch.zeros(n, lora_r, dtype=torch.float32, device=device)) for n in splits])
+
+    @torch.no_grad()
+    def reset_parameters(self, std: float, gen: torch.Generator | None):
+        self.weight.normal_(0.0, std, generator=gen)
+        if self.lora_r > 0:
+            bound = 1.0 / math.sqrt(self.in_features)
+            self.lora_a.uniform_(-bound, bound, generator=gen)
+            for b in self.lora_b:
+                b.zero_()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.lora_r > 0:
+            return ops.lora_linear(x, self.weight, self.lora_a, list(self.lora_b), self.splits, self.scaling)
+        return ops.linear(x, self.weight)
+
+
+class LlamaLayer(nn.Module):
+    def __init__(self, cfg: LlamaConfig, *, dtype, device, lora_r: int, lora_alpha: float, train_base: bool):
+        super().__init__()
+        kw = dict(dtype=dtype, device=device, lora_r=lora_r, lora_alpha=lora_alpha, train_base=train_base)
+        h = cfg.hidden
+        self.attn_norm = nn.Parameter(torch.ones(h, dtype=dtype, device=device), requires_grad=train_base)
+        self.mlp_norm = nn.Parameter(torch.ones(h, dtype=dtype, device=device), requires_grad=train_base)
+        self.wqkv = FusedLinear(h, [cfg.q_dim, cfg.kv_dim, cfg.kv_dim], **kw)
+        self.wo = FusedLinear(cfg.q_dim, [h], **kw)
+        self.wgu = FusedLinear(h, [cfg.ffn, cfg.ffn], **kw)
+        self.wd = FusedLinear(cfg.ffn, [h], **kw)
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig, *, device=None, dtype=torch.bfloat16, lora_r: int = 0,
+                 lora_alpha: float = 16.0, seed: int = 0, init: bool = True, activation_checkpointing: bool = False):
+        super().__init__()
+        device = torch.device(device) if device is not None else torch.device("cpu")
+        self.cfg = cfg
+        self.lora = lora_r > 0
+        train_base = not self.lora
+        self.activation_checkpointing = activation_checkpointing
+        self.tok_emb = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, dtype=dtype, device=device),
+                                    requires_grad=train_base)
+        self.layers = nn.ModuleList([
+            LlamaLayer(cfg, dtype=dtype, device=device, lora_r=lora_r, lora_alpha=lora_alpha, train_base=train_base)
+            for _ in range(cfg.n_layers)])
+        self.final_norm = nn.Parameter(torch.ones(cfg.hidden, dtype=dtype, device=device), requires_grad=train_base)
+        if cfg.tie_embeddings:
+            self.lm_head = None
+        else:
+            self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, dtype=dtype, device=device),
+                                        requires_grad=train_base)
+        cos, sin = ref.rope_tables(min(cfg.max_seq_len, 131072), cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
+        self.register_buffer("rope_cos", cos.to(device), persistent=False)
+        self.register_buffer("rope_sin", sin.to(device), persistent=False)
+        if init:
+            self.reset_parameters(seed)
+
+    @torch.no_grad()
+    def reset_parameters(self, seed: int = 0):
+        dev = self.tok_emb.device
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        std = 0.02
+        self.tok_emb.normal_(0.0, std, generator=gen)
+        for layer in self.layers:
+            for lin in (layer.wqkv, layer.wo, layer.wgu, layer.wd):
+                lin.reset_parameters(std, gen)
+        if self.lm_head is not None:
+            self.lm_head.normal_(0.0, std, generator=gen)
+
+    @property
+    def head_weight(self) -> torch.Tensor:
+        return self.tok_emb if self.lm_head is None else self.lm_head
+
+    # ------------------------------------------------------------------ training forward
+    def _layer(self, i: int, x: torch.Tensor, h: torch.Tensor, B: int, S: int):
+        cfg = self.cfg
+        layer = self.layers[i]
+        qkv = layer.wqkv(x)
+        o = ops.attention_block(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads,
+                                cfg.head_dim, causal=True)
+        a = layer.wo(o)
+        x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps)
+        m = ops.swiglu(layer.wgu(x))
+        d = layer.wd(m)
+        nxt = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
+        x, h = ops.add_rms_norm(d, h, nxt, cfg.norm_eps)
+        return x, h
+
+    def hidden_states(self, ids: torch.Tensor) -> torch.Tensor:
+        """ids [B, S] -> final normed hidden [B*S, H]."""
+        B, S = ids.shape
+        h = ops.embedding(ids.reshape(-1), self.tok_emb)
+        x = ops.rms_norm(h, self.layers[0].attn_norm, self.cfg.norm_eps) if len(self.layers) else h
+        for i in range(len(self.layers)):
+            if self.activation_checkpointing and self.training and torch.is_grad_enabled():
+                x, h = ckpt.checkpoint(self._layer, i, x, h, B, S, use_reentrant=False)
+            else:
+                x, h = self._layer(i, x, h, B, S)
+        if not len(self.layers):
+            x = ops.rms_norm(h, self.final_norm, self.cfg.norm_eps)
+        return x
+
+    def forward(self, ids: torch.Tensor, labels: torch.Tensor | None = None, ignore_index: int = -100):
+        """Training/eval forward.  With labels: mean token CE (fused head+CE).
+        Without: logits [B, S, V] (bf16)."""
+        B, S = ids.shape
+        x = self.hidden_states(ids)
+        if labels is not None:
+            return ops.linear_cross_entropy(x, self.head_weight, labels.reshape(-1), ignore_index)
+        return torch.matmul(x, self.head_weight.t()).view(B, S, -1)
+
+    # ------------------------------------------------------------------ utilities
+    def trainable_parameters(self):
+        return [p for p in self.parameters() if p.requires_grad]
+
+    def named_trainable_parameters(self):
+        return [(n, p) for n, p in self.named_parameters() if p.requires_grad]
+
+    def num_params(self, trainable_only: bool = False) -> int:
+        return sum(p.numel() for p in (self.trainable_parameters() if trainable_only else self.parameters()))

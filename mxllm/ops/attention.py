@@ -1,0 +1,59 @@
+"""Fused attention block: QKV split + Llama-3 RoPE + causal GQA flash attention.
+
+SURVEY §2.4 K6 + K7 (+K13 prefill).  The whole ``qkv -> o`` segment is ONE
+autograd node so the backward can hand the attention kernel's f32 dQ and
+per-q-head dK/dV partials straight to the inverse-RoPE merge kernel, which
+writes d(qkv) in the projection's token-major layout — no intermediate
+re-layout tensors and no autograd shape constraints between them.
+
+GPU path (csrc/kernels/rope.hip, attn_fwd.hip, attn_bwd.hip):
+  forward : qkv [T,(Hq+2Hkv)D] --rope_split--> q [B,Hq,S,D], k,v [B,Hkv,S,D]
+            --attn_fwd (MFMA 32x32x16 bf16)--> o [B,S,Hq*D] token-major, lse [B,Hq,S]
+  backward: attn_bwd -> dq f32 [B,Hq,S,D] (f32 atomics), dk/dv partials
+            [B,Hq,S,D] f32 --rope_merge_bwd--> d(qkv) bf16 [T,(Hq+2Hkv)D]
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import reference as ref
+from ._ext import native, use_native
+
+
+def split_heads_ref(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, D: int):
+    x = qkv.view(B, S, Hq + 2 * Hkv, D)
+    return x[:, :, :Hq], x[:, :, Hq:Hq + Hkv], x[:, :, Hq + Hkv:]
+
+
+class _AttnBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal):
+        ops = native()
+        q, k, v = ops.rope_split(qkv, cos, sin, B, S, Hq, Hkv, D)
+        o, lse = ops.attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D))
+        ctx.save_for_backward(q, k, v, o, lse, cos, sin)
+        ctx.dims = (B, S, Hq, Hkv, D, causal)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        B, S, Hq, Hkv, D, causal = ctx.dims
+        ops = native()
+        dq, dkp, dvp = ops.attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D))
+        dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D)
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+def attention_block(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, S: int, Hq: int,
+                    Hkv: int, D: int, causal: bool = True) -> torch.Tensor:
+    """qkv [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE at positions 0..S-1)."""
+    if use_native(qkv):
+        return _AttnBlockFn.apply(qkv.contiguous(), cos, sin, B, S, Hq, Hkv, D, causal)
+    q, k, v = split_heads_ref(qkv, B, S, Hq, Hkv, D)
+    q = ref.apply_rope(q, cos, sin)
+    k = ref.apply_rope(k, cos, sin)
+    o = ref.attention(q, k, v, causal=causal)
+    return o.reshape(B * S, Hq * D)

@@ -1,0 +1,60 @@
+"""RMSNorm (and residual-add + RMSNorm) with HIP forward/backward kernels.
+
+SURVEY §2.4 K5.  On GPU both directions run ``csrc/kernels/rmsnorm.hip``;
+the residual add of a transformer sub-block is fused into the norm that follows
+it (forward) and the residual-gradient add into the norm's backward, which
+removes a full read+write of the [T, H] residual stream per sub-block.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._ext import native, use_native
+
+
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        y, rstd, _ = native().rmsnorm_fwd(x, None, w, eps)
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = native().rmsnorm_bwd(dy.contiguous(), x, w, rstd, None, ctx.needs_input_grad[1])
+        return dx, (dw.to(w.dtype) if ctx.needs_input_grad[1] else None), None
+
+
+class _AddRMSNormFn(torch.autograd.Function):
+    """(x, res, w) -> (y = rmsnorm(x + res) * w, h = x + res)."""
+
+    @staticmethod
+    def forward(ctx, x, res, w, eps):
+        y, rstd, h = native().rmsnorm_fwd(x, res, w, eps)
+        ctx.save_for_backward(h, w, rstd)
+        return y, h
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        h, w, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(h)
+        dres = dh.contiguous() if dh is not None else None
+        dx, dw = native().rmsnorm_bwd(dy.contiguous(), h, w, rstd, dres, ctx.needs_input_grad[2])
+        return dx, dx, (dw.to(w.dtype) if ctx.needs_input_grad[2] else None), None
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    if use_native(x):
+        return _RMSNormFn.apply(x.contiguous(), w, eps)
+    return ref.rms_norm(x, w, eps)
+
+
+def add_rms_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5):
+    """Returns (normed, new_residual) where new_residual = x + res."""
+    if use_native(x):
+        return _AddRMSNormFn.apply(x.contiguous(), res.contiguous(), w, eps)
+    h = x + res
+    return ref.rms_norm(h, w, eps), h
