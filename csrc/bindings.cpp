@@ -133,6 +133,178 @@ at::Tensor sqnorm_f32(const at::Tensor& x) {
   return out;
 }
 
+// ---------------------------------------------------------------- SwiGLU
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  check_bf16(gu, "gu");
+  DevGuard g(gu.device());
+  const int64_t F2 = gu.size(-1);
+  MX_CHECK(F2 % 16 == 0, "2F must be a multiple of 16");
+  const int64_t T = gu.numel() / F2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto m = at::empty(sizes, gu.options());
+  if (T > 0) MX_OK(mx_swiglu_fwd(bf(gu), bfm(m), T, (int)(F2 / 2), cur_stream()));
+  return m;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu) {
+  check_bf16(dm, "dm");
+  check_bf16(gu, "gu");
+  DevGuard g(gu.device());
+  const int64_t F2 = gu.size(-1);
+  const int64_t T = gu.numel() / F2;
+  MX_CHECK(dm.numel() == T * (F2 / 2), "dm shape mismatch");
+  auto dgu = at::empty_like(gu);
+  if (T > 0) MX_OK(mx_swiglu_bwd(bf(dm), bf(gu), bfm(dgu), T, (int)(F2 / 2), cur_stream()));
+  return dgu;
+}
+
+// ---------------------------------------------------------------- AdamW
+void adamw_step(at::Tensor master, const at::Tensor& grad, at::Tensor m, at::Tensor v,
+                const c10::optional<at::Tensor>& lowp, double lr, double b1, double b2, double eps, double wd,
+                double bc1, double bc2, const c10::optional<at::Tensor>& scale_t, double scale_f) {
+  check_f32(master, "master");
+  check_f32(m, "m");
+  check_f32(v, "v");
+  MX_CHECK(grad.is_cuda() && grad.is_contiguous(), "grad must be contiguous GPU");
+  MX_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16, "grad f32/bf16");
+  const int64_t n = master.numel();
+  MX_CHECK(grad.numel() == n && m.numel() == n && v.numel() == n, "adamw size mismatch");
+  DevGuard g(master.device());
+  uint16_t* lp = nullptr;
+  if (lowp.has_value()) {
+    check_bf16(*lowp, "lowp");
+    MX_CHECK(lowp->numel() == n, "lowp size");
+    lp = reinterpret_cast<uint16_t*>(lowp->data_ptr());
+  }
+  const float* st = nullptr;
+  if (scale_t.has_value()) {
+    check_f32(*scale_t, "scale_t");
+    st = scale_t->data_ptr<float>();
+  }
+  MX_OK(mx_adamw(master.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kBFloat16 ? 1 : 0,
+                 m.data_ptr<float>(), v.data_ptr<float>(), lp, n, (float)lr, (float)b1, (float)b2, (float)eps,
+                 (float)wd, (float)bc1, (float)bc2, st, (float)scale_f, cur_stream()));
+}
+
+// ---------------------------------------------------------------- embedding
+at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& w) {
+  check_bf16(w, "weight");
+  MX_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong, "ids must be int64 GPU");
+  DevGuard g(w.device());
+  auto idc = ids.contiguous();
+  const int64_t T = idc.numel(), H = w.size(1), V = w.size(0);
+  auto out = at::empty({T, H}, w.options());
+  MX_OK(mx_embedding_fwd(idc.data_ptr<int64_t>(), bf(w), bfm(out), T, (int)H, V, cur_stream()));
+  return out;
+}
+
+at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V) {
+  check_bf16(dy, "dy");
+  DevGuard g(dy.device());
+  auto idc = ids.contiguous();
+  const int64_t H = dy.size(-1), T = idc.numel();
+  auto dw = at::zeros({V, H}, dy.options().dtype(at::kFloat));
+  MX_OK(mx_embedding_bwd(idc.data_ptr<int64_t>(), bf(dy), dw.data_ptr<float>(), T, (int)H, V, cur_stream()));
+  return dw;
+}
+
+// ---------------------------------------------------------------- cross-entropy
+// logits [T, V] bf16 is overwritten in place with d(mean loss)/d(logits).
+std::tuple<at::Tensor, at::Tensor> ce_fwd_bwd(at::Tensor logits, const at::Tensor& labels, int64_t ignore) {
+  check_bf16(logits, "logits");
+  MX_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong, "labels must be int64 GPU");
+  DevGuard g(logits.device());
+  const int64_t V = logits.size(-1), T = logits.numel() / V;
+  MX_CHECK(labels.numel() == T, "labels size mismatch");
+  auto lab = labels.contiguous();
+  auto losses = at::empty({T}, logits.options().dtype(at::kFloat));
+  auto ws = at::empty({2}, logits.options().dtype(at::kFloat));
+  auto loss = at::empty({}, logits.options().dtype(at::kFloat));
+  MX_OK(mx_ce_fwd_bwd(bfm(logits), lab.data_ptr<int64_t>(), losses.data_ptr<float>(), ws.data_ptr<float>(),
+                      loss.data_ptr<float>(), T, (int)V, ignore, cur_stream()));
+  return {loss, losses};
+}
+
+// ---------------------------------------------------------------- RoPE split / merge
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_split(const at::Tensor& qkv, const at::Tensor& cos,
+                                                          const at::Tensor& sin, int64_t B, int64_t S, int64_t Hq,
+                                                          int64_t Hkv, int64_t D,
+                                                          const c10::optional<at::Tensor>& positions) {
+  check_bf16(qkv, "qkv");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  MX_CHECK(qkv.numel() == B * S * (Hq + 2 * Hkv) * D, "qkv shape mismatch");
+  MX_CHECK(cos.size(-1) == D / 2, "rope table width");
+  DevGuard g(qkv.device());
+  const int32_t* pos = nullptr;
+  if (positions.has_value()) {
+    MX_CHECK(positions->scalar_type() == at::kInt && positions->numel() == B * S, "positions int32 [B*S]");
+    pos = positions->data_ptr<int32_t>();
+  } else {
+    MX_CHECK(cos.size(0) >= S, "rope table too short");
+  }
+  auto q = at::empty({B, Hq, S, D}, qkv.options());
+  auto k = at::empty({B, Hkv, S, D}, qkv.options());
+  auto v = at::empty({B, Hkv, S, D}, qkv.options());
+  MX_OK(mx_rope_split(bf(qkv), cos.data_ptr<float>(), sin.data_ptr<float>(), pos, bfm(q), bfm(k), bfm(v), (int)B,
+                      (int)S, (int)Hq, (int)Hkv, (int)D, cur_stream()));
+  return {q, k, v};
+}
+
+at::Tensor rope_merge_bwd(const at::Tensor& dq, const at::Tensor& dkp, const at::Tensor& dvp, const at::Tensor& cos,
+                          const at::Tensor& sin, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D) {
+  check_f32(dq, "dq");
+  check_f32(dkp, "dkp");
+  check_f32(dvp, "dvp");
+  DevGuard g(dq.device());
+  const int64_t kvin = dkp.size(1);
+  MX_CHECK(dkp.dim() == 4 && dkp.size(0) == B && dkp.size(2) == S && dkp.size(3) == D, "dk partial shape");
+  auto dqkv = at::empty({B * S, (Hq + 2 * Hkv) * D}, dq.options().dtype(at::kBFloat16));
+  MX_OK(mx_rope_merge_bwd(dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), cos.data_ptr<float>(),
+                          sin.data_ptr<float>(), bfm(dqkv), (int)B, (int)S, (int)Hq, (int)Hkv, (int)kvin, (int)D,
+                          cur_stream()));
+  return dqkv;
+}
+
+// ---------------------------------------------------------------- attention
+std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                            bool causal, double scale) {
+  check_bf16(q, "q");
+  check_bf16(k, "k");
+  check_bf16(v, "v");
+  MX_CHECK(q.dim() == 4 && k.dim() == 4 && v.sizes() == k.sizes(), "q [B,Hq,S,D], k/v [B,Hkv,Sk,D]");
+  const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
+  const int64_t Hkv = k.size(1), Sk = k.size(2);
+  MX_CHECK(k.size(0) == B && k.size(3) == D && Hq % Hkv == 0, "attention shape mismatch");
+  DevGuard g(q.device());
+  auto o = at::empty({B, S, Hq * D}, q.options());
+  auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  MX_OK(mx_attn_fwd(bf(q), bf(k), bf(v), bfm(o), lse.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv, (int)S, (int)Sk,
+                    (int)D, causal ? 1 : 0, (float)scale, cur_stream()));
+  return {o, lse};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q,
+                                                        const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+                                                        const at::Tensor& lse, bool causal, double scale) {
+  check_bf16(dout, "dout");
+  check_bf16(o, "o");
+  check_f32(lse, "lse");
+  const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
+  const int64_t Hkv = k.size(1), Sk = k.size(2);
+  MX_CHECK(dout.numel() == B * S * Hq * D && o.numel() == dout.numel(), "dout/o shape");
+  DevGuard g(q.device());
+  auto dq = at::zeros({B, Hq, S, D}, q.options().dtype(at::kFloat));
+  auto dkp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
+  auto dvp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
+  auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                    dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
+                    (int)S, (int)Sk, (int)D, causal ? 1 : 0, (float)scale, cur_stream()));
+  return {dq, dkp, dvp};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(mxllm, m) {
@@ -140,6 +312,16 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw) -> (Tensor, Tensor)");
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
   m.def("sqnorm_f32(Tensor x) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor dm, Tensor gu) -> Tensor");
+  m.def("adamw_step(Tensor(a!) master, Tensor grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f) -> ()");
+  m.def("embedding_fwd(Tensor ids, Tensor w) -> Tensor");
+  m.def("embedding_bwd(Tensor dy, Tensor ids, int V) -> Tensor");
+  m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
+  m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
+  m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D) -> Tensor");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
@@ -147,4 +329,14 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("segmented_mean", &segmented_mean);
   m.impl("sqnorm_f32", &sqnorm_f32);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("adamw_step", &adamw_step);
+  m.impl("embedding_fwd", &embedding_fwd);
+  m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("ce_fwd_bwd", &ce_fwd_bwd);
+  m.impl("rope_split", &rope_split);
+  m.impl("rope_merge_bwd", &rope_merge_bwd);
+  m.impl("attn_fwd", &attn_fwd);
+  m.impl("attn_bwd", &attn_bwd);
 }

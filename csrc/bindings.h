@@ -18,3 +18,30 @@ int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, float* out,
                           hipStream_t stream);
 int mx_sqnorm_f32(const float* x, int64_t n, float* out, hipStream_t stream);
 }
+
+extern "C" {
+// elementwise.hip
+int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, hipStream_t stream);
+int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, hipStream_t stream);
+int mx_adamw(float* p, const void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
+             float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t, float scale_f,
+             hipStream_t stream);
+int mx_embedding_fwd(const int64_t* ids, const uint16_t* w, uint16_t* out, int64_t T, int H, int64_t V,
+                     hipStream_t stream);
+int mx_embedding_bwd(const int64_t* ids, const uint16_t* dy, float* dw, int64_t T, int H, int64_t V,
+                     hipStream_t stream);
+// cross_entropy.hip
+int mx_ce_fwd_bwd(uint16_t* logits, const int64_t* labels, float* losses, float* inv_n, float* loss_out, int64_t T,
+                  int V, int64_t ignore, hipStream_t stream);
+// rope.hip
+int mx_rope_split(const uint16_t* qkv, const float* cosb, const float* sinb, const int32_t* positions, uint16_t* q,
+                  uint16_t* k, uint16_t* v, int B, int S, int Hq, int Hkv, int D, hipStream_t stream);
+int mx_rope_merge_bwd(const float* dq, const float* dkp, const float* dvp, const float* cosb, const float* sinb,
+                      uint16_t* dqkv, int B, int S, int Hq, int Hkv, int kv_heads_in, int D, hipStream_t stream);
+// attn_fwd.hip / attn_bwd.hip
+int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B, int Hq,
+                int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream);
+int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o, const uint16_t* dout,
+                const float* lse, float* delta, float* dq, float* dkp, float* dvp, int B, int Hq, int Hkv, int S,
+                int Sk, int D, int causal, float scale, hipStream_t stream);
+}

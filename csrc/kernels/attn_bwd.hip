@@ -1,0 +1,305 @@
+// Causal GQA flash-attention backward for gfx950 (SURVEY §2.4 K7 bwd).
+//
+// Recompute-P formulation (guide App. B "Attention backward"): per tile
+//   S = Q K^T, P = exp2(S*sl - lse2), dP = dO V^T, dS = P (dP - delta),
+//   dV^T += dO^T P, dK^T += Q^T dS, dQ += dS K   (x softmax scale for dQ, dK)
+//
+// Decomposition (sized for small-batch fine-tuning shapes, e.g. B=2, Hq=64,
+// S=2048 -> 2048 workgroups instead of the 128 a per-KV-head split would give):
+//  * workgroup = 4 waves = 128 keys of ONE q-head (32 keys per wave, key on the
+//    MFMA lane); it sweeps all q tiles (64 rows) that can see its keys;
+//  * K and V fragments of the wave's keys stay in registers (B operands of S
+//    and dP); S/dP accumulators, converted to bf16, are directly the B
+//    operands of dV^T and dK^T (no LDS round trip); dO^T / Q^T fragments via
+//    ds_read_b64_tr_b16 from the same swizzled tile images used for row reads;
+//  * dS crosses LDS once ([key][q] image), the workgroup then computes its
+//    64 x D dQ contribution over all 128 keys with MFMA and adds it to an f32
+//    dQ with no-return atomics (256-B row segments per wave instruction);
+//    128 keys per workgroup -> 320 FLOP per atomic byte;
+//  * dK/dV are per-q-head partials [B,Hq,Sk,D] f32; the GQA group sum is
+//    fused into the inverse-RoPE merge kernel (rope.hip), so no atomics and a
+//    deterministic dK/dV;
+//  * heaviest key blocks (most visible q tiles) scheduled first.
+#include "common.h"
+
+namespace mx {
+
+typedef __bf16 bf16x8_b __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4_b;
+
+__device__ __forceinline__ f32x16 mfma32b(const u16x8& a, const u16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_b, a), __builtin_bit_cast(bf16x8_b, b),
+                                                 c, 0, 0, 0);
+}
+__device__ __forceinline__ u16x4 trd(const char* p) {
+  return __builtin_bit_cast(u16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_b*)(p)));
+}
+template <int CH>
+__device__ __forceinline__ int swzb(int row) {
+  return (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
+}
+
+// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]   (token-major inputs)
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dO,
+                                                             const uint16_t* __restrict__ O,
+                                                             float* __restrict__ delta, int B, int S, int Hq,
+                                                             int D) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*S*Hq (token-major order)
+  const int lane = threadIdx.x & 63;
+  if (row >= (int64_t)B * S * Hq) return;
+  const uint16_t* a = dO + row * D;
+  const uint16_t* c = O + row * D;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += bf2f(a[d]) * bf2f(c[d]);
+  s = wave_sum(s);
+  if (lane == 0) {
+    const int h = (int)(row % Hq);
+    const int64_t t = row / Hq;
+    const int b = (int)(t / S), q = (int)(t % S);
+    delta[((int64_t)b * Hq + h) * S + q] = s;
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                float* __restrict__ dQ, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq, int Hkv,
+                int S, int Sk, int off, float sl, float scale) {
+  constexpr int BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int KIMG = BN * ROWB;           // K image [128][D]
+  constexpr int QT = BQ * ROWB;             // Q tile / dO tile [64][D]
+  constexpr int DSROWB = BQ * 2;            // dS image row: 64 q bf16 = 128 B
+  constexpr int DSIMG = BN * DSROWB;        // [128 keys][64 q]
+  constexpr int LPT_Q = BQ * CH / 256;      // 16-B chunks per thread per tile
+  constexpr int LPT_K = BN * CH / 256;
+  __shared__ __attribute__((aligned(16))) char smem[KIMG + 2 * QT + DSIMG + 2 * BQ * 4];
+  char* kimg = smem;
+  char* qt = smem + KIMG;
+  char* dot = qt + QT;
+  char* dsi = dot + QT;
+  float* lse_s = reinterpret_cast<float*>(dsi + DSIMG);
+  float* del_s = lse_s + BQ;
+
+  const int nkb = (Sk + BN - 1) / BN;
+  const int BH = B * Hq;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = bid / BH;  // ascending: key block 0 sees the most q tiles (causal) -> heaviest first
+  const int bh = bid % BH;
+  if (kb >= nkb) return;
+  const int b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
+  const uint16_t* Qp = Q + (size_t)(b * Hq + h) * S * D;
+  const uint16_t* Kp = K + (size_t)(b * Hkv + hk) * Sk * D;
+  const uint16_t* Vp = V + (size_t)(b * Hkv + hk) * Sk * D;
+  const size_t dstride = (size_t)Hq * D;  // token-major row stride of dO
+  const uint16_t* dOp = dO + (size_t)b * S * dstride + (size_t)h * D;
+  const float* lsep = LSE + (size_t)(b * Hq + h) * S;
+  const float* delp = DELTA + (size_t)(b * Hq + h) * S;
+  float* dQp = dQ + (size_t)(b * Hq + h) * S * D;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int k0 = kb * BN;
+  const int key = k0 + 32 * w + r;  // this lane's key
+
+  // K image (whole WG) + per-wave K/V fragments
+#pragma unroll
+  for (int i = 0; i < LPT_K; ++i) {
+    const int c = tid + 256 * i, row = c / CH, ch = c % CH, kk = k0 + row;
+    u16x8 val = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (kk < Sk) val = *reinterpret_cast<const u16x8*>(Kp + (size_t)kk * D + ch * 8);
+    *reinterpret_cast<u16x8*>(kimg + row * ROWB + 16 * (ch ^ swzb<CH>(row))) = val;
+  }
+  u16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (key < Sk) {
+      kf[s] = *reinterpret_cast<const u16x8*>(Kp + (size_t)key * D + 16 * s + 8 * hh);
+      vf[s] = *reinterpret_cast<const u16x8*>(Vp + (size_t)key * D + 16 * s + 8 * hh);
+    } else {
+      kf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { dk[d][j] = 0.f; dv[d][j] = 0.f; }
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, (k0 - off) / BQ * BQ);
+  const int nqt = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
+
+  u16x8 qst[LPT_Q], dost[LPT_Q];
+  float lse_r = 0.f, del_r = 0.f;
+  auto gload = [&](int it) {
+    const int q0 = qstart + it * BQ;
+#pragma unroll
+    for (int i = 0; i < LPT_Q; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH, q = q0 + row;
+      if (q < S) {
+        qst[i] = *reinterpret_cast<const u16x8*>(Qp + (size_t)q * D + ch * 8);
+        dost[i] = *reinterpret_cast<const u16x8*>(dOp + (size_t)q * dstride + ch * 8);
+      } else {
+        qst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        dost[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+    if (tid < BQ) {
+      const int q = q0 + tid;
+      lse_r = q < S ? lsep[q] : INFINITY;
+      del_r = q < S ? delp[q] : 0.f;
+    }
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < LPT_Q; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int o = row * ROWB + 16 * (ch ^ swzb<CH>(row));
+      *reinterpret_cast<u16x8*>(qt + o) = qst[i];
+      *reinterpret_cast<u16x8*>(dot + o) = dost[i];
+    }
+    if (tid < BQ) { lse_s[tid] = lse_r; del_s[tid] = del_r; }
+  };
+
+  if (nqt > 0) gload(0);
+  for (int it = 0; it < nqt; ++it) {
+    const int q0 = qstart + it * BQ;
+    swrite();
+    __syncthreads();  // tiles visible; previous iteration's dS image fully consumed
+    if (it + 1 < nqt) gload(it + 1);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      f32x16 sa, dp;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) { sa[j] = 0.f; dp[j] = 0.f; }
+      const int qr = 32 * m + r;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int o = qr * ROWB + 16 * ((2 * s + hh) ^ swzb<CH>(qr));
+        sa = mfma32b(*reinterpret_cast<const u16x8*>(qt + o), kf[s], sa);
+        dp = mfma32b(*reinterpret_cast<const u16x8*>(dot + o), vf[s], dp);
+      }
+      // rows of sa/dp: q = q0 + 32m + (j&3) + 8(j>>2) + 4hh ; column = key (lane)
+      f32x4 lv[4], dl[4];
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        lv[gq] = *reinterpret_cast<const f32x4*>(lse_s + 32 * m + 8 * gq + 4 * hh);
+        dl[gq] = *reinterpret_cast<const f32x4*>(del_s + 32 * m + 8 * gq + 4 * hh);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        float p = __builtin_amdgcn_exp2f(sa[j] * sl - lv[j >> 2][j & 3]);
+        if (key >= Sk || (CAUSAL && key > q + off)) p = 0.f;
+        sa[j] = p;
+        dp[j] = p * (dp[j] - dl[j >> 2][j & 3]);  // dS
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS   (k index = q rows of this m-subtile)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u16x8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = f2bf(sa[8 * s2 + j]);
+          sb[j] = f2bf(dp[8 * s2 + j]);
+        }
+        const int rb = 32 * m + 16 * s2 + 4 * hh;
+        const int rowA = rb + tq, rowB = rb + 8 + tq;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+          const int oA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
+          const int oB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
+          const u16x4 a0 = trd(dot + oA), a1 = trd(dot + oB);
+          dv[db] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]}, pb, dv[db]);
+          const u16x4 b0 = trd(qt + oA), b1 = trd(qt + oB);
+          dk[db] = mfma32b(u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, sb, dk[db]);
+        }
+      }
+      // dS -> LDS image [key][q] (bf16): 4 consecutive q per 8-byte write
+      const int krow = 32 * w + r;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int q = 32 * m + 8 * gq + 4 * hh;  // local q, multiple of 4
+        const int chunk = q >> 3;
+        u16x4 v4 = u16x4{f2bf(dp[4 * gq]), f2bf(dp[4 * gq + 1]), f2bf(dp[4 * gq + 2]), f2bf(dp[4 * gq + 3])};
+        *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swzb<8>(krow)) + 8 * hh) = v4;
+      }
+    }
+    __syncthreads();  // dS image complete
+    // dQ[q0 .. q0+63][:] += scale * dS[64 x 128] . K[128 x D]
+    for (int tile = w; tile < 2 * DB; tile += 4) {
+      const int m = tile / DB, db = tile % DB;
+      f32x16 acc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int s = 0; s < BN / 16; ++s) {
+        const int kbse = 16 * s + 4 * hh;
+        const int rA = kbse + tq, rB = kbse + 8 + tq;
+        // A = dS[q][key]: rows of the [key][q] image, columns q = 32m + 16(g&1) + ...
+        const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
+        const u16x4 a0 = trd(dsi + rA * DSROWB + 16 * (qchunk ^ swzb<8>(rA)) + 8 * (tp & 1));
+        const u16x4 a1 = trd(dsi + rB * DSROWB + 16 * (qchunk ^ swzb<8>(rB)) + 8 * (tp & 1));
+        // B = K[key][d]
+        const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+        const u16x4 b0 = trd(kimg + rA * ROWB + 16 * (dchunk ^ swzb<CH>(rA)) + 8 * (tp & 1));
+        const u16x4 b1 = trd(kimg + rB * ROWB + 16 * (dchunk ^ swzb<CH>(rB)) + 8 * (tp & 1));
+        acc = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]},
+                      u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc);
+      }
+      // C: col = d (lane r), row = q
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (q < S) atomicAdd(dQp + (size_t)q * D + db * 32 + r, acc[j] * scale);
+      }
+    }
+  }
+  // write per-q-head dK/dV partials: C rows = d, col = key (lane)
+  if (key < Sk) {
+    float* dkq = dKp + ((size_t)(b * Hq + h) * Sk + key) * D;
+    float* dvq = dVp + ((size_t)(b * Hq + h) * Sk + key) * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d = db * 32 + 8 * gq + 4 * hh;
+        *reinterpret_cast<f32x4*>(dkq + d) =
+            f32x4{dk[db][4 * gq] * scale, dk[db][4 * gq + 1] * scale, dk[db][4 * gq + 2] * scale,
+                  dk[db][4 * gq + 3] * scale};
+        *reinterpret_cast<f32x4*>(dvq + d) = f32x4{dv[db][4 * gq], dv[db][4 * gq + 1], dv[db][4 * gq + 2],
+                                                  dv[db][4 * gq + 3]};
+      }
+  }
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+// dq must be ZEROED by the caller (f32 atomics).  delta: workspace [B,Hq,S].
+extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
+                           const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
+                           int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || Sk <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv) return -1;
+  const int64_t rows = (int64_t)B * S * Hq;
+  attn_bwd_delta_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(dout, o, delta, B, S, Hq, D);
+  const int nkb = (Sk + 127) / 128;
+  const int grid = nkb * B * Hq;
+  const float sl = scale * 1.4426950408889634f;
+  const int off = Sk - S;
+#define BWD(DD, C)                                                                                          \
+  attn_bwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv, S, Sk, \
+                                                   off, sl, scale)
+  if (D == 128) { if (causal) BWD(128, true); else BWD(128, false); }
+  else if (D == 64) { if (causal) BWD(64, true); else BWD(64, false); }
+  else if (D == 32) { if (causal) BWD(32, true); else BWD(32, false); }
+  else return -1;
+#undef BWD
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,232 @@
+// Causal GQA flash-attention forward for gfx950 (SURVEY §2.4 K7 fwd, K13).
+//
+// Layouts: q [B,Hq,S,D], k/v [B,Hkv,Sk,D] bf16 head-major (written by
+// rope_split), o token-major [B,S,Hq,D] (feeds the Wo GEMM directly),
+// lse [B,Hq,S] f32 in the log2 domain of the scaled scores.
+//
+// Structure (CDNA HIP guide App. B "Fused attention prefill"):
+//  * workgroup = 4 waves = 128 query rows (32 per wave), KV tile = 64 keys;
+//  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_32x32x16_bf16, so each lane
+//    owns one query column and the tile's keys sit in its 16+16 accumulator
+//    registers -> row max / row sum are in-register (+1 cross-half shuffle);
+//  * the f32 S^T accumulator, converted pairwise to bf16, IS the B operand of
+//    O^T += V^T . P^T (guide §3 "accumulator tile as the next MFMA's operand");
+//  * V^T fragments come from the row-major V tile via ds_read_b64_tr_b16 (T10);
+//  * K/V tiles live in LDS as 16-B-chunk XOR-swizzled images
+//    (chunk ^ ((row&3)<<2 | (row>>2)&3)): conflict-free for both the
+//    ds_read_b128 row reads of K and the transposed reads of V;
+//  * register-staged double buffer with the async-STAGE split (T14): tile t+1's
+//    global loads issue before tile t's MFMAs, the LDS write lands after them;
+//  * causal blocks scheduled heaviest-first, XCD-aware block remap so the
+//    q-heads sharing one KV head run on the same XCD (shared L2).
+#include "common.h"
+
+namespace mx {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int CH>
+__device__ __forceinline__ int swz(int row) {
+  return (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
+}
+
+__device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                 c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ds_read_b64_tr_b16: generic -> LDS address-space cast of a __shared__ pointer
+__device__ __forceinline__ u16x4 tr_read(const char* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(u16x4, v);
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2)
+attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
+                int causal_off, float sl) {
+  constexpr int BM = 128, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int TILE = BN * ROWB;
+  constexpr int LPT = BN * CH / 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int nqb = (S + BM - 1) / BM;
+  const int BH = B * Hq;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = nqb - 1 - bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / Hq, h = bh % Hq;
+  const int hk = h / (Hq / Hkv);
+  const uint16_t* Qp = Q + ((size_t)(b * Hq + h) * S) * D;
+  const uint16_t* Kp = K + ((size_t)(b * Hkv + hk) * Sk) * D;
+  const uint16_t* Vp = V + ((size_t)(b * Hkv + hk) * Sk) * D;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = qb * BM;
+  const int qrow = q0 + 32 * w + r;
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (qrow < S) qf[s] = *reinterpret_cast<const u16x8*>(Qp + (size_t)qrow * D + 16 * s + 8 * hh);
+    else qf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM + causal_off);
+  const int ntiles = kend > 0 ? (kend + BN - 1) / BN : 0;
+
+  u16x8 kst[LPT], vst[LPT];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH, key = kt * BN + row;
+      if (key < Sk) {
+        kst[i] = *reinterpret_cast<const u16x8*>(Kp + (size_t)key * D + ch * 8);
+        vst[i] = *reinterpret_cast<const u16x8*>(Vp + (size_t)key * D + ch * 8);
+      } else {
+        kst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        vst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* kb = smem + buf * 2 * TILE;
+    char* vb = kb + TILE;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int off = row * ROWB + 16 * (ch ^ swz<CH>(row));
+      *reinterpret_cast<u16x8*>(kb + off) = kst[i];
+      *reinterpret_cast<u16x8*>(vb + off) = vst[i];
+    }
+  };
+
+  f32x16 o[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[d][j] = 0.f;
+  float m_i = -1e30f, l_i = 0.f;
+
+  // per-lane constants for the transposed V reads
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+
+  if (ntiles > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  const int wq_hi = q0 + 32 * w + 31;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) gload(kt + 1);
+    const char* kb = smem + cur * 2 * TILE;
+    const char* vb = kb + TILE;
+    const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
+    if (active) {
+      f32x16 sacc[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sacc[n][j] = 0.f;
+        const int krow = n * 32 + r;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const u16x8 a = *reinterpret_cast<const u16x8*>(kb + krow * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(krow)));
+          sacc[n] = mfma32(a, qf[s], sacc[n]);
+        }
+      }
+      float mx = -INFINITY;
+      const bool need_mask = (kt * BN + BN > Sk) || (CAUSAL && (kt * BN + BN - 1 > q0 + 32 * w + causal_off));
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          float x = sacc[n][j] * sl;
+          if (need_mask) {
+            const int key = kt * BN + n * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+            if (key >= Sk || (CAUSAL && key > qrow + causal_off)) x = -INFINITY;
+          }
+          sacc[n][j] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m_i, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_i - mnew);
+      float ls = 0.f;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float p = __builtin_amdgcn_exp2f(sacc[n][j] - mnew);
+          sacc[n][j] = p;
+          ls += p;
+        }
+      l_i = l_i * alpha + ls;
+      m_i = mnew;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) o[d] *= alpha;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          u16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[n][8 * s2 + j]);
+          const int keyb = n * 32 + 16 * s2 + 4 * hh;
+          const int rowA = keyb + tq, rowB = keyb + 8 + tq;
+#pragma unroll
+          for (int db = 0; db < DB; ++db) {
+            const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+            const u16x4 va = tr_read(vb + rowA * ROWB + 16 * (chunk ^ swz<CH>(rowA)) + 8 * (tp & 1));
+            const u16x4 vc = tr_read(vb + rowB * ROWB + 16 * (chunk ^ swz<CH>(rowB)) + 8 * (tp & 1));
+            const u16x8 a = u16x8{va[0], va[1], va[2], va[3], vc[0], vc[1], vc[2], vc[3]};
+            o[db] = mfma32(a, pb, o[db]);
+          }
+        }
+    }
+    if (kt + 1 < ntiles) swrite((kt + 1) & 1);
+    __syncthreads();
+  }
+  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qrow < S) {
+    uint16_t* op = O + ((size_t)b * S + qrow) * (size_t)(Hq * D) + (size_t)h * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d = db * 32 + 8 * gq + 4 * hh;
+        u16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(o[db][4 * gq + j] * inv);
+        *reinterpret_cast<u16x4*>(op + d) = v4;
+      }
+    if (hh == 0) LSE[(size_t)(b * Hq + h) * S + qrow] = m_i + __log2f(l_tot);
+  }
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B,
+                           int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv) return -1;
+  const int nqb = (S + 127) / 128;
+  const int grid = nqb * B * Hq;
+  const float sl = scale * 1.4426950408889634f;
+  const int off = Sk - S;
+#define FWD(DD, C) attn_fwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl)
+  if (D == 128) { if (causal) FWD(128, true); else FWD(128, false); }
+  else if (D == 64) { if (causal) FWD(64, true); else FWD(64, false); }
+  else if (D == 32) { if (causal) FWD(32, true); else FWD(32, false); }
+  else return -1;
+#undef FWD
+  return (int)hipGetLastError();
+}

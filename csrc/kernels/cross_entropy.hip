@@ -1,0 +1,114 @@
+// Fused softmax cross-entropy forward + backward, in place.
+//
+// logits [T, V] bf16 (V = 128,256 for Llama-3) are produced by one hipBLASLt
+// GEMM.  One 256-thread workgroup per row:
+//   pass 1: 16-B vector loads, per-lane online (max, sum) in the log2 domain
+//           (one rescale per 8 elements), wave-shuffle + LDS combine -> lse;
+//   pass 2: re-read the row (served from the Infinity Cache: rows in flight
+//           x 256 KB << 256 MiB) and overwrite it with
+//           (softmax - onehot(label)) / n_valid  in bf16.
+// Rows whose label == ignore_index get loss 0 and a zero gradient row.
+// n_valid is counted on device first (no host sync anywhere).
+#include "common.h"
+
+namespace mx {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__global__ void __launch_bounds__(256) count_valid_kernel(const int64_t* __restrict__ labels, int64_t T,
+                                                          int64_t ignore, float* __restrict__ inv_n) {
+  __shared__ float scratch[16];
+  float c = 0.f;
+  for (int64_t i = threadIdx.x; i < T; i += 256) c += (labels[i] != ignore) ? 1.f : 0.f;
+  c = block_sum(c, scratch);
+  if (threadIdx.x == 0) inv_n[0] = c > 0.f ? 1.f / c : 0.f;
+}
+
+__global__ void __launch_bounds__(256) ce_fwd_bwd_kernel(uint16_t* __restrict__ logits,
+                                                         const int64_t* __restrict__ labels,
+                                                         float* __restrict__ losses,
+                                                         const float* __restrict__ inv_n_p, int V,
+                                                         int64_t ignore) {
+  __shared__ float sm[16], ss[16];
+  const int64_t row = blockIdx.x;
+  uint16_t* x = logits + row * (int64_t)V;
+  const int64_t lab = labels[row];
+  const float inv_n = inv_n_p[0];
+  if (lab == ignore || lab < 0 || lab >= V) {
+    const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = threadIdx.x * 8; c < V; c += 256 * 8) *reinterpret_cast<u16x8*>(x + c) = z;
+    if (threadIdx.x == 0) losses[row] = 0.f;
+    return;
+  }
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    u16x8 a = *reinterpret_cast<const u16x8*>(x + c);
+    float v[8];
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = bf2f(a[j]) * kLog2e;
+      lm = fmaxf(lm, v[j]);
+    }
+    const float nm = fmaxf(m, lm);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += exp2f(v[j] - nm);
+    s = s * exp2f(m - nm) + acc;
+    m = nm;
+  }
+  // combine (m, s) across the wave, then across waves
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (nm == -INFINITY) ? 0.f : s * exp2f(m - nm) + os * exp2f(om - nm);
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  __syncthreads();
+  float M = -INFINITY;
+  for (int i = 0; i < 4; ++i) M = fmaxf(M, sm[i]);
+  float S = 0.f;
+  for (int i = 0; i < 4; ++i) S += ss[i] * exp2f(sm[i] - M);
+  const float lse2 = M + log2f(S);
+  if (threadIdx.x == 0) losses[row] = (lse2 - bf2f(x[lab]) * kLog2e) * kLn2;
+  __syncthreads();  // the label logit is read above before any lane overwrites it
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    u16x8 a = *reinterpret_cast<const u16x8*>(x + c);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float p = exp2f(bf2f(a[j]) * kLog2e - lse2);
+      if (c + j == lab) p -= 1.f;
+      o[j] = f2bf(p * inv_n);
+    }
+    *reinterpret_cast<u16x8*>(x + c) = o;
+  }
+}
+
+// loss = sum(losses) * inv_n
+__global__ void __launch_bounds__(256) ce_reduce_kernel(const float* __restrict__ losses, int64_t T,
+                                                        const float* __restrict__ inv_n, float* __restrict__ out) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < T; i += 256) s += losses[i];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) out[0] = s * inv_n[0];
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+// workspace: inv_n[1], losses[T]
+extern "C" int mx_ce_fwd_bwd(uint16_t* logits, const int64_t* labels, float* losses, float* inv_n, float* loss_out,
+                             int64_t T, int V, int64_t ignore, hipStream_t stream) {
+  if (V % 8 || T <= 0) return T <= 0 ? 0 : -1;
+  count_valid_kernel<<<1, 256, 0, stream>>>(labels, T, ignore, inv_n);
+  ce_fwd_bwd_kernel<<<(unsigned)T, 256, 0, stream>>>(logits, labels, losses, inv_n, V, ignore);
+  ce_reduce_kernel<<<1, 256, 0, stream>>>(losses, T, inv_n, loss_out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,176 @@
+// Memory-bound fused elementwise kernels for gfx950:
+//   * swiglu fwd/bwd over a fused [gate | up] projection
+//   * fused AdamW over flat buffers (fp32 master, fp32/bf16 grad, optional bf16 copy)
+//   * token-embedding gather / f32-atomic scatter-add
+// Every kernel moves 16 B per lane per access (G13), grid-strides with
+// <= 2048 workgroups x 256 threads (G11).
+#include "common.h"
+
+namespace mx {
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+// m[t, c] = silu(gu[t, c]) * gu[t, F + c]
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ m,
+                                                         int64_t T, int F) {
+  const int64_t per_row = F / 8;
+  const int64_t n = T * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t t = i / per_row;
+    const int c = (int)(i - t * per_row) * 8;
+    const uint16_t* row = gu + t * (2 * (int64_t)F);
+    u16x8 g = *reinterpret_cast<const u16x8*>(row + c);
+    u16x8 u = *reinterpret_cast<const u16x8*>(row + F + c);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(silu_f(bf2f(g[j])) * bf2f(u[j]));
+    *reinterpret_cast<u16x8*>(m + t * (int64_t)F + c) = o;
+  }
+}
+
+// dg = dm * u * s * (1 + g (1 - s)),  du = dm * g * s,  s = sigmoid(g)
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ dm,
+                                                         const uint16_t* __restrict__ gu,
+                                                         uint16_t* __restrict__ dgu, int64_t T, int F) {
+  const int64_t per_row = F / 8;
+  const int64_t n = T * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t t = i / per_row;
+    const int c = (int)(i - t * per_row) * 8;
+    const uint16_t* row = gu + t * (2 * (int64_t)F);
+    u16x8 g = *reinterpret_cast<const u16x8*>(row + c);
+    u16x8 u = *reinterpret_cast<const u16x8*>(row + F + c);
+    u16x8 d = *reinterpret_cast<const u16x8*>(dm + t * (int64_t)F + c);
+    u16x8 og, ou;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+      const float s = 1.f / (1.f + __expf(-gf));
+      og[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
+      ou[j] = f2bf(df * gf * s);
+    }
+    uint16_t* orow = dgu + t * (2 * (int64_t)F);
+    *reinterpret_cast<u16x8*>(orow + c) = og;
+    *reinterpret_cast<u16x8*>(orow + F + c) = ou;
+  }
+}
+
+// Fused AdamW, 4 elements per lane per iteration (n % 4 == 0).
+template <bool GRAD_BF16, bool LOWP>
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const void* __restrict__ gv,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    uint16_t* __restrict__ lowp, int64_t n, float lr, float b1,
+                                                    float b2, float eps, float wd, float inv_bc1, float inv_bc2,
+                                                    const float* __restrict__ scale_t, float scale_f) {
+  const float gs = scale_f * (scale_t ? scale_t[0] : 1.f);
+  const float decay = 1.f - lr * wd;
+  const float step = lr * inv_bc1;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * 256 * 4) {
+    f32x4 g;
+    if constexpr (GRAD_BF16) {
+      u16x4 gb = *reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(gv) + i);
+      g = f32x4{bf2f(gb[0]), bf2f(gb[1]), bf2f(gb[2]), bf2f(gb[3])};
+    } else {
+      g = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(gv) + i);
+    }
+    f32x4 pp = *reinterpret_cast<f32x4*>(p + i);
+    f32x4 mm = *reinterpret_cast<f32x4*>(m + i);
+    f32x4 vv = *reinterpret_cast<f32x4*>(v + i);
+    u16x4 lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = g[j] * gs;
+      mm[j] = b1 * mm[j] + (1.f - b1) * gj;
+      vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
+      const float den = sqrtf(vv[j] * inv_bc2) + eps;
+      pp[j] = pp[j] * decay - step * mm[j] / den;
+      if constexpr (LOWP) lo[j] = f2bf(pp[j]);
+    }
+    *reinterpret_cast<f32x4*>(p + i) = pp;
+    *reinterpret_cast<f32x4*>(m + i) = mm;
+    *reinterpret_cast<f32x4*>(v + i) = vv;
+    if constexpr (LOWP) *reinterpret_cast<u16x4*>(lowp + i) = lo;
+  }
+}
+
+// out[t, :] = W[ids[t], :]  — one 256-thread block per token row
+__global__ void __launch_bounds__(256) embedding_fwd_kernel(const int64_t* __restrict__ ids,
+                                                            const uint16_t* __restrict__ w,
+                                                            uint16_t* __restrict__ out, int H, int64_t V) {
+  const int64_t t = blockIdx.x;
+  int64_t id = ids[t];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const uint16_t* src = w + id * H;
+  uint16_t* dst = out + t * H;
+  for (int c = threadIdx.x * 8; c < H; c += 256 * 8)
+    *reinterpret_cast<u16x8*>(dst + c) = *reinterpret_cast<const u16x8*>(src + c);
+}
+
+// dW[ids[t], :] += dy[t, :]  (f32 accumulator, no-return atomics; each wave
+// instruction covers 64 consecutive floats = one 256-B segment)
+__global__ void __launch_bounds__(256) embedding_bwd_kernel(const int64_t* __restrict__ ids,
+                                                            const uint16_t* __restrict__ dy,
+                                                            float* __restrict__ dw, int H, int64_t V) {
+  const int64_t t = blockIdx.x;
+  const int64_t id = ids[t];
+  if (id < 0 || id >= V) return;
+  const uint16_t* src = dy + t * H;
+  float* dst = dw + id * H;
+  for (int c = threadIdx.x; c < H; c += 256) atomicAdd(dst + c, bf2f(src[c]));
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+static int grid_for(int64_t items) {
+  int64_t b = (items + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+extern "C" int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, hipStream_t stream) {
+  if (F % 8) return -1;
+  swiglu_fwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(gu, m, T, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F,
+                             hipStream_t stream) {
+  if (F % 8) return -1;
+  swiglu_bwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(dm, gu, dgu, T, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_adamw(float* p, const void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n,
+                        float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
+                        const float* scale_t, float scale_f, hipStream_t stream) {
+  if (n % 4) return -1;
+  const int grid = grid_for(n / 4);
+  const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
+#define ADAM_LAUNCH(GB, LP)                                                                          \
+  adamw_kernel<GB, LP><<<grid, 256, 0, stream>>>(p, g, m, v, lowp, n, lr, b1, b2, eps, wd, ib1, ib2, \
+                                                 scale_t, scale_f)
+  if (grad_bf16) {
+    if (lowp) ADAM_LAUNCH(true, true); else ADAM_LAUNCH(true, false);
+  } else {
+    if (lowp) ADAM_LAUNCH(false, true); else ADAM_LAUNCH(false, false);
+  }
+#undef ADAM_LAUNCH
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_embedding_fwd(const int64_t* ids, const uint16_t* w, uint16_t* out, int64_t T, int H,
+                                int64_t V, hipStream_t stream) {
+  if (H % 8 || T <= 0) return T <= 0 ? 0 : -1;
+  embedding_fwd_kernel<<<(unsigned)T, 256, 0, stream>>>(ids, w, out, H, V);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_embedding_bwd(const int64_t* ids, const uint16_t* dy, float* dw, int64_t T, int H, int64_t V,
+                                hipStream_t stream) {
+  if (T <= 0) return 0;
+  embedding_bwd_kernel<<<(unsigned)T, 256, 0, stream>>>(ids, dy, dw, H, V);
+  return (int)hipGetLastError();
+}

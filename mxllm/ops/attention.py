@@ -35,7 +35,7 @@ class _AttnBlockFn(torch.autograd.Function):
         o, lse = ops.attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D))
         ctx.save_for_backward(q, k, v, o, lse, cos, sin)
         ctx.dims = (B, S, Hq, Hkv, D, causal)
-        return o
+        return o.view(B * S, Hq * D)
 
     @staticmethod
     def backward(ctx, do):

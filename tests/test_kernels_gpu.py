@@ -1,0 +1,210 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 references.
+
+Random (never zero) data, odd shapes where the kernel supports them.
+"""
+import math
+
+import pytest
+import torch
+
+from mxllm.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from mxllm.ops import native
+
+    return native()
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("T,H", [(1, 64), (37, 512), (512, 4096), (64, 8192), (3, 16384)])
+def test_rmsnorm_fwd_bwd(gpu, T, H):
+    torch.manual_seed(0)
+    x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).to(torch.bfloat16)
+    y, rstd, _ = _ops().rmsnorm_fwd(x, None, w, 1e-5)
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    yr = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn_like(x)
+    yr.backward(dy.float())
+    dres = torch.randn_like(x)
+    dx, dw = _ops().rmsnorm_bwd(dy, x, w, rstd, dres, True)
+    assert rel_err(dx, xf.grad + dres.float()) < 1e-2
+    assert rel_err(dw, wf.grad) < 1e-3
+
+
+def test_add_rmsnorm(gpu):
+    torch.manual_seed(1)
+    x = torch.randn(300, 1024, device=gpu, dtype=torch.bfloat16)
+    r = torch.randn_like(x)
+    w = torch.randn(1024, device=gpu, dtype=torch.bfloat16)
+    y, rstd, h = _ops().rmsnorm_fwd(x, r, w, 1e-5)
+    href = (x.float() + r.float()).to(torch.bfloat16)
+    assert torch.equal(h, href)
+    assert rel_err(y, ref.rms_norm(href, w, 1e-5).float()) < 1e-2
+
+
+@pytest.mark.parametrize("T,F", [(1, 8), (129, 1024), (1024, 14336)])
+def test_swiglu(gpu, T, F):
+    torch.manual_seed(2)
+    gu = torch.randn(T, 2 * F, device=gpu, dtype=torch.bfloat16)
+    m = _ops().swiglu_fwd(gu)
+    guf = gu.float().requires_grad_(True)
+    mr = torch.nn.functional.silu(guf[:, :F]) * guf[:, F:]
+    assert rel_err(m, mr) < 1e-2
+    dm = torch.randn_like(m)
+    mr.backward(dm.float())
+    dgu = _ops().swiglu_bwd(dm, gu)
+    assert rel_err(dgu, guf.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T,V", [(5, 1000), (256, 128256)])
+def test_cross_entropy(gpu, T, V):
+    torch.manual_seed(3)
+    logits = (3 * torch.randn(T, V, device=gpu)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device=gpu)
+    labels[1] = -100
+    lf = logits.float().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(lf, labels, ignore_index=-100)
+    lr_.backward()
+    work = logits.clone()
+    loss, _ = _ops().ce_fwd_bwd(work, labels, -100)
+    assert abs(loss.item() - lr_.item()) < 1e-3 * max(1.0, abs(lr_.item()))
+    assert rel_err(work, lf.grad) < 1e-2
+    assert work[1].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_adamw(gpu, gdt):
+    torch.manual_seed(4)
+    n = 10000 * 4
+    p = torch.randn(n, device=gpu)
+    g = torch.randn(n, device=gpu).to(gdt)
+    m = torch.randn(n, device=gpu).abs() * 0.1
+    v = torch.randn(n, device=gpu).abs() * 0.1
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    lowp = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+    kw = dict(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=3)
+    ref.adamw_(pr, g, mr, vr, grad_scale=0.5, **kw)
+    from mxllm.ops import adamw_step_
+
+    adamw_step_(p, g, m, v, lowp, grad_scale=torch.tensor([0.5], device=gpu), **kw)
+    assert rel_err(p, pr) < 1e-6 and rel_err(m, mr) < 1e-6 and rel_err(v, vr) < 1e-6
+    assert torch.equal(lowp, p.to(torch.bfloat16))
+
+
+def test_embedding(gpu):
+    torch.manual_seed(5)
+    V, H, T = 1000, 512, 333
+    w = torch.randn(V, H, device=gpu, dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (T,), device=gpu)
+    out = _ops().embedding_fwd(ids, w)
+    assert torch.equal(out, w[ids])
+    dy = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    dw = _ops().embedding_bwd(dy, ids, V)
+    dref = torch.zeros(V, H, device=gpu).index_add_(0, ids, dy.float())
+    assert rel_err(dw, dref) < 1e-5
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_rope_split_merge(gpu, D):
+    torch.manual_seed(6)
+    B, S, Hq, Hkv = 2, 70, 8, 2
+    cos, sin = ref.rope_tables(256, D, 500000.0, {"factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                                    "original_max_position_embeddings": 8192}, gpu)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=gpu, dtype=torch.bfloat16)
+    q, k, v = _ops().rope_split(qkv, cos, sin, B, S, Hq, Hkv, D)
+    x = qkv.view(B, S, Hq + 2 * Hkv, D)
+    qr = ref.apply_rope(x[:, :, :Hq], cos, sin).transpose(1, 2)
+    kr = ref.apply_rope(x[:, :, Hq:Hq + Hkv], cos, sin).transpose(1, 2)
+    assert rel_err(q, qr) < 1e-2 and rel_err(k, kr) < 1e-2
+    assert torch.equal(v, x[:, :, Hq + Hkv:].transpose(1, 2).contiguous())
+    # backward: merge(dq, dk partials per q head, dv partials) == autograd of split+rope+GQA-repeat
+    xf = qkv.float().view(B, S, Hq + 2 * Hkv, D).requires_grad_(True)
+    qf = ref.apply_rope(xf[:, :, :Hq], cos, sin).transpose(1, 2)
+    kf = ref.apply_rope(xf[:, :, Hq:Hq + Hkv], cos, sin).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    vf = xf[:, :, Hq + Hkv:].transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    dq = torch.randn(B, Hq, S, D, device=gpu)
+    dkp = torch.randn(B, Hq, S, D, device=gpu)
+    dvp = torch.randn(B, Hq, S, D, device=gpu)
+    (qf * dq + kf * dkp + vf * dvp).sum().backward()
+    dqkv = _ops().rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D)
+    assert rel_err(dqkv, xf.grad.view(B * S, -1)) < 1e-2
+
+
+ATTN_SHAPES = [
+    (1, 4, 1, 128, 128, 128, True),
+    (2, 8, 2, 200, 200, 128, True),
+    (1, 8, 8, 256, 256, 64, False),
+    (1, 4, 2, 77, 77, 32, True),
+    (2, 16, 2, 512, 512, 128, True),
+    (1, 8, 2, 64, 320, 128, True),   # prefill with a cached prefix (bottom-right causal)
+]
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,S,Sk,D,causal", ATTN_SHAPES)
+def test_attention_fwd_bwd(gpu, B, Hq, Hkv, S, Sk, D, causal):
+    torch.manual_seed(7)
+    q = torch.randn(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, Sk, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, Sk, D, device=gpu, dtype=torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, causal, scale)
+    qf, kf, vf = [t.float().requires_grad_(True) for t in (q, k, v)]
+    orf = ref.attention(qf.transpose(1, 2), kf.transpose(1, 2), vf.transpose(1, 2), causal=causal)  # [B,S,Hq,D]
+    assert rel_err(o.view(B, S, Hq, D), orf) < 2e-2
+    # lse (log2 domain) vs reference
+    s = torch.matmul(qf, kf.repeat_interleave(Hq // Hkv, 1).transpose(-1, -2)) * scale
+    if causal:
+        i = torch.arange(S, device=gpu).view(S, 1)
+        j = torch.arange(Sk, device=gpu).view(1, Sk)
+        s = s.masked_fill(j > i + (Sk - S), float("-inf"))
+    lse_ref = torch.logsumexp(s, -1) / math.log(2)
+    assert (lse - lse_ref).abs().max().item() < 2e-2
+    do = torch.randn(B, S, Hq, D, device=gpu, dtype=torch.bfloat16)
+    orf.backward(do.float())
+    dq, dkp, dvp = _ops().attn_bwd(do.view(B, S, Hq * D), q, k, v, o, lse, causal, scale)
+    rep = Hq // Hkv
+    dk = dkp.view(B, Hkv, rep, Sk, D).sum(2)
+    dv = dvp.view(B, Hkv, rep, Sk, D).sum(2)
+    assert rel_err(dq, qf.grad) < 3e-2
+    assert rel_err(dk, kf.grad) < 3e-2
+    assert rel_err(dv, vf.grad) < 3e-2
+
+
+def test_attention_block_autograd(gpu):
+    """Full split+rope+attention autograd node vs the reference path."""
+    from mxllm.ops.attention import attention_block
+
+    torch.manual_seed(8)
+    B, S, Hq, Hkv, D = 2, 192, 8, 2, 128
+    cos, sin = ref.rope_tables(S, D, 500000.0, None, gpu)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=gpu, dtype=torch.bfloat16, requires_grad=True)
+    o = attention_block(qkv, cos, sin, B, S, Hq, Hkv, D)
+    go = torch.randn_like(o)
+    o.backward(go)
+    x = qkv.detach().float().requires_grad_(True)
+    from mxllm.ops.attention import split_heads_ref
+
+    qq, kk, vv = split_heads_ref(x, B, S, Hq, Hkv, D)
+    orf = ref.attention(ref.apply_rope(qq, cos, sin), ref.apply_rope(kk, cos, sin), vv).reshape(B * S, -1)
+    orf.backward(go.float())
+    assert rel_err(o, orf) < 2e-2
+    assert rel_err(qkv.grad, x.grad) < 3e-2
+
+
+def test_segmented_mean(gpu):
+    texts = ["test", "hello world", "é漢字", "x" * 5000]
+    codes = torch.tensor([ord(c) for t in texts for c in t], dtype=torch.int32, device=gpu)
+    offs = torch.tensor([0] + list(torch.tensor([len(t) for t in texts]).cumsum(0)), dtype=torch.int64, device=gpu)
+    out = _ops().segmented_mean(codes, offs).cpu()
+    for i, t in enumerate(texts):
+        assert abs(out[i].item() - torch.tensor([ord(c) for c in t], dtype=torch.float32).mean().item()) < 1e-3
