@@ -305,6 +305,58 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, 
   return {dq, dkp, dvp};
 }
 
+// ---------------------------------------------------------------- decode
+// qkv [B, NH*D]; k_cache/v_cache [slots, Hkv, max_seq, D]; pos/slots int32 [B]
+at::Tensor rope_append(const at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin, const at::Tensor& pos,
+                       const c10::optional<at::Tensor>& slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
+                       int64_t Hkv, int64_t D) {
+  check_bf16(qkv, "qkv");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  MX_CHECK(pos.scalar_type() == at::kInt, "pos int32");
+  const int64_t B = qkv.size(0);
+  MX_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width");
+  MX_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "cache shape");
+  DevGuard g(qkv.device());
+  const int32_t* sl = nullptr;
+  if (slots.has_value()) sl = slots->data_ptr<int32_t>();
+  auto q = at::empty({B, Hq, D}, qkv.options());
+  MX_OK(mx_rope_append(bf(qkv), cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int32_t>(), sl, bfm(q),
+                       bfm(k_cache), bfm(v_cache), (int)B, (int)Hq, (int)Hkv, (int)D, (int)k_cache.size(2),
+                       cur_stream()));
+  return q;
+}
+
+at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                       const at::Tensor& lens, const c10::optional<at::Tensor>& slots, int64_t max_len, double scale) {
+  check_bf16(q, "q");
+  MX_CHECK(lens.scalar_type() == at::kInt, "lens int32");
+  const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
+  const int64_t Hkv = k_cache.size(1), max_seq = k_cache.size(2);
+  DevGuard g(q.device());
+  const int64_t nsplit = std::max<int64_t>(1, (std::min(max_len, max_seq) + 255) / 256);
+  auto ml = at::empty({B, Hq, nsplit, 2}, q.options().dtype(at::kFloat));
+  auto po = at::empty({B, Hq, nsplit, D}, q.options().dtype(at::kFloat));
+  auto out = at::empty({B, Hq * D}, q.options());
+  const int32_t* sl = nullptr;
+  if (slots.has_value()) sl = slots->data_ptr<int32_t>();
+  MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), sl, ml.data_ptr<float>(),
+                       po.data_ptr<float>(), bfm(out), (int)B, (int)Hq, (int)Hkv, (int)D, (int)max_seq, (int)nsplit,
+                       (float)scale, cur_stream()));
+  return out;
+}
+
+at::Tensor sample(const at::Tensor& logits, double temperature, int64_t seed, int64_t step) {
+  MX_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "logits [B, V] contiguous GPU");
+  MX_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16/f32");
+  DevGuard g(logits.device());
+  auto out = at::empty({logits.size(0)}, logits.options().dtype(at::kLong));
+  MX_OK(mx_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16 ? 1 : 0, out.data_ptr<int64_t>(),
+                  (int)logits.size(0), (int)logits.size(1), (float)temperature, (uint32_t)seed, (uint32_t)step,
+                  cur_stream()));
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(mxllm, m) {
@@ -321,6 +373,9 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D) -> Tensor");
+  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale) -> Tensor");
+  m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale) -> (Tensor, Tensor, Tensor)");
 }
 
@@ -339,4 +394,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rope_merge_bwd", &rope_merge_bwd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("rope_append", &rope_append);
+  m.impl("decode_attn", &decode_attn);
+  m.impl("sample", &sample);
 }

@@ -1,0 +1,282 @@
+// Inference-side kernels for gfx950:
+//   * rope_append : decode-step q/k RoPE at per-sequence positions + KV-cache append
+//   * decode_attn : single-token GQA attention over a per-slot KV cache,
+//                   split over the sequence (flash-decoding), memory-bound:
+//                   each workgroup streams 256 keys of one (seq, kv-head) once
+//                   and serves all q-heads of that group (GQA reuse);
+//   * decode_combine : merges the per-split (m, l, o) partials;
+//   * sample : greedy argmax or exact temperature sampling via Gumbel-max with
+//              a counter-based hash RNG (one pass, no softmax materialised).
+// KV cache layout per layer: [slots, Hkv, max_seq, D] bf16 (contiguous per slot
+// and head: one 256-B row per token for D = 128).
+#include "common.h"
+
+namespace mx {
+
+// qkv [B, (Hq+2Hkv)*D] -> q [B, Hq, D] (rotated), K/V cache rows at pos[b]
+template <int D>
+__global__ void __launch_bounds__(256) rope_append_kernel(const uint16_t* __restrict__ qkv,
+                                                          const float* __restrict__ cosb,
+                                                          const float* __restrict__ sinb,
+                                                          const int32_t* __restrict__ pos,
+                                                          const int32_t* __restrict__ slots,
+                                                          uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
+                                                          uint16_t* __restrict__ vc, int B, int Hq, int Hkv,
+                                                          int max_seq) {
+  constexpr int HALF = D / 2, CPH = HALF / 8;
+  const int NH = Hq + 2 * Hkv;
+  const int64_t n = (int64_t)B * NH * CPH;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int cc = (int)(i % CPH);
+    const int head = (int)((i / CPH) % NH);
+    const int b = (int)(i / ((int64_t)CPH * NH));
+    const int c = cc * 8;
+    const int p = pos[b];
+    const int slot = slots ? slots[b] : b;
+    const uint16_t* src = qkv + (int64_t)b * NH * D + (int64_t)head * D;
+    u16x8 x1 = *reinterpret_cast<const u16x8*>(src + c);
+    u16x8 x2 = *reinterpret_cast<const u16x8*>(src + HALF + c);
+    uint16_t* dst;
+    if (head >= Hq + Hkv) {
+      dst = vc + (((int64_t)slot * Hkv + (head - Hq - Hkv)) * max_seq + p) * D;
+      *reinterpret_cast<u16x8*>(dst + c) = x1;
+      *reinterpret_cast<u16x8*>(dst + HALF + c) = x2;
+      continue;
+    }
+    dst = head < Hq ? q + ((int64_t)b * Hq + head) * D
+                    : kc + (((int64_t)slot * Hkv + (head - Hq)) * max_seq + p) * D;
+    const float* cp = cosb + (int64_t)p * HALF + c;
+    const float* sp = sinb + (int64_t)p * HALF + c;
+    u16x8 y1, y2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = bf2f(x1[j]), bb = bf2f(x2[j]);
+      y1[j] = f2bf(a * cp[j] - bb * sp[j]);
+      y2[j] = f2bf(bb * cp[j] + a * sp[j]);
+    }
+    *reinterpret_cast<u16x8*>(dst + c) = y1;
+    *reinterpret_cast<u16x8*>(dst + HALF + c) = y2;
+  }
+}
+
+constexpr int kSplit = 256;  // keys per workgroup
+constexpr int kMaxRep = 16;  // q-heads per kv-head supported
+
+// grid (nsplit, Hkv, B); block 256 = one key per thread for the score phase.
+template <int D>
+__global__ void __launch_bounds__(256) decode_attn_kernel(const uint16_t* __restrict__ q,
+                                                          const uint16_t* __restrict__ kc,
+                                                          const uint16_t* __restrict__ vc,
+                                                          const int32_t* __restrict__ lens,
+                                                          const int32_t* __restrict__ slots,
+                                                          float* __restrict__ part_ml, float* __restrict__ part_o,
+                                                          int Hq, int Hkv, int max_seq, int nsplit, float sl) {
+  __shared__ float qs[kMaxRep][D];
+  __shared__ float ps[kMaxRep][kSplit];
+  __shared__ float red[kMaxRep][4];
+  __shared__ __attribute__((aligned(16))) uint16_t vs[kSplit * D];
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int rep = Hq / Hkv;
+  const int len = lens[b];
+  const int slot = slots ? slots[b] : b;
+  const int k_lo = split * kSplit;
+  const int k_hi = min(len, k_lo + kSplit);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float* pml = part_ml + (((int64_t)b * Hq + hk * rep) * nsplit + split) * 2;
+  if (k_lo >= k_hi) {  // empty split: neutral partial
+    if (tid < rep) {
+      pml[(int64_t)tid * nsplit * 2] = -INFINITY;
+      pml[(int64_t)tid * nsplit * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  for (int i = tid; i < rep * D; i += 256) {
+    const int h = i / D, d = i % D;
+    qs[h][d] = bf2f(q[((int64_t)b * Hq + hk * rep + h) * D + d]);
+  }
+  const uint16_t* kbase = kc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
+  const uint16_t* vbase = vc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
+  // stage V rows of this split into LDS (coalesced 16-B chunks)
+  constexpr int CH = D / 8;
+  for (int c = tid; c < kSplit * CH; c += 256) {
+    const int row = c / CH, ch = c % CH, key = k_lo + row;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (key < k_hi) v = *reinterpret_cast<const u16x8*>(vbase + (int64_t)key * D + ch * 8);
+    *reinterpret_cast<u16x8*>(vs + row * D + ch * 8) = v;
+  }
+  __syncthreads();
+  const int key = k_lo + tid;
+  float s[kMaxRep];
+#pragma unroll
+  for (int h = 0; h < kMaxRep; ++h) s[h] = -INFINITY;
+  if (key < k_hi) {
+#pragma unroll
+    for (int h = 0; h < kMaxRep; ++h) s[h] = 0.f;
+    const uint16_t* kr = kbase + (int64_t)key * D;
+#pragma unroll 4
+    for (int c = 0; c < D; c += 8) {
+      const u16x8 kv = *reinterpret_cast<const u16x8*>(kr + c);
+      float kf[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[j] = bf2f(kv[j]);
+#pragma unroll
+      for (int h = 0; h < kMaxRep; ++h) {
+        if (h < rep) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[h] += qs[h][c + j] * kf[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kMaxRep; ++h) s[h] *= sl;
+  }
+  // per-head max over the split
+#pragma unroll
+  for (int h = 0; h < kMaxRep; ++h) {
+    if (h < rep) {
+      const float m = wave_max(s[h]);
+      if (lane == 0) red[h][wid] = m;
+    }
+  }
+  __syncthreads();
+  float mh[kMaxRep];
+#pragma unroll
+  for (int h = 0; h < kMaxRep; ++h)
+    mh[h] = h < rep ? fmaxf(fmaxf(red[h][0], red[h][1]), fmaxf(red[h][2], red[h][3])) : 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < kMaxRep; ++h) {
+    if (h < rep) {
+      const float p = key < k_hi ? __builtin_amdgcn_exp2f(s[h] - mh[h]) : 0.f;
+      ps[h][tid] = p;
+      const float l = wave_sum(p);
+      if (lane == 0) red[h][wid] = l;
+    }
+  }
+  __syncthreads();
+  if (tid < rep) {
+    pml[(int64_t)tid * nsplit * 2] = mh[tid];
+    pml[(int64_t)tid * nsplit * 2 + 1] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+  }
+  // o[h][d] = sum_key p[h][key] v[key][d]: thread -> (h, d pair)
+  const int nkeys = k_hi - k_lo;
+  for (int o = tid; o < rep * (D / 2); o += 256) {
+    const int h = o / (D / 2), d = (o % (D / 2)) * 2;
+    float a0 = 0.f, a1 = 0.f;
+    for (int kk = 0; kk < nkeys; ++kk) {
+      const float p = ps[h][kk];
+      const uint32_t pr = *reinterpret_cast<const uint32_t*>(vs + kk * D + d);
+      a0 += p * bf2f((uint16_t)(pr & 0xffff));
+      a1 += p * bf2f((uint16_t)(pr >> 16));
+    }
+    float* po = part_o + ((((int64_t)b * Hq + hk * rep + h) * nsplit + split) * D) + d;
+    po[0] = a0;
+    po[1] = a1;
+  }
+}
+
+// merge splits: out[b, h, :] = sum_s exp2(m_s - M) o_s / sum_s exp2(m_s - M) l_s
+template <int D>
+__global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restrict__ part_ml,
+                                                           const float* __restrict__ part_o,
+                                                           uint16_t* __restrict__ out, int nsplit) {
+  const int64_t bh = blockIdx.x;
+  const float* ml = part_ml + bh * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float L = 0.f, acc = 0.f;
+  const int d = threadIdx.x;
+  for (int s = 0; s < nsplit; ++s) {
+    const float m = ml[2 * s];
+    if (m == -INFINITY) continue;
+    const float wgt = __builtin_amdgcn_exp2f(m - M);
+    L += wgt * ml[2 * s + 1];
+    acc += wgt * part_o[(bh * nsplit + s) * D + d];
+  }
+  out[bh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+
+// logits [B, V] (bf16 or f32); temperature <= 0 -> greedy.  out ids [B] int64
+template <typename T>
+__global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logits, int64_t* __restrict__ out, int V,
+                                                     float inv_temp, uint32_t seed, uint32_t step) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int64_t row = blockIdx.x;
+  const T* x = logits + row * V;
+  float best = -INFINITY;
+  int bi = 0;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    float v;
+    if constexpr (sizeof(T) == 2) v = bf2f(reinterpret_cast<const uint16_t*>(x)[c]);
+    else v = reinterpret_cast<const float*>(x)[c];
+    if (inv_temp > 0.f) {
+      const uint32_t h = hash3(seed + (uint32_t)row * 7919u, step, (uint32_t)c);
+      const float u = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      v = v * inv_temp - __logf(-__logf(u));  // Gumbel-max
+    }
+    if (v > best) { best = v; bi = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = best; si[threadIdx.x >> 6] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (sv[w] > best || (sv[w] == best && si[w] < bi)) { best = sv[w]; bi = si[w]; }
+    out[row] = bi;
+  }
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+extern "C" int mx_rope_append(const uint16_t* qkv, const float* cosb, const float* sinb, const int32_t* pos,
+                              const int32_t* slots, uint16_t* q, uint16_t* kc, uint16_t* vc, int B, int Hq, int Hkv,
+                              int D, int max_seq, hipStream_t stream) {
+  const int64_t items = (int64_t)B * (Hq + 2 * Hkv) * (D / 16);
+  if (items <= 0) return 0;
+  const int grid = (int)std::min<int64_t>(1024, (items + 255) / 256);
+#define RA(DD) rope_append_kernel<DD><<<grid, 256, 0, stream>>>(qkv, cosb, sinb, pos, slots, q, kc, vc, B, Hq, Hkv, max_seq)
+  if (D == 128) RA(128); else if (D == 64) RA(64); else if (D == 32) RA(32); else return -1;
+#undef RA
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens,
+                              const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B, int Hq,
+                              int Hkv, int D, int max_seq, int nsplit, float scale, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (Hq % Hkv || Hq / Hkv > kMaxRep) return -1;
+  dim3 grid(nsplit, Hkv, B);
+  const float sl = scale * 1.4426950408889634f;
+#define DA(DD)                                                                                                 \
+  decode_attn_kernel<DD><<<grid, 256, 0, stream>>>(q, kc, vc, lens, slots, part_ml, part_o, Hq, Hkv, max_seq, \
+                                                   nsplit, sl);                                                \
+  decode_combine_kernel<DD><<<B * Hq, DD, 0, stream>>>(part_ml, part_o, out, nsplit)
+  if (D == 128) { DA(128); } else if (D == 64) { DA(64); } else if (D == 32) { DA(32); } else return -1;
+#undef DA
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
+                         uint32_t seed, uint32_t step, hipStream_t stream) {
+  if (B <= 0) return 0;
+  const float it = temperature > 0.f ? 1.f / temperature : 0.f;
+  if (is_bf16)
+    sample_kernel<uint16_t><<<B, 256, 0, stream>>>((const uint16_t*)logits, out, V, it, seed, step);
+  else
+    sample_kernel<float><<<B, 256, 0, stream>>>((const float*)logits, out, V, it, seed, step);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,153 @@
+"""LiteLLM-compatible ``completion(model, messages)`` client.
+
+Mirrors the slice of the LiteLLM API the reference uses
+(reference src/distributed_inference.py:7-8, 34-41, 53-54):
+``completion(model, messages)`` returning an object with
+``.choices[0].message.content``, and a module-level ``api_base``.
+LiteLLM itself is not installed in this image, so this module
+can stand in for it: ``from mxllm.serve import client as litellm``.
+
+Routing:
+  * ``api_base`` in (None, "", "local", "inproc") -> an in-process mxllm Engine
+    registered with ``register_local(model, engine, tokenizer)``;
+  * otherwise an OpenAI-compatible HTTP endpoint ``{api_base}/chat/completions``
+    (an mxllm server or any OpenAI-compatible server), Bearer auth from
+    ``api_key`` / ``OPENAI_API_KEY``.
+Failures are retried with exponential backoff + full jitter and a per-request
+timeout (the reference has neither — SURVEY D11 / A5).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+import time
+from dataclasses import dataclass, field
+
+log = logging.getLogger("mxllm.client")
+
+api_base: str | None = None
+api_key: str | None = None
+request_timeout: float = 120.0
+num_retries: int = 3
+
+_LOCAL: dict[str, tuple] = {}
+
+
+@dataclass
+class Message:
+    content: str
+    role: str = "assistant"
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+@dataclass
+class Choice:
+    message: Message
+    index: int = 0
+    finish_reason: str | None = "stop"
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+@dataclass
+class ModelResponse:
+    choices: list
+    model: str = ""
+    usage: dict = field(default_factory=dict)
+    id: str = ""
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+class CompletionError(RuntimeError):
+    pass
+
+
+def register_local(model: str, engine, tokenizer) -> None:
+    """Serve ``model`` from an in-process Engine (no HTTP)."""
+    _LOCAL[model] = (engine, tokenizer)
+
+
+def unregister_local(model: str | None = None) -> None:
+    if model is None:
+        _LOCAL.clear()
+    else:
+        _LOCAL.pop(model, None)
+
+
+def _local(model, messages, max_tokens, temperature, **kw) -> ModelResponse:
+    if model in _LOCAL:
+        eng, tok = _LOCAL[model]
+    elif len(_LOCAL) == 1:
+        eng, tok = next(iter(_LOCAL.values()))
+    else:
+        raise CompletionError(f"no local engine registered for model {model!r}")
+    ids = tok.apply_chat_template(messages)
+    out = eng.generate([ids], max_new_tokens=max_tokens, temperature=temperature,
+                       top_p=kw.get("top_p", 1.0), seed=kw.get("seed", 0))[0]
+    text = tok.decode([t for t in out if t not in eng.eos_ids])
+    return ModelResponse([Choice(Message(text))], model=model,
+                         usage={"prompt_tokens": len(ids), "completion_tokens": len(out)})
+
+
+def batch_local(model: str, prompts: list[str], max_tokens: int = 32, temperature: float = 0.0) -> list[str]:
+    """Batched in-process generation for a list of user prompts (one engine pass)."""
+    eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+    ids = [tok.apply_chat_template([{"role": "user", "content": p}]) for p in prompts]
+    outs = eng.generate(ids, max_new_tokens=max_tokens, temperature=temperature)
+    return [tok.decode([t for t in o if t not in eng.eos_ids]) for o in outs]
+
+
+def _http(model, messages, base, key, timeout, max_tokens, temperature, **kw) -> ModelResponse:
+    import httpx
+
+    url = base.rstrip("/")
+    if not url.endswith("/chat/completions"):
+        url += "/chat/completions"
+    headers = {"Content-Type": "application/json"}
+    if key:
+        headers["Authorization"] = f"Bearer {key}"
+    body = {"model": model, "messages": messages, "max_tokens": max_tokens, "temperature": temperature}
+    body.update({k: v for k, v in kw.items() if k in ("top_p", "stop", "seed", "top_k")})
+    r = httpx.post(url, json=body, headers=headers, timeout=timeout)
+    if r.status_code == 429 or r.status_code >= 500:
+        raise _Retryable(f"HTTP {r.status_code}: {r.text[:200]}")
+    if r.status_code != 200:
+        raise CompletionError(f"HTTP {r.status_code}: {r.text[:200]}")
+    j = r.json()
+    ch = [Choice(Message(c["message"]["content"], c["message"].get("role", "assistant")), c.get("index", i),
+                 c.get("finish_reason")) for i, c in enumerate(j["choices"])]
+    return ModelResponse(ch, model=j.get("model", model), usage=j.get("usage", {}), id=j.get("id", ""))
+
+
+class _Retryable(Exception):
+    pass
+
+
+def completion(model: str, messages: list[dict], *, api_base: str | None = None, api_key: str | None = None,
+               timeout: float | None = None, num_retries: int | None = None, max_tokens: int = 128,
+               temperature: float = 0.0, backoff_base: float = 0.5, backoff_max: float = 8.0, **kw) -> ModelResponse:
+    base = api_base if api_base is not None else globals()["api_base"]
+    key = api_key or globals()["api_key"] or os.environ.get("OPENAI_API_KEY")
+    timeout = timeout if timeout is not None else request_timeout
+    retries = num_retries if num_retries is not None else globals()["num_retries"]
+    if base in (None, "", "local", "inproc") or str(base).startswith("local://"):
+        return _local(model, messages, max_tokens, temperature, **kw)
+    attempt = 0
+    while True:
+        try:
+            return _http(model, messages, base, key, timeout, max_tokens, temperature, **kw)
+        except CompletionError:
+            raise
+        except Exception as e:  # noqa: BLE001 — connection errors, timeouts, 429/5xx
+            attempt += 1
+            if attempt > retries:
+                raise CompletionError(f"completion failed after {retries} retries: {e}") from e
+            delay = random.uniform(0, min(backoff_max, backoff_base * 2 ** (attempt - 1)))
+            log.warning("completion attempt %d failed (%s); retrying in %.2fs", attempt, e, delay)
+            time.sleep(delay)

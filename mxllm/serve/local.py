@@ -1,0 +1,68 @@
+"""Build and register the in-process engine that answers ``completion()`` calls
+when ``API_BASE`` is "local" (the default) — the model is served from this
+rank's own GPU instead of the reference's remote API."""
+from __future__ import annotations
+
+import logging
+
+import torch
+
+from . import client
+from .engine import Engine
+
+log = logging.getLogger("mxllm.local")
+
+
+def preset_for(model_name: str, device: torch.device) -> str:
+    n = (model_name or "").lower()
+    if "tiny" in n:
+        return "tiny"
+    if device.type != "cuda":
+        return "tiny"  # CPU plumbing runs: tiny random-init stub (BASELINE config 1)
+    for key, preset in (("70b", "llama3.1-70b"), ("8b", "llama3.1-8b"), ("1b", "llama3.2-1b")):
+        if key in n:
+            return preset
+    return "tiny"
+
+
+def ensure_local_engine(model_name: str, device, engine_model: str = "", max_batch: int = 8, max_seq: int = 2048,
+                        tokenizer_path: str = "", checkpoint: str = "", seed: int = 0):
+    from ..data.tokenizer import get_tokenizer
+    from ..models import Llama, get_config
+
+    if model_name in client._LOCAL:
+        return client._LOCAL[model_name]
+    device = torch.device(device)
+    preset = engine_model or preset_for(model_name, device)
+    cfg = get_config(preset)
+    log.info("local engine: %s (%s) on %s", model_name, preset, device)
+    model = Llama(cfg, device=device, seed=seed)
+    if checkpoint:
+        from ..train.checkpoint import load_model_weights
+
+        load_model_weights(model, checkpoint)
+    model.eval()
+    tok = get_tokenizer(cfg.vocab_size, tokenizer_path or None, cfg.bos_id, cfg.eos_id)
+    if cfg.vocab_size > 512 and not tokenizer_path:
+        max_seq = max_seq
+    eng = Engine(model, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id,))
+    client.register_local(model_name, eng, _Truncating(tok, max_seq - 64))
+    return client._LOCAL[model_name]
+
+
+class _Truncating:
+    """Keeps prompts inside the engine's context window (left-truncation)."""
+
+    def __init__(self, tok, max_prompt: int):
+        self.tok, self.max_prompt = tok, max(16, max_prompt)
+        self.eos_id = getattr(tok, "eos_id", None)
+
+    def apply_chat_template(self, messages):
+        ids = self.tok.apply_chat_template(messages)
+        return ids[-self.max_prompt:]
+
+    def encode(self, text, bos=True):
+        return self.tok.encode(text, bos)[-self.max_prompt:]
+
+    def decode(self, ids):
+        return self.tok.decode(ids)

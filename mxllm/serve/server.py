@@ -1,0 +1,205 @@
+"""OpenAI-compatible HTTP server backed by the mxllm engine.
+
+Endpoints: POST /v1/chat/completions, POST /v1/completions (both with
+optional SSE streaming), GET /v1/models, GET /health, GET /metrics
+(Prometheus text).  This is the local stand-in for the "LiteLLM-compatible
+API endpoint" hosting Llama-3.1-70B that the reference calls remotely
+(reference README.md:18, docs/setup_guide.md:10).
+
+Run:  python -m mxllm.serve.server --model llama3.1-8b --port 8000
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import time
+import uuid
+
+import torch
+
+from .engine import Engine, SamplingParams
+
+log = logging.getLogger("mxllm.server")
+
+
+def _stop_ids(tok, stop):
+    if not stop:
+        return ()
+    if isinstance(stop, str):
+        stop = [stop]
+    ids = []
+    for s in stop:
+        enc = tok.encode(s, bos=False)
+        if len(enc) == 1:
+            ids.append(enc[0])
+    return tuple(ids)
+
+
+def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = None):
+    from fastapi import FastAPI, HTTPException, Request
+    from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+
+    app = FastAPI(title="mxllm OpenAI-compatible server")
+    engine.start()
+    stats = {"requests": 0, "errors": 0, "prompt_tokens": 0, "completion_tokens": 0}
+
+    def auth(req: Request):
+        if api_key:
+            h = req.headers.get("authorization", "")
+            if h != f"Bearer {api_key}":
+                raise HTTPException(status_code=401, detail="invalid api key")
+
+    async def run(prompt_ids, body):
+        params = SamplingParams(
+            max_new_tokens=int(body.get("max_tokens") or body.get("max_completion_tokens") or 128),
+            temperature=float(body.get("temperature", 0.0) or 0.0),
+            top_p=float(body.get("top_p", 1.0) or 1.0),
+            top_k=int(body.get("top_k", 0) or 0),
+            stop_ids=_stop_ids(tokenizer, body.get("stop")),
+            seed=int(body.get("seed", 0) or 0),
+        )
+        r = engine.submit(prompt_ids, params)
+        while not r.done.is_set():
+            await asyncio.sleep(0.002)
+        if r.error:
+            stats["errors"] += 1
+            raise HTTPException(status_code=500, detail=r.error)
+        stats["prompt_tokens"] += len(prompt_ids)
+        stats["completion_tokens"] += len(r.output)
+        return r
+
+    def usage(r):
+        return {"prompt_tokens": len(r.prompt), "completion_tokens": len(r.output),
+                "total_tokens": len(r.prompt) + len(r.output)}
+
+    @app.get("/health")
+    async def health():
+        return {"status": "ok", "model": model_name, "active": len(engine.active), "waiting": len(engine.waiting)}
+
+    @app.get("/v1/models")
+    async def models():
+        return {"object": "list", "data": [{"id": model_name, "object": "model", "owned_by": "mxllm"}]}
+
+    @app.get("/metrics")
+    async def metrics():
+        lines = [f"mxllm_requests_total {stats['requests']}", f"mxllm_errors_total {stats['errors']}",
+                 f"mxllm_prompt_tokens_total {stats['prompt_tokens']}",
+                 f"mxllm_completion_tokens_total {stats['completion_tokens']}",
+                 f"mxllm_engine_steps_total {engine.steps}", f"mxllm_active_sequences {len(engine.active)}"]
+        return PlainTextResponse("\n".join(lines) + "\n")
+
+    @app.post("/v1/chat/completions")
+    @app.post("/chat/completions")
+    async def chat(req: Request):
+        auth(req)
+        body = await req.json()
+        stats["requests"] += 1
+        msgs = body.get("messages") or []
+        ids = tokenizer.apply_chat_template(msgs)
+        if body.get("stream"):
+            return StreamingResponse(_stream(ids, body, chat=True), media_type="text/event-stream")
+        r = await run(ids, body)
+        text = tokenizer.decode([t for t in r.output if t not in engine.eos_ids])
+        return JSONResponse({
+            "id": f"chatcmpl-{uuid.uuid4().hex[:24]}", "object": "chat.completion", "created": int(time.time()),
+            "model": body.get("model", model_name),
+            "choices": [{"index": 0, "message": {"role": "assistant", "content": text},
+                         "finish_reason": r.finish_reason}],
+            "usage": usage(r)})
+
+    @app.post("/v1/completions")
+    @app.post("/completions")
+    async def completions(req: Request):
+        auth(req)
+        body = await req.json()
+        stats["requests"] += 1
+        prompt = body.get("prompt", "")
+        ids = tokenizer.encode(prompt if isinstance(prompt, str) else prompt[0])
+        if body.get("stream"):
+            return StreamingResponse(_stream(ids, body, chat=False), media_type="text/event-stream")
+        r = await run(ids, body)
+        text = tokenizer.decode([t for t in r.output if t not in engine.eos_ids])
+        return JSONResponse({
+            "id": f"cmpl-{uuid.uuid4().hex[:24]}", "object": "text_completion", "created": int(time.time()),
+            "model": body.get("model", model_name),
+            "choices": [{"index": 0, "text": text, "finish_reason": r.finish_reason}], "usage": usage(r)})
+
+    async def _stream(ids, body, chat: bool):
+        r = engine.submit(ids, SamplingParams(
+            max_new_tokens=int(body.get("max_tokens") or 128), temperature=float(body.get("temperature", 0.0) or 0.0),
+            top_p=float(body.get("top_p", 1.0) or 1.0), stop_ids=_stop_ids(tokenizer, body.get("stop"))))
+        sent = 0
+        cid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+        while True:
+            done = r.done.is_set()
+            toks = r.output[sent:]
+            if toks:
+                sent += len(toks)
+                text = tokenizer.decode([t for t in toks if t not in engine.eos_ids])
+                if chat:
+                    chunk = {"id": cid, "object": "chat.completion.chunk", "model": model_name,
+                             "choices": [{"index": 0, "delta": {"content": text}, "finish_reason": None}]}
+                else:
+                    chunk = {"id": cid, "object": "text_completion", "model": model_name,
+                             "choices": [{"index": 0, "text": text, "finish_reason": None}]}
+                yield f"data: {json.dumps(chunk)}\n\n"
+            if done and sent >= len(r.output):
+                break
+            await asyncio.sleep(0.005)
+        fin = {"id": cid, "object": "chat.completion.chunk" if chat else "text_completion", "model": model_name,
+               "choices": [{"index": 0, ("delta" if chat else "text"): ({} if chat else ""),
+                            "finish_reason": r.finish_reason}]}
+        yield f"data: {json.dumps(fin)}\n\n"
+        yield "data: [DONE]\n\n"
+
+    @app.on_event("shutdown")
+    async def _shutdown():
+        engine.stop()
+
+    return app
+
+
+def build_default(model: str = "tiny", device: str | None = None, max_batch: int = 8, max_seq: int = 2048,
+                  checkpoint: str | None = None, tokenizer_path: str | None = None, seed: int = 0):
+    from ..data.tokenizer import get_tokenizer
+    from ..models import Llama, get_config
+
+    cfg = get_config(model)
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    m = Llama(cfg, device=device, seed=seed)
+    if checkpoint:
+        from ..train.checkpoint import load_model_weights
+
+        load_model_weights(m, checkpoint)
+    m.eval()
+    tok = get_tokenizer(cfg.vocab_size, tokenizer_path, cfg.bos_id, cfg.eos_id)
+    eng = Engine(m, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id, getattr(tok, "eos_id", cfg.eos_id)))
+    return eng, tok
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default=os.environ.get("MXLLM_MODEL", "tiny"))
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--max-batch", type=int, default=8)
+    ap.add_argument("--max-seq", type=int, default=2048)
+    ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--tokenizer", default=None)
+    ap.add_argument("--api-key", default=os.environ.get("MXLLM_API_KEY"))
+    ap.add_argument("--served-name", default=None)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
+    eng, tok = build_default(a.model, None, a.max_batch, a.max_seq, a.checkpoint, a.tokenizer)
+    app = build_app(eng, tok, a.served_name or a.model, a.api_key)
+    import uvicorn
+
+    uvicorn.run(app, host=a.host, port=a.port, log_level="warning")
+
+
+if __name__ == "__main__":
+    main()

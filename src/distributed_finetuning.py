@@ -1,0 +1,138 @@
+"""Distributed fine-tuning driver — the program the reference's launch scripts
+and tests name (reference scripts/run_node0.sh:16, tests/...:4) but never
+shipped.
+
+Exposes the same ``setup``/``cleanup``/``CustomDataset`` API as
+``src/distributed_inference.py`` and a real ``main()``: Llama-3.1 (tiny / 8B /
+70B presets) with LoRA or full fine-tuning, mxllm's bucketed DDP over RCCL
+(or ZeRO-3 sharding), fused HIP kernels, the native threaded token loader,
+checkpoint/resume and fault-injection hooks.
+
+  torchrun --nproc_per_node=8 src/distributed_finetuning.py --model llama3.1-8b \
+      --finetune full --seq-len 2048 --micro-batch 2 --steps 100 --ckpt-dir /tmp/ck
+"""
+import logging
+import math
+import os
+import sys
+import time
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+for _p in (_HERE, os.path.dirname(_HERE)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+from mxllm.config import load_config  # noqa: E402
+from mxllm.data.datasets import CustomDataset, load_text_dataset  # noqa: E402,F401
+from mxllm.parallel import runtime  # noqa: E402
+from mxllm.utils.faults import maybe_inject  # noqa: E402
+from mxllm.utils.metrics import MetricsWriter  # noqa: E402
+
+try:
+    from utils import setup_logging
+    from config import CONFIG
+except ImportError:
+    from src.utils import setup_logging
+    from src.config import CONFIG
+
+
+def setup(rank, world_size):
+    """Create the process group (env:// rendezvous, RCCL with GPUs / gloo on CPU)."""
+    return runtime.init(rank=rank, world_size=world_size, master_addr=CONFIG.get('MASTER_ADDR'),
+                        master_port=CONFIG.get('MASTER_PORT'))
+
+
+def cleanup():
+    runtime.cleanup()
+
+
+def build_trainer(run, env):
+    from mxllm.models import Llama, get_config
+    from mxllm.train.trainer import OptimConfig, Trainer
+
+    cfg = get_config(run.model)
+    lora_r = run.lora_r if run.finetune == "lora" else 0
+    opt = OptimConfig(lr=run.lr, weight_decay=run.weight_decay, grad_clip=run.grad_clip,
+                      warmup_steps=run.warmup_steps, total_steps=run.steps)
+    if run.parallel == "zero3":
+        from mxllm.parallel.zero3 import Zero3Trainer
+
+        return Zero3Trainer(cfg, env, opt, seed=run.seed, activation_checkpointing=run.activation_checkpointing)
+    model = Llama(cfg, device=env.device, lora_r=lora_r, lora_alpha=run.lora_alpha, seed=run.seed,
+                  activation_checkpointing=run.activation_checkpointing)
+    return Trainer(model, env, opt, bucket_mb=run.bucket_mb)
+
+
+def main(argv=None):
+    setup_logging()
+    code = 0
+    try:
+        run = load_config(CONFIG, sys.argv[1:] if argv is None else argv)
+        rank = int(os.environ.get("RANK", 0))
+        world_size = int(os.environ.get("WORLD_SIZE", 1))
+        env = setup(rank, world_size)
+        logging.info(f"Using device: {env.device}")
+
+        from mxllm.data.loader import TokenLoader, pack_texts
+        from mxllm.data.tokenizer import get_tokenizer
+        from mxllm.models import get_config
+        from mxllm.train import checkpoint
+
+        trainer = build_trainer(run, env)
+        mcfg = get_config(run.model)
+        tok = get_tokenizer(mcfg.vocab_size, run.tokenizer or None, mcfg.bos_id, mcfg.eos_id)
+        texts, _ = load_text_dataset(run.dataset, run.split, run.n_rows, run.seed)
+        tokens = pack_texts(texts, tok, getattr(tok, "eos_id", mcfg.eos_id))
+        loader = TokenLoader(tokens, run.seq_len, run.micro_batch, rank, world_size, run.seed, env.device)
+        steps_per_epoch = max(1, loader.batches_per_epoch // run.grad_accum)
+        total = run.steps or run.epochs * steps_per_epoch
+        start = 0
+        if run.ckpt_dir and run.resume:
+            extra = checkpoint.load(run.ckpt_dir, trainer)
+            if extra is not None:
+                loader.restore(extra["loader"])
+                start = trainer.step_num
+                logging.info(f"Resumed at step {start}")
+        metrics = MetricsWriter(run.metrics_file or None, rank)
+        tok_per_step = run.micro_batch * run.seq_len * run.grad_accum * world_size
+        t_last, n_since = time.perf_counter(), 0
+        for step in range(start, total):
+            maybe_inject(run, rank, step)
+            mbs = []
+            for _ in range(run.grad_accum):
+                ids, lab, epoch, _i = loader.next_device()
+                mbs.append((ids, lab))
+            loss = trainer.train_step(mbs)
+            n_since += 1
+            last = step == total - 1
+            if step % run.log_every == 0 or last:
+                lv = runtime.all_reduce_scalars([float(loss)], "sum")[0] / world_size
+                if not math.isfinite(lv):
+                    raise FloatingPointError(f"non-finite loss {lv} at step {step}")
+                if env.device.type == "cuda":
+                    torch.cuda.synchronize()
+                dt = time.perf_counter() - t_last
+                tps = tok_per_step * n_since / max(dt, 1e-9)
+                gn = float(trainer.last_grad_norm) if getattr(trainer, "last_grad_norm", None) is not None else 0.0
+                if rank == 0:
+                    logging.info(f"step {step} epoch {epoch} loss {lv:.4f} grad_norm {gn:.3f} tokens/s {tps:.0f}")
+                metrics.write(step=step, epoch=epoch, loss=lv, grad_norm=gn, tokens_per_s=tps)
+                t_last, n_since = time.perf_counter(), 0
+            if run.ckpt_dir and run.save_every and (step + 1) % run.save_every == 0:
+                checkpoint.save(run.ckpt_dir, trainer, step + 1, extra={"loader": loader.state()},
+                                sharded=run.parallel == "zero3")
+        loader.close()
+        runtime.barrier()
+    except Exception as e:
+        logging.error(f"An error occurred in the main function: {e}")
+        code = 1
+    finally:
+        cleanup()
+    if code:
+        sys.exit(code)
+
+
+if __name__ == "__main__":
+    main()
