@@ -92,7 +92,7 @@ def init(backend: str | None = None, timeout_s: float | None = None, rank: int |
         if timeout_s is None:
             timeout_s = float(os.environ.get("MXLLM_PG_TIMEOUT_S", "600"))
         kw = dict(backend=backend, rank=rank, world_size=world_size,
-                  timeout=datetime.timedelta(seconds=timeout_s))
+                  timeout=datetime.timedelta(seconds=timeout_s), store=_attempt_store(rank, world_size, timeout_s))
         if backend == "nccl" and device.type == "cuda":
             kw["device_id"] = device
         dist.init_process_group(**kw)
@@ -104,6 +104,19 @@ def init(backend: str | None = None, timeout_s: float | None = None, rank: int |
                 dist.barrier()
     _ENV = e
     return e
+
+
+def _attempt_store(rank: int, world_size: int, timeout_s: float):
+    """TCPStore client (or rank-0 server when not under torchrun) namespaced by
+    the elastic restart attempt: after ``--max-restarts`` the agent keeps its
+    store, and without a per-attempt prefix restarted ranks would read the dead
+    attempt's rendezvous keys (stale peer addresses) and fail to connect."""
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+    store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world_size=world_size,
+                          is_master=(not agent and rank == 0), timeout=datetime.timedelta(seconds=timeout_s),
+                          wait_for_workers=False)
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    return dist.PrefixStore(f"mxllm/attempt_{attempt}", store)
 
 
 def get_env() -> DistEnv:

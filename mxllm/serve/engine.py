@@ -189,12 +189,11 @@ class Engine:
         tokens = torch.tensor([r.output[-1] for r in reqs], dtype=torch.long, device=self.device)
         logits = self.decode(slots, tokens)
         self.steps += 1
-        temps = {r.params.temperature for r in reqs}
-        if len(temps) == 1 and all(r.params.top_p >= 1.0 and r.params.top_k == 0 for r in reqs):
-            nxt = dops.sample(logits, reqs[0].params.temperature, reqs[0].params.seed, self.steps).tolist()
-        else:
-            nxt = [int(dops.sample(logits[i:i + 1], r.params.temperature, r.params.seed, self.steps, r.params.top_p,
-                                   r.params.top_k)[0]) for i, r in enumerate(reqs)]
+        if all(r.params.temperature <= 0 and r.params.top_p >= 1.0 and r.params.top_k == 0 for r in reqs):
+            nxt = dops.sample(logits, 0.0).tolist()  # batched greedy
+        else:  # per-request RNG stream: (seed, token index) -> reproducible regardless of batching
+            nxt = [int(dops.sample(logits[i:i + 1], r.params.temperature, r.params.seed, len(r.output),
+                                   r.params.top_p, r.params.top_k)[0]) for i, r in enumerate(reqs)]
         for r, t in zip(reqs, nxt):
             self._accept(r, int(t))
         return True

@@ -19,6 +19,8 @@ import time
 import uuid
 
 import torch
+from fastapi import FastAPI, HTTPException, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 
 from .engine import Engine, SamplingParams
 
@@ -39,9 +41,6 @@ def _stop_ids(tok, stop):
 
 
 def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = None):
-    from fastapi import FastAPI, HTTPException, Request
-    from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
-
     app = FastAPI(title="mxllm OpenAI-compatible server")
     engine.start()
     stats = {"requests": 0, "errors": 0, "prompt_tokens": 0, "completion_tokens": 0}

@@ -1,0 +1,137 @@
+"""Inference engine + OpenAI-compatible server + LiteLLM-compatible client (CPU).
+
+SURVEY §4.2 item 3: the framework's own server on localhost with the tiny
+model; ``completion()`` over HTTP, the reference's error fallback string,
+retry/backoff (A5).
+"""
+import socket
+import threading
+import time
+
+import pytest
+import torch
+
+from mxllm.data.tokenizer import ByteTokenizer
+from mxllm.models import Llama, get_config
+from mxllm.serve import client
+from mxllm.serve.engine import Engine
+
+
+@pytest.fixture(scope="module")
+def tiny_engine():
+    torch.manual_seed(0)
+    cfg = get_config("tiny")
+    m = Llama(cfg, seed=0).eval()
+    return Engine(m, max_batch=4, max_seq=256)
+
+
+def test_greedy_decode_matches_full_forward(tiny_engine):
+    m = tiny_engine.model
+    prompt = [5, 9, 77, 1, 300]
+    out = tiny_engine.generate([prompt], max_new_tokens=6)[0]
+    seq = list(prompt)
+    with torch.no_grad():
+        for _ in range(6):
+            seq.append(int(m(torch.tensor([seq]))[0, -1].float().argmax()))
+    assert out == seq[len(prompt):]
+
+
+def test_continuous_batching_is_order_independent(tiny_engine):
+    prompts = [[i, i + 1, i + 2] for i in range(1, 10)]  # 9 prompts through 4 slots
+    batched = tiny_engine.generate(prompts, max_new_tokens=5)
+    single = [tiny_engine.generate([p], max_new_tokens=5)[0] for p in prompts]
+    assert batched == single
+
+
+def test_sampling_temperature_reproducible(tiny_engine):
+    a = tiny_engine.generate([[3, 4, 5]], max_new_tokens=8, temperature=1.0, seed=7)
+    b = tiny_engine.generate([[3, 4, 5]], max_new_tokens=8, temperature=1.0, seed=7)
+    assert a == b
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def server(tiny_engine):
+    import uvicorn
+
+    from mxllm.serve.server import build_app
+
+    port = _free_port()
+    app = build_app(tiny_engine, ByteTokenizer(512), "tiny-test", api_key="sekret")
+    cfg = uvicorn.Config(app, host="127.0.0.1", port=port, log_level="error")
+    srv = uvicorn.Server(cfg)
+    th = threading.Thread(target=srv.run, daemon=True)
+    th.start()
+    for _ in range(200):
+        if srv.started:
+            break
+        time.sleep(0.05)
+    yield f"http://127.0.0.1:{port}/v1"
+    srv.should_exit = True
+    th.join(10)
+    tiny_engine.stop()
+
+
+def test_http_completion_roundtrip(server):
+    r = client.completion("tiny-test", [{"role": "user", "content": "hello"}], api_base=server, api_key="sekret",
+                          max_tokens=5, timeout=30)
+    assert isinstance(r.choices[0].message.content, str)
+    assert r.usage["completion_tokens"] >= 1
+
+
+def test_http_auth_rejected(server):
+    with pytest.raises(client.CompletionError):
+        client.completion("tiny-test", [{"role": "user", "content": "x"}], api_base=server, api_key="wrong",
+                          max_tokens=2, timeout=30)
+
+
+def test_http_models_and_stream(server):
+    import httpx
+
+    j = httpx.get(server + "/models", timeout=10).json()
+    assert j["data"][0]["id"] == "tiny-test"
+    with httpx.stream("POST", server + "/chat/completions", timeout=30, headers={"Authorization": "Bearer sekret"},
+                      json={"messages": [{"role": "user", "content": "hi"}], "max_tokens": 4, "stream": True}) as s:
+        lines = [ln for ln in s.iter_lines() if ln]
+    assert lines[-1] == "data: [DONE]"
+
+
+def test_fallback_string_on_dead_endpoint(monkeypatch):
+    import src.distributed_inference as di
+
+    monkeypatch.setattr(client, "api_base", f"http://127.0.0.1:{_free_port()}/v1")
+    monkeypatch.setattr(di.RUN, "num_retries", 1)
+    monkeypatch.setattr(di.RUN, "request_timeout", 2.0)
+    assert di.get_model_response("hi") == "Error: Unable to get model response"
+
+
+def test_retry_with_backoff(monkeypatch):
+    calls = {"n": 0}
+
+    def flaky(*a, **k):
+        calls["n"] += 1
+        if calls["n"] < 3:
+            raise client._Retryable("HTTP 429")
+        return client.ModelResponse([client.Choice(client.Message("ok"))])
+
+    monkeypatch.setattr(client, "_http", flaky)
+    r = client.completion("m", [{"role": "user", "content": "x"}], api_base="http://x", num_retries=3,
+                          backoff_base=0.001)
+    assert r.choices[0].message.content == "ok" and calls["n"] == 3
+    calls["n"] = -10
+    with pytest.raises(client.CompletionError):
+        client.completion("m", [], api_base="http://x", num_retries=2, backoff_base=0.001)
+
+
+def test_local_inproc_route(tiny_engine):
+    client.register_local("tiny-local", tiny_engine, ByteTokenizer(512))
+    try:
+        r = client.completion("tiny-local", [{"role": "user", "content": "abc"}], api_base="local", max_tokens=3)
+        assert isinstance(r.choices[0].message.content, str)
+    finally:
+        client.unregister_local("tiny-local")
