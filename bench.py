@@ -55,6 +55,7 @@ def parse(argv=None):
     ap.add_argument("--device", default=None, help="force 'cpu' for a plumbing run")
     ap.add_argument("--layers", type=int, default=None, help="override n_layers (NOT valid for the headline)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-gemm-table", action="store_true", help="ignore the tuned hipBLASLt solution table")
     return ap.parse_args(argv)
 
 
@@ -69,6 +70,9 @@ def main(argv=None):
 
     env = runtime.init()
     dev = env.device
+    from mxllm.utils import gemm_tuning
+
+    tuned = gemm_tuning.enable() if not a.no_gemm_table else False
     cfg = get_config(a.model)
     if a.layers:
         cfg = cfg.replace(n_layers=a.layers)
@@ -135,6 +139,7 @@ def main(argv=None):
             "grad_accum": a.grad_accum,
             "activation_checkpointing": a.act_ckpt,
             "optimizer": "fused AdamW (HIP), grad clip 1.0",
+            "gemm": "hipBLASLt/rocBLAS" + (" (tuned solution table)" if tuned else ""),
         },
         "tokens_per_sec_per_gpu": round(tps / env.world_size, 2),
         "model_tflops_per_gpu": round(tps * flops_tok / env.world_size / 1e12, 1),

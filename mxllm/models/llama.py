@@ -41,11 +41,19 @@ class FusedLinear(nn.Module):
                                    requires_grad=train_base)
         self.lora_r = lora_r
         if lora_r > 0:
+            n = len(splits)
             self.scaling = lora_alpha / lora_r
-            self.lora_a = nn.Parameter(torch.empty(len(splits) * lora_r, in_features, dtype=torch.float32,
-                                                   device=device))
-            self.lora_b = nn.ParameterList([
-                nn.Parameter(torch.zeros(n, lora_r, dtype=torch.float32, device=device)) for n in splits])
+            # A: all splits' down-projections stacked; B: block-diagonal up-projection
+            self.lora_a = nn.Parameter(torch.empty(n * lora_r, in_features, dtype=dtype, device=device))
+            self.lora_b = nn.Parameter(torch.zeros(sum(splits), n * lora_r, dtype=dtype, device=device))
+
+    def lora_b_blocks(self):
+        """Views of the diagonal blocks B_i [n_i, r] of the block-diagonal B."""
+        out, off = [], 0
+        for i, n_i in enumerate(self.splits):
+            out.append(self.lora_b[off:off + n_i, i * self.lora_r:(i + 1) * self.lora_r])
+            off += n_i
+        return out
 
     @torch.no_grad()
     def reset_parameters(self, std: float, gen: torch.Generator | None):
@@ -53,12 +61,11 @@ class FusedLinear(nn.Module):
         if self.lora_r > 0:
             bound = 1.0 / math.sqrt(self.in_features)
             self.lora_a.uniform_(-bound, bound, generator=gen)
-            for b in self.lora_b:
-                b.zero_()
+            self.lora_b.zero_()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.lora_r > 0:
-            return ops.lora_linear(x, self.weight, self.lora_a, list(self.lora_b), self.splits, self.scaling)
+            return ops.lora_linear(x, self.weight, self.lora_a, self.lora_b, self.splits, self.scaling)
         return ops.linear(x, self.weight)
 
 

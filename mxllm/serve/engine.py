@@ -254,12 +254,8 @@ def merge_lora_(model) -> None:
     """Fold LoRA adapters into the base weights (W += s * B @ A) for serving."""
     for mod in model.modules():
         if getattr(mod, "lora_r", 0) > 0:
-            r = mod.lora_r
-            off = 0
-            for i, (n_i, b) in enumerate(zip(mod.splits, mod.lora_b)):
-                a = mod.lora_a[i * r:(i + 1) * r]
-                mod.weight[off:off + n_i] += (mod.scaling * (b.float() @ a.float())).to(mod.weight.dtype)
-                off += n_i
+            delta = mod.scaling * (mod.lora_b.float() @ mod.lora_a.float())
+            mod.weight += delta.to(mod.weight.dtype)
             mod.lora_r = 0
             del mod.lora_a
             del mod.lora_b

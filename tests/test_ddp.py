@@ -32,9 +32,10 @@ def _worker(rank, world, port, out_q, full, bucket_mb, accum):
     model = Llama(cfg, lora_r=0 if full else 4, seed=3)
     if not full:  # make LoRA B non-zero so every adapter gets gradient
         with torch.no_grad():
-            for n, p in model.named_parameters():
-                if "lora_b" in n:
-                    p.normal_(0, 0.02, generator=torch.Generator().manual_seed(len(n)))
+            for i, mod in enumerate(model.modules()):
+                if getattr(mod, "lora_r", 0):
+                    for blk in mod.lora_b_blocks():
+                        blk.normal_(0, 0.02, generator=torch.Generator().manual_seed(i))
     tr = Trainer(model, env, OptimConfig(lr=1e-2, grad_clip=0.0), bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
     g = torch.Generator().manual_seed(11)
     ids = torch.randint(0, cfg.vocab_size, (world * 2 * accum, 32), generator=g)
@@ -68,9 +69,10 @@ def _single_grads(world, full, accum):
     model = Llama(cfg, lora_r=0 if full else 4, seed=3)
     if not full:
         with torch.no_grad():
-            for n, p in model.named_parameters():
-                if "lora_b" in n:
-                    p.normal_(0, 0.02, generator=torch.Generator().manual_seed(len(n)))
+            for i, mod in enumerate(model.modules()):
+                if getattr(mod, "lora_r", 0):
+                    for blk in mod.lora_b_blocks():
+                        blk.normal_(0, 0.02, generator=torch.Generator().manual_seed(i))
     flat = FlatParams([(n, p) for n, p in model.named_parameters() if p.requires_grad])
     g = torch.Generator().manual_seed(11)
     ids = torch.randint(0, cfg.vocab_size, (world * 2 * accum, 32), generator=g)

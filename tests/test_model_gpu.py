@@ -1,0 +1,147 @@
+"""Model / engine level checks on the MI355X: the HIP path against the
+pure-PyTorch reference path with the same weights, decode kernels against
+their references, the native loader feeding the GPU, and smoke()."""
+import math
+import os
+
+import pytest
+import torch
+
+from mxllm.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("preset,lora", [("tiny-d128", 0), ("tiny-d128", 8), ("tiny", 0)])
+def test_train_step_matches_reference_path(gpu, preset, lora, monkeypatch):
+    from mxllm.models import Llama, get_config
+
+    cfg = get_config(preset)
+    torch.manual_seed(0)
+    m = Llama(cfg, device=gpu, lora_r=lora, seed=5)
+    if lora:
+        with torch.no_grad():
+            for mod in m.modules():
+                if getattr(mod, "lora_r", 0):
+                    for blk in mod.lora_b_blocks():
+                        blk.normal_(0, 0.02)
+    ids = torch.randint(0, cfg.vocab_size, (2, 192), device=gpu)
+    loss = m(ids, ids)
+    loss.backward()
+    g_native = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.requires_grad}
+    m.zero_grad(set_to_none=True)
+    monkeypatch.setenv("MXLLM_REFERENCE_OPS", "1")
+    loss_ref = m(ids, ids)
+    loss_ref.backward()
+    assert abs(loss.item() - loss_ref.item()) < 2e-2 * max(1, abs(loss_ref.item()))
+    for n, p in m.named_parameters():
+        if p.requires_grad:
+            e = _rel(g_native[n], p.grad)
+            assert e < 6e-2, (n, e)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 32, 8), (32, 8, 2)])
+def test_decode_kernels(gpu, D, Hq, Hkv):
+    from mxllm.ops import native
+
+    torch.manual_seed(1)
+    B, max_seq = 3, 700
+    lens = [5, 300, 640]
+    kc = torch.randn(4, Hkv, max_seq, D, device=gpu, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    slots = torch.tensor([2, 0, 3], dtype=torch.int32, device=gpu)
+    pos = torch.tensor(lens, dtype=torch.int32, device=gpu)
+    cos, sin = ref.rope_tables(1024, D, 500000.0, None, gpu)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=gpu, dtype=torch.bfloat16)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q = native().rope_append(qkv, cos, sin, pos, slots, kc, vc, Hq, Hkv, D)
+    out = native().decode_attn(q, kc, vc, pos + 1, slots, max(lens) + 1, 1.0 / math.sqrt(D))
+    x = qkv.float().view(B, Hq + 2 * Hkv, D)
+    for i in range(B):
+        p, s = lens[i], int(slots[i])
+        c, sn = cos[p].view(1, -1), sin[p].view(1, -1)
+
+        def rot(t):
+            return torch.cat([t[..., :D // 2] * c - t[..., D // 2:] * sn, t[..., D // 2:] * c + t[..., :D // 2] * sn], -1)
+
+        qr = rot(x[i, :Hq])
+        assert _rel(q[i], qr) < 1e-2
+        kc_ref[s, :, p] = rot(x[i, Hq:Hq + Hkv]).to(torch.bfloat16)
+        vc_ref[s, :, p] = x[i, Hq + Hkv:].to(torch.bfloat16)
+        assert torch.equal(kc[s, :, p], kc_ref[s, :, p]) and torch.equal(vc[s, :, p], vc_ref[s, :, p])
+        kk = kc_ref[s, :, :p + 1].float().repeat_interleave(Hq // Hkv, 0)
+        vv = vc_ref[s, :, :p + 1].float().repeat_interleave(Hq // Hkv, 0)
+        att = (torch.einsum("hd,hld->hl", q[i].float(), kk) / math.sqrt(D)).softmax(-1)
+        o = torch.einsum("hl,hld->hd", att, vv)
+        assert _rel(out[i].view(Hq, D), o) < 2e-2
+
+
+def test_sampler(gpu):
+    from mxllm.ops import native
+
+    logits = torch.randn(5, 128256, device=gpu)
+    assert torch.equal(native().sample(logits, 0.0, 0, 0), logits.argmax(-1))
+    # temperature sampling follows the softmax distribution (chi-square-ish sanity)
+    small = torch.tensor([[0.0, 1.0, 2.0, -1.0]], device=gpu).repeat(4000, 1).contiguous()
+    draws = native().sample(small, 1.0, 123, 0).cpu()
+    freq = torch.bincount(draws, minlength=4).float() / 4000
+    p = torch.softmax(torch.tensor([0.0, 1.0, 2.0, -1.0]), 0)
+    assert (freq - p).abs().max().item() < 0.03
+
+
+def test_engine_gpu_matches_cpu(gpu):
+    from mxllm.models import Llama, get_config
+    from mxllm.serve.engine import Engine
+
+    cfg = get_config("tiny-d128")
+    m = Llama(cfg, device=gpu, seed=3).eval()
+    eng = Engine(m, max_batch=4, max_seq=512)
+    prompts = [[1, 2, 3, 4, 5], list(range(10, 300)), [7]]
+    out = eng.generate(prompts, max_new_tokens=8)
+    # recompute greedily with full forwards through the HIP training path
+    for p, o in zip(prompts, out):
+        seq = list(p)
+        with torch.no_grad():
+            for _ in range(len(o)):
+                seq.append(int(m(torch.tensor([seq], device=gpu))[0, -1].float().argmax()))
+        agree = sum(int(a == b) for a, b in zip(o, seq[len(p):]))
+        assert agree >= len(o) - 1, (o, seq[len(p):])  # bf16 ties may flip at most one late token
+
+
+def test_native_loader_to_gpu(gpu):
+    from mxllm.data.loader import TokenLoader
+
+    toks = torch.randint(0, 1000, (20000,), dtype=torch.int32)
+    ld = TokenLoader(toks, 256, 4, 0, 1, seed=0, device=gpu)
+    ids, lab, _, _ = ld.next_device()
+    assert ids.is_cuda and ids.shape == (4, 256) and torch.equal(ids[:, 1:], lab[:, :-1])
+    ld.close()
+
+
+def test_smoke_entry(gpu):
+    import __graft_entry__
+
+    __graft_entry__.smoke()
+
+
+def test_bench_contract_tiny(gpu, tmp_path):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "b.json"
+    r = subprocess.run([sys.executable, "bench.py", "--model", "tiny-d128", "--steps", "2", "--warmup", "1",
+                        "--seq-len", "256", "--json-out", str(out)], cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads(out.read_text())
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in j
+    assert j["value"] > 0 and j["n_gpus"] == 1

@@ -1,0 +1,99 @@
+"""CPU checks of op semantics: fused LoRA linear autograd vs a plain-PyTorch
+formulation, Llama-3.1 RoPE frequencies vs the transformers implementation,
+reference attention vs torch SDPA, AdamW reference vs torch.optim.AdamW."""
+import math
+
+import pytest
+import torch
+
+from mxllm.ops import reference as ref
+from mxllm.ops.linear import lora_linear
+
+
+def test_lora_linear_matches_plain_autograd():
+    torch.manual_seed(0)
+    T, K, splits, r, s = 7, 24, [16, 8, 8], 4, 2.0
+    x = torch.randn(T, K, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(sum(splits), K, dtype=torch.float64)
+    a = torch.randn(len(splits) * r, K, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(sum(splits), len(splits) * r, dtype=torch.float64)
+    off = 0
+    for i, n in enumerate(splits):
+        b[off:off + n, i * r:(i + 1) * r] = torch.randn(n, r, dtype=torch.float64)
+        off += n
+    b.requires_grad_(True)
+    y = lora_linear(x, w, a, b, splits, s)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    gx, ga, gb = x.grad.clone(), a.grad.clone(), b.grad.clone()
+    x.grad = a.grad = b.grad = None
+    # plain: separate adapter per split
+    outs, off = [], 0
+    for i, n in enumerate(splits):
+        bi = b[off:off + n, i * r:(i + 1) * r]
+        ai = a[i * r:(i + 1) * r]
+        outs.append(x @ w[off:off + n].t() + s * (x @ ai.t()) @ bi.t())
+        off += n
+    yr = torch.cat(outs, -1)
+    yr.backward(gy)
+    assert torch.allclose(y, yr, atol=1e-10)
+    assert torch.allclose(gx, x.grad, atol=1e-10) and torch.allclose(ga, a.grad, atol=1e-10)
+    mask = b.detach() != 0
+    assert torch.allclose(gb[mask], b.grad[mask], atol=1e-10)
+    assert (gb[~mask] == 0).all(), "off-diagonal blocks of B must get exactly zero gradient"
+
+
+def test_llama3_rope_matches_transformers():
+    tr = pytest.importorskip("transformers.modeling_rope_utils")
+    from transformers import LlamaConfig
+
+    cfg = LlamaConfig(rope_theta=500000.0, head_dim=128, hidden_size=8192, num_attention_heads=64,
+                      max_position_embeddings=131072,
+                      rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                    "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    fn = tr.ROPE_INIT_FUNCTIONS["llama3"]
+    inv_hf, _ = fn(cfg, "cpu")
+    mine = ref.llama3_inv_freq(128, 500000.0, {"factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                               "original_max_position_embeddings": 8192})
+    assert torch.allclose(inv_hf.double(), mine, rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("S,Sk,causal", [(17, 17, True), (5, 23, True), (9, 9, False)])
+def test_reference_attention_vs_sdpa(S, Sk, causal):
+    torch.manual_seed(1)
+    q = torch.randn(2, S, 4, 16)
+    k = torch.randn(2, Sk, 2, 16)
+    v = torch.randn(2, Sk, 2, 16)
+    o = ref.attention(q, k, v, causal=causal)
+    kk, vv = k.repeat_interleave(2, 2), v.repeat_interleave(2, 2)
+    mask = None
+    if causal:
+        i = torch.arange(S).view(S, 1)
+        j = torch.arange(Sk).view(1, Sk)
+        mask = j <= i + (Sk - S)
+    o2 = torch.nn.functional.scaled_dot_product_attention(q.transpose(1, 2), kk.transpose(1, 2), vv.transpose(1, 2),
+                                                          attn_mask=mask).transpose(1, 2)
+    assert torch.allclose(o, o2, atol=1e-5)
+
+
+def test_adamw_reference_matches_torch():
+    torch.manual_seed(2)
+    p0 = torch.randn(50)
+    grads = [torch.randn(50) for _ in range(4)]
+    p = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.AdamW([p], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    mine, m, v = p0.clone(), torch.zeros(50), torch.zeros(50)
+    for i, g in enumerate(grads):
+        p.grad = g.clone()
+        opt.step()
+        ref.adamw_(mine, g, m, v, lr=1e-2, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=i + 1)
+    assert torch.allclose(mine, p.detach(), atol=1e-6)
+
+
+def test_flops_model():
+    from mxllm.models import get_config
+
+    c = get_config("llama3.1-70b")
+    assert abs(c.n_params() / 1e9 - 70.55) < 0.05
+    assert abs(get_config("llama3.1-8b").n_params() / 1e9 - 8.03) < 0.01
+    assert math.isclose(c.train_flops_per_token(2048) / 1e9, 431.4, rel_tol=0.02)
