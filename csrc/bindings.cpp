@@ -285,9 +285,10 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   return {o, lse};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q,
-                                                        const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
-                                                        const at::Tensor& lse, bool causal, double scale) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q,
+                                                             const at::Tensor& k, const at::Tensor& v,
+                                                             const at::Tensor& o, const at::Tensor& lse, int causal,
+                                                             double scale) {
   check_bf16(dout, "dout");
   check_bf16(o, "o");
   check_f32(lse, "lse");
@@ -295,14 +296,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, 
   const int64_t Hkv = k.size(1), Sk = k.size(2);
   MX_CHECK(dout.numel() == B * S * Hq * D && o.numel() == dout.numel(), "dout/o shape");
   DevGuard g(q.device());
-  auto dq = at::zeros({B, Hq, S, D}, q.options().dtype(at::kFloat));
+  const int64_t S_pad = (S + 63) / 64 * 64;
+  auto dq_pad = at::zeros({B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
   auto dkp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
   auto dvp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
-                    dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                    (int)S, (int)Sk, (int)D, causal ? 1 : 0, (float)scale, cur_stream()));
+                    dq_pad.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
+                    (int)S, (int)Sk, (int)D, causal, (float)scale, cur_stream()));
+  auto dq = S_pad == S ? dq_pad : dq_pad.narrow(2, 0, S).contiguous();
   return {dq, dkp, dvp};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q,
+                                                        const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+                                                        const at::Tensor& lse, bool causal, double scale) {
+  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale);
+}
+
+// timing-only ablation variants (mode: -1 = causal without dQ atomics)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_ablate(const at::Tensor& dout, const at::Tensor& q,
+                                                               const at::Tensor& k, const at::Tensor& v,
+                                                               const at::Tensor& o, const at::Tensor& lse,
+                                                               int64_t mode, double scale) {
+  return attn_bwd_impl(dout, q, k, v, o, lse, (int)mode, scale);
 }
 
 // ---------------------------------------------------------------- decode
@@ -376,6 +393,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D) -> Tensor");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
+  m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale) -> (Tensor, Tensor, Tensor)");
 }
 
@@ -394,6 +412,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rope_merge_bwd", &rope_merge_bwd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("attn_bwd_ablate", &attn_bwd_ablate);
   m.impl("rope_append", &rope_append);
   m.impl("decode_attn", &decode_attn);
   m.impl("sample", &sample);

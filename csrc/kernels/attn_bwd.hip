@@ -60,26 +60,27 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
   }
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool ATOMIC = true>
 __global__ void __launch_bounds__(256, 1)
 attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                 float* __restrict__ dQ, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq, int Hkv,
-                int S, int Sk, int off, float sl, float scale) {
+                int S, int Sk, int off, float sl, float scale, int S_pad) {
   constexpr int BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
-  constexpr int KIMG = BN * ROWB;           // K image [128][D]
-  constexpr int QT = BQ * ROWB;             // Q tile / dO tile [64][D]
-  constexpr int DSROWB = BQ * 2;            // dS image row: 64 q bf16 = 128 B
-  constexpr int DSIMG = BN * DSROWB;        // [128 keys][64 q]
-  constexpr int LPT_Q = BQ * CH / 256;      // 16-B chunks per thread per tile
+  constexpr int KIMG = BN * ROWB;      // K image [128][D]
+  constexpr int QT = BQ * ROWB;        // one Q tile / dO tile [64][D]
+  constexpr int DSROWB = BQ * 2;       // dS image row: 64 q bf16 = 128 B
+  constexpr int DSIMG = BN * DSROWB;   // [128 keys][64 q]
   constexpr int LPT_K = BN * CH / 256;
-  __shared__ __attribute__((aligned(16))) char smem[KIMG + 2 * QT + DSIMG + 2 * BQ * 4];
+  constexpr int SEGS = QT / 1024;      // 1-KiB LDS-DMA segments per tile
+  constexpr int NT = (2 * DB + 3) / 4; // dQ output tiles per wave
+  // LDS: K image | 2 x (Q tile, dO tile, lse[64], delta[64]) | dS image  -- ONE array (guide §5 trap 4a)
+  constexpr int BUF = 2 * QT + 2 * BQ * 4;
+  __shared__ __attribute__((aligned(16))) char smem[KIMG + 2 * BUF + DSIMG];
   char* kimg = smem;
-  char* qt = smem + KIMG;
-  char* dot = qt + QT;
-  char* dsi = dot + QT;
-  float* lse_s = reinterpret_cast<float*>(dsi + DSIMG);
-  float* del_s = lse_s + BQ;
+  char* dsi = smem + KIMG + 2 * BUF;
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
 
   const int nkb = (Sk + BN - 1) / BN;
   const int BH = B * Hq;
@@ -95,32 +96,28 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const uint16_t* dOp = dO + (size_t)b * S * dstride + (size_t)h * D;
   const float* lsep = LSE + (size_t)(b * Hq + h) * S;
   const float* delp = DELTA + (size_t)(b * Hq + h) * S;
-  float* dQp = dQ + (size_t)(b * Hq + h) * S * D;
+  float* dQp = dQ + (size_t)(b * Hq + h) * S_pad * D;  // rows padded to S_pad: atomics need no guard
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
   const int k0 = kb * BN;
   const int key = k0 + 32 * w + r;  // this lane's key
+  const int kld = min(key, Sk - 1);
 
-  // K image (whole WG) + per-wave K/V fragments
+  // K image (whole WG) + per-wave K/V fragments (clamped rows; masked later)
 #pragma unroll
   for (int i = 0; i < LPT_K; ++i) {
-    const int c = tid + 256 * i, row = c / CH, ch = c % CH, kk = k0 + row;
-    u16x8 val = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (kk < Sk) val = *reinterpret_cast<const u16x8*>(Kp + (size_t)kk * D + ch * 8);
-    *reinterpret_cast<u16x8*>(kimg + row * ROWB + 16 * (ch ^ swzb<CH>(row))) = val;
+    const int c = tid + 256 * i, row = c / CH, ch = c % CH, kk = min(k0 + row, Sk - 1);
+    *reinterpret_cast<u16x8*>(kimg + row * ROWB + 16 * (ch ^ swzb<CH>(row))) =
+        *reinterpret_cast<const u16x8*>(Kp + (size_t)kk * D + ch * 8);
   }
   u16x8 kf[KS], vf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    if (key < Sk) {
-      kf[s] = *reinterpret_cast<const u16x8*>(Kp + (size_t)key * D + 16 * s + 8 * hh);
-      vf[s] = *reinterpret_cast<const u16x8*>(Vp + (size_t)key * D + 16 * s + 8 * hh);
-    } else {
-      kf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    kf[s] = *reinterpret_cast<const u16x8*>(Kp + (size_t)kld * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const u16x8*>(Vp + (size_t)kld * D + 16 * s + 8 * hh);
   }
   f32x16 dk[DB], dv[DB];
 #pragma unroll
@@ -132,44 +129,62 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   if (CAUSAL) qstart = max(0, (k0 - off) / BQ * BQ);
   const int nqt = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
 
-  u16x8 qst[LPT_Q], dost[LPT_Q];
-  float lse_r = 0.f, del_r = 0.f;
-  auto gload = [&](int it) {
+  // LDS-DMA of q tile `it` into buffer `buf`: Q / dO rows (swizzle via source
+  // chunk permutation), lse / delta by wave 0 (4 B per lane).
+  auto glds = [&](int it, int buf) {
+    char* qt = smem + KIMG + buf * BUF;
+    char* dot = qt + QT;
+    char* ld = dot + QT;
     const int q0 = qstart + it * BQ;
 #pragma unroll
-    for (int i = 0; i < LPT_Q; ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH, q = q0 + row;
-      if (q < S) {
-        qst[i] = *reinterpret_cast<const u16x8*>(Qp + (size_t)q * D + ch * 8);
-        dost[i] = *reinterpret_cast<const u16x8*>(dOp + (size_t)q * dstride + ch * 8);
-      } else {
-        qst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        dost[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
+    for (int i = 0; i < SEGS / 4; ++i) {
+      const int seg = w * (SEGS / 4) + i;
+      const int byte = seg * 1024 + lane * 16;
+      const int row = byte / ROWB, slot = (byte % ROWB) / 16;
+      const int ch = slot ^ swzb<CH>(row);
+      const int q = min(q0 + row, S - 1);
+      __builtin_amdgcn_global_load_lds((gptr_t)(Qp + (size_t)q * D + ch * 8), (lptr_t)(qt + seg * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(dOp + (size_t)q * dstride + ch * 8), (lptr_t)(dot + seg * 1024), 16,
+                                       0, 0);
     }
-    if (tid < BQ) {
-      const int q = q0 + tid;
-      lse_r = q < S ? lsep[q] : INFINITY;
-      del_r = q < S ? delp[q] : 0.f;
+    if (w == 0) {
+      const int q = min(q0 + lane, S - 1);
+      __builtin_amdgcn_global_load_lds((gptr_t)(lsep + q), (lptr_t)(ld), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(delp + q), (lptr_t)(ld + BQ * 4), 4, 0, 0);
     }
-  };
-  auto swrite = [&]() {
-#pragma unroll
-    for (int i = 0; i < LPT_Q; ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
-      const int o = row * ROWB + 16 * (ch ^ swzb<CH>(row));
-      *reinterpret_cast<u16x8*>(qt + o) = qst[i];
-      *reinterpret_cast<u16x8*>(dot + o) = dost[i];
-    }
-    if (tid < BQ) { lse_s[tid] = lse_r; del_s[tid] = del_r; }
   };
 
-  if (nqt > 0) gload(0);
+  f32x16 pend[NT];  // dQ tile of the previous iteration, added after the next barrier
+  int pend_q0 = -1;
+  auto flush_dq = [&]() {
+    if (!ATOMIC || pend_q0 < 0) return;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int tile = w + 4 * t;
+      if (tile < 2 * DB) {
+        const int m = tile / DB, db = tile % DB;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int q = pend_q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          atomicAdd(dQp + (size_t)q * D + db * 32 + r, pend[t][j]);
+        }
+      }
+    }
+  };
+
+  if (nqt > 0) glds(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): prologue loads retired (visible to the waitcnt pass)
+  __syncthreads();
   for (int it = 0; it < nqt; ++it) {
     const int q0 = qstart + it * BQ;
-    swrite();
-    __syncthreads();  // tiles visible; previous iteration's dS image fully consumed
-    if (it + 1 < nqt) gload(it + 1);
+    const int buf = it & 1;
+    const char* qt = smem + KIMG + buf * BUF;
+    const char* dot = qt + QT;
+    const float* lse_s = reinterpret_cast<const float*>(dot + QT);
+    const float* del_s = lse_s + BQ;
+    if (it + 1 < nqt) glds(it + 1, buf ^ 1);  // prefetch next tile (its buffer was last read before the barrier)
+    flush_dq();                              // previous tile's dQ atomics overlap this tile's MFMAs
+    const bool need_mask = (q0 + BQ > S) || (k0 + BN > Sk) || (CAUSAL && (k0 + 32 * w + 31 > q0 + off));
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       f32x16 sa, dp;
@@ -189,13 +204,22 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         lv[gq] = *reinterpret_cast<const f32x4*>(lse_s + 32 * m + 8 * gq + 4 * hh);
         dl[gq] = *reinterpret_cast<const f32x4*>(del_s + 32 * m + 8 * gq + 4 * hh);
       }
+      if (need_mask) {  // wave-uniform; branch-free selects
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        float p = __builtin_amdgcn_exp2f(sa[j] * sl - lv[j >> 2][j & 3]);
-        if (key >= Sk || (CAUSAL && key > q + off)) p = 0.f;
-        sa[j] = p;
-        dp[j] = p * (dp[j] - dl[j >> 2][j & 3]);  // dS
+        for (int j = 0; j < 16; ++j) {
+          const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          const bool dead = (key >= Sk) | (q >= S) | (CAUSAL & (key > q + off));
+          const float p = dead ? 0.f : __builtin_amdgcn_exp2f(sa[j] * sl - lv[j >> 2][j & 3]);
+          sa[j] = p;
+          dp[j] = p * (dp[j] - dl[j >> 2][j & 3]);  // dS
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float p = __builtin_amdgcn_exp2f(sa[j] * sl - lv[j >> 2][j & 3]);
+          sa[j] = p;
+          dp[j] = p * (dp[j] - dl[j >> 2][j & 3]);
+        }
       }
       // dV^T += dO^T P ; dK^T += Q^T dS   (k index = q rows of this m-subtile)
 #pragma unroll
@@ -229,36 +253,37 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swzb<8>(krow)) + 8 * hh) = v4;
       }
     }
-    __syncthreads();  // dS image complete
-    // dQ[q0 .. q0+63][:] += scale * dS[64 x 128] . K[128 x D]
-    for (int tile = w; tile < 2 * DB; tile += 4) {
-      const int m = tile / DB, db = tile % DB;
-      f32x16 acc;
+    __syncthreads();  // dS image complete (also retires the DMA + atomics issued above)
+    // dQ[q0 .. q0+63][:] = scale * dS[64 x 128] . K[128 x D]  -> kept in `pend`, added next iteration
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int t = 0; t < NT; ++t) {
+      const int tile = w + 4 * t;
+      if (tile < 2 * DB) {
+        const int m = tile / DB, db = tile % DB;
+        f32x16 acc;
 #pragma unroll
-      for (int s = 0; s < BN / 16; ++s) {
-        const int kbse = 16 * s + 4 * hh;
-        const int rA = kbse + tq, rB = kbse + 8 + tq;
-        // A = dS[q][key]: rows of the [key][q] image, columns q = 32m + 16(g&1) + ...
-        const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
-        const u16x4 a0 = trd(dsi + rA * DSROWB + 16 * (qchunk ^ swzb<8>(rA)) + 8 * (tp & 1));
-        const u16x4 a1 = trd(dsi + rB * DSROWB + 16 * (qchunk ^ swzb<8>(rB)) + 8 * (tp & 1));
-        // B = K[key][d]
-        const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
-        const u16x4 b0 = trd(kimg + rA * ROWB + 16 * (dchunk ^ swzb<CH>(rA)) + 8 * (tp & 1));
-        const u16x4 b1 = trd(kimg + rB * ROWB + 16 * (dchunk ^ swzb<CH>(rB)) + 8 * (tp & 1));
-        acc = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]},
-                      u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc);
-      }
-      // C: col = d (lane r), row = q
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        if (q < S) atomicAdd(dQp + (size_t)q * D + db * 32 + r, acc[j] * scale);
+        for (int s = 0; s < BN / 16; ++s) {
+          const int kbse = 16 * s + 4 * hh;
+          const int rA = kbse + tq, rB = kbse + 8 + tq;
+          const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
+          const u16x4 a0 = trd(dsi + rA * DSROWB + 16 * (qchunk ^ swzb<8>(rA)) + 8 * (tp & 1));
+          const u16x4 a1 = trd(dsi + rB * DSROWB + 16 * (qchunk ^ swzb<8>(rB)) + 8 * (tp & 1));
+          const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+          const u16x4 b0 = trd(kimg + rA * ROWB + 16 * (dchunk ^ swzb<CH>(rA)) + 8 * (tp & 1));
+          const u16x4 b1 = trd(kimg + rB * ROWB + 16 * (dchunk ^ swzb<CH>(rB)) + 8 * (tp & 1));
+          acc = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]},
+                        u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc);
+        }
+        pend[t] = acc * scale;
+        if constexpr (!ATOMIC) asm volatile("" ::"v"(pend[t][0]));
       }
     }
+    pend_q0 = q0;
+    __syncthreads();  // dS image consumed; next tile's DMA landed
   }
+  flush_dq();
   // write per-q-head dK/dV partials: C rows = d, col = key (lane)
   if (key < Sk) {
     float* dkq = dKp + ((size_t)(b * Hq + h) * Sk + key) * D;
@@ -281,7 +306,8 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 
 using namespace mx;
 
-// dq must be ZEROED by the caller (f32 atomics).  delta: workspace [B,Hq,S].
+// dq [B,Hq,ceil(S/64)*64,D] f32 must be ZEROED by the caller (f32 atomics; padded rows absorb
+// the unguarded tail atomics).  delta: workspace [B,Hq,S].
 extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
                            const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
                            int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream) {
@@ -293,9 +319,15 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   const int grid = nkb * B * Hq;
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
+  const int S_pad = (S + 63) / 64 * 64;  // dq rows are padded (see mx_attn_bwd contract)
 #define BWD(DD, C)                                                                                          \
   attn_bwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv, S, Sk, \
-                                                   off, sl, scale)
+                                                   off, sl, scale, S_pad)
+  if (causal < 0) {  // ablation: no dQ atomics (timing experiments only; dq left zero)
+    attn_bwd_kernel<128, true, false><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv,
+                                                                S, Sk, off, sl, scale, S_pad);
+    return (int)hipGetLastError();
+  }
   if (D == 128) { if (causal) BWD(128, true); else BWD(128, false); }
   else if (D == 64) { if (causal) BWD(64, true); else BWD(64, false); }
   else if (D == 32) { if (causal) BWD(32, true); else BWD(32, false); }

@@ -63,45 +63,39 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const uint16_t* Qp = Q + ((size_t)(b * Hq + h) * S) * D;
   const uint16_t* Kp = K + ((size_t)(b * Hkv + hk) * Sk) * D;
   const uint16_t* Vp = V + ((size_t)(b * Hkv + hk) * Sk) * D;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (no divergent branches)
   const int r = lane & 31, hh = lane >> 5;
   const int q0 = qb * BM;
   const int qrow = q0 + 32 * w + r;
+  const int qld = min(qrow, S - 1);  // clamped, unconditional loads: no phi -> no early vmcnt(0)
 
   u16x8 qf[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (qrow < S) qf[s] = *reinterpret_cast<const u16x8*>(Qp + (size_t)qrow * D + 16 * s + 8 * hh);
-    else qf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
+  for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const u16x8*>(Qp + (size_t)qld * D + 16 * s + 8 * hh);
 
   int kend = Sk;
   if (CAUSAL) kend = min(Sk, q0 + BM + causal_off);
   const int ntiles = kend > 0 ? (kend + BN - 1) / BN : 0;
 
-  u16x8 kst[LPT], vst[LPT];
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH, key = kt * BN + row;
-      if (key < Sk) {
-        kst[i] = *reinterpret_cast<const u16x8*>(Kp + (size_t)key * D + ch * 8);
-        vst[i] = *reinterpret_cast<const u16x8*>(Vp + (size_t)key * D + ch * 8);
-      } else {
-        kst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        vst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
-    }
-  };
-  auto swrite = [&](int buf) {
+  // K/V tiles stream straight into LDS with LDS-DMA (global_load_lds_dwordx4):
+  // one wave instruction writes 1 KiB lane-linearly, so the XOR-swizzled image
+  // is produced by permuting each lane's SOURCE chunk (guide rule 21) and no
+  // VGPRs are spent on staging (the kernel sits at the 256-VGPR cap).
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  auto glds = [&](int kt, int buf) {
     char* kb = smem + buf * 2 * TILE;
     char* vb = kb + TILE;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
-      const int off = row * ROWB + 16 * (ch ^ swz<CH>(row));
-      *reinterpret_cast<u16x8*>(kb + off) = kst[i];
-      *reinterpret_cast<u16x8*>(vb + off) = vst[i];
+      const int seg = w * LPT + i;            // 1 KiB segment of the tile image
+      const int byte = seg * 1024 + lane * 16;
+      const int row = byte / ROWB, slot = (byte % ROWB) / 16;
+      const int ch = slot ^ swz<CH>(row);     // logical chunk stored in this slot
+      const int key = min(kt * BN + row, Sk - 1);  // tail rows: duplicate valid row, masked later
+      __builtin_amdgcn_global_load_lds((gptr_t)(Kp + (size_t)key * D + ch * 8), (lptr_t)(kb + seg * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(Vp + (size_t)key * D + ch * 8), (lptr_t)(vb + seg * 1024), 16, 0, 0);
     }
   };
 
@@ -115,15 +109,16 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   // per-lane constants for the transposed V reads
   const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
 
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0);
-  }
+  if (ntiles > 0) glds(0, 0);
+  // Retire the prologue's Q loads and tile-0 DMA with a wait the compiler's
+  // waitcnt pass can see (otherwise it treats them as possibly pending at the
+  // loop header and drains the in-loop prefetch under the QK MFMAs).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   const int wq_hi = q0 + 32 * w + 31;
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < ntiles) gload(kt + 1);
+    if (kt + 1 < ntiles) glds(kt + 1, (kt + 1) & 1);  // prefetch next tile into the other buffer
     const char* kb = smem + cur * 2 * TILE;
     const char* vb = kb + TILE;
     const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
@@ -142,18 +137,27 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
       }
       float mx = -INFINITY;
       const bool need_mask = (kt * BN + BN > Sk) || (CAUSAL && (kt * BN + BN - 1 > q0 + 32 * w + causal_off));
+      if (need_mask) {  // wave-uniform: diagonal / tail tiles only; branch-free select per element
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+        for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          float x = sacc[n][j] * sl;
-          if (need_mask) {
+          for (int j = 0; j < 16; ++j) {
             const int key = kt * BN + n * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;
-            if (key >= Sk || (CAUSAL && key > qrow + causal_off)) x = -INFINITY;
+            const bool dead = (key >= Sk) | (CAUSAL & (key > qrow + causal_off));
+            const float x = dead ? -INFINITY : sacc[n][j] * sl;
+            sacc[n][j] = x;
+            mx = fmaxf(mx, x);
           }
-          sacc[n][j] = x;
-          mx = fmaxf(mx, x);
-        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float x = sacc[n][j] * sl;
+            sacc[n][j] = x;
+            mx = fmaxf(mx, x);
+          }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m_i, mx);
       const float alpha = __builtin_amdgcn_exp2f(m_i - mnew);
@@ -189,8 +193,8 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           }
         }
     }
-    if (kt + 1 < ntiles) swrite((kt + 1) & 1);
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for tile kt+1 landed
+    __syncthreads();                     // ... and every other wave's; buffer cur free again
   }
   const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;

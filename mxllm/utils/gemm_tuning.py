@@ -29,14 +29,20 @@ def enable(path: str = TABLE) -> bool:
     if os.environ.get("MXLLM_GEMM_TUNING", "1") == "0" or not torch.cuda.is_available() or not os.path.exists(path):
         return False
     try:
+        import shutil
+        import tempfile
+
+        # work on a private copy: TunableOp may rewrite its file at exit
+        tmp = os.path.join(tempfile.gettempdir(), f"mxllm_tunableop_{os.getpid()}.csv")
+        shutil.copyfile(path, tmp)
         tun = torch.cuda.tunable
         tun.enable(True)
         tun.tuning_enable(False)
-        tun.record_untuned_enable(False)
-        tun.write_file_on_exit(False)
-        tun.set_filename(path, insert_device_ordinal=False)
-        tun.read_file(path)
-        _ON = True
+        if hasattr(tun, "record_untuned_enable"):
+            tun.record_untuned_enable(False)
+        tun.set_filename(tmp, insert_device_ordinal=False)
+        ok = tun.read_file(tmp)
+        _ON = bool(ok) or ok is None
     except Exception as e:  # noqa: BLE001
         log.warning("TunableOp table not used: %s", e)
         return False
