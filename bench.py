@@ -45,6 +45,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama3.1-70b")
     ap.add_argument("--finetune", choices=["lora", "full"], default="lora")
+    ap.add_argument("--parallel", choices=["ddp", "zero3"], default="ddp",
+                    help="zero3 = sharded params/grads/optimizer (full fine-tuning of 70B on 8 GPUs)")
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--lora-alpha", type=float, default=32.0)
     ap.add_argument("--micro-batch", type=int, default=2)
@@ -79,9 +81,18 @@ def main(argv=None):
     torch.manual_seed(0)
     lora_r = a.lora_r if a.finetune == "lora" else 0
     t0 = time.perf_counter()
-    model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
-                  activation_checkpointing=a.act_ckpt)
-    trainer = Trainer(model, env, OptimConfig(lr=1e-4, weight_decay=0.0, grad_clip=1.0), bucket_mb=a.bucket_mb)
+    opt = OptimConfig(lr=1e-4, weight_decay=0.0, grad_clip=1.0)
+    if a.parallel == "zero3":
+        if a.finetune != "full":
+            raise SystemExit("--parallel zero3 requires --finetune full")
+        from mxllm.parallel.zero3 import Zero3Trainer
+
+        trainer = Zero3Trainer(cfg, env, opt, seed=1234)
+        model = trainer.model
+    else:
+        model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
+                      activation_checkpointing=a.act_ckpt)
+        trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb)
     data = SyntheticTokens(cfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1, rank=env.rank)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -132,7 +143,7 @@ def main(argv=None):
             "model": PRETTY.get(cfg.name, cfg.name) + (f" ({cfg.n_layers} layers)" if a.layers else ""),
             "global_batch": a.micro_batch * a.grad_accum * env.world_size,
             "seq_len": a.seq_len,
-            "parallelism": f"dp{env.world_size}",
+            "parallelism": (f"zero3-dp{env.world_size}" if a.parallel == "zero3" else f"dp{env.world_size}"),
             "finetune": (f"lora r={lora_r} alpha={a.lora_alpha} on q,k,v,o,gate,up,down; frozen bf16 base"
                          if a.finetune == "lora" else "full (bf16 params+grads, fp32 master/Adam)"),
             "micro_batch": a.micro_batch,
@@ -147,7 +158,7 @@ def main(argv=None):
         "peak_hbm_gb": round(peak_gb, 1),
         "init_s": round(init_s, 1),
         "final_loss": round(loss_v, 4),
-        "trainable_params": model.num_params(trainable_only=True),
+        "trainable_params": (cfg.n_params() if a.parallel == "zero3" else model.num_params(trainable_only=True)),
     }
     if env.is_main:
         line = json.dumps(out)
