@@ -40,19 +40,25 @@ __device__ __forceinline__ int swzb(int row) {
 }
 
 // delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]   (token-major inputs)
+// D/8 lanes per row, 16-B loads of both operands, shuffle-reduced (G13).
+template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dO,
                                                              const uint16_t* __restrict__ O,
-                                                             float* __restrict__ delta, int B, int S, int Hq,
-                                                             int D) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*S*Hq (token-major order)
-  const int lane = threadIdx.x & 63;
-  if (row >= (int64_t)B * S * Hq) return;
-  const uint16_t* a = dO + row * D;
-  const uint16_t* c = O + row * D;
+                                                             float* __restrict__ delta, int B, int S, int Hq) {
+  constexpr int LPR = D / 8;  // lanes per row
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;  // over B*S*Hq (token-major order)
+  const int sub = threadIdx.x % LPR;
+  const bool valid = row < (int64_t)B * S * Hq;
   float s = 0.f;
-  for (int d = lane; d < D; d += 64) s += bf2f(a[d]) * bf2f(c[d]);
-  s = wave_sum(s);
-  if (lane == 0) {
+  if (valid) {
+    const u16x8 a = *reinterpret_cast<const u16x8*>(dO + row * D + sub * 8);
+    const u16x8 c = *reinterpret_cast<const u16x8*>(O + row * D + sub * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(c[j]);
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (valid && sub == 0) {
     const int h = (int)(row % Hq);
     const int64_t t = row / Hq;
     const int b = (int)(t / S), q = (int)(t % S);
@@ -314,7 +320,12 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   if (B <= 0 || S <= 0 || Sk <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int64_t rows = (int64_t)B * S * Hq;
-  attn_bwd_delta_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(dout, o, delta, B, S, Hq, D);
+  const int64_t dthreads = rows * (D / 8);
+  const unsigned dgrid = (unsigned)((dthreads + 255) / 256);
+  if (D == 128) attn_bwd_delta_kernel<128><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq);
+  else if (D == 64) attn_bwd_delta_kernel<64><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq);
+  else if (D == 32) attn_bwd_delta_kernel<32><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq);
+  else return -1;
   const int nkb = (Sk + 127) / 128;
   const int grid = nkb * B * Hq;
   const float sl = scale * 1.4426950408889634f;

@@ -18,7 +18,10 @@ TFLOP/s as beta=0 on every Llama-3.1 projection shape):
   backward: g  = s dy B             ; dx  = g A      ; dx += dy W (base GEMM, C = dx)
             dB_i = s dy_i^T t_i (diagonal blocks only) ; dA = g^T x
 Only x and the tiny t are saved for backward; the frozen base weight's
-gradient is never formed.
+gradient is never formed.  The LoRA scale rides in the GEMM alpha, and when
+the trainer has pre-attached flat .grad buffers the adapter gradients are
+accumulated into them by the GEMMs themselves (beta = 1) — no zero-fill,
+cast or accumulate kernels — and DDP is told via ``mark_ready``.
 """
 from __future__ import annotations
 
@@ -27,14 +30,16 @@ from typing import Sequence
 import torch
 import torch.nn.functional as F
 
+from ..parallel.grad_ready import direct_grad, mark_ready
+
 
 class _LoRALinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, a, b, scaling, splits, r):
         x2 = x.reshape(-1, x.shape[-1])
         t = torch.matmul(x2, a.t())  # [T, n*r]
-        ts = t * scaling if scaling != 1.0 else t  # scale the tiny t, not the big output
-        y = torch.matmul(ts, b.t())  # [T, N]   LoRA term first ...
+        y = torch.empty(x2.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        y.addmm_(t, b.t(), beta=0.0, alpha=scaling)  # LoRA term first (scale folded into alpha) ...
         y.addmm_(x2, w.t())  # ... then the base GEMM with C = y (beta = 1)
         ctx.save_for_backward(x2, w, a, b, t)
         ctx.scaling, ctx.splits, ctx.r, ctx.xshape = scaling, tuple(splits), r, x.shape
@@ -45,16 +50,29 @@ class _LoRALinearFn(torch.autograd.Function):
         x2, w, a, b, t = ctx.saved_tensors
         s, r = ctx.scaling, ctx.r
         dy2 = dy.reshape(-1, dy.shape[-1])
-        g = torch.matmul(dy2, b)  # [T, n*r] (block-diagonal B)
-        if s != 1.0:
-            g.mul_(s)
-        db = torch.zeros_like(b)
-        off = 0
-        for i, n_i in enumerate(ctx.splits):
-            db[off:off + n_i, i * r:(i + 1) * r].addmm_(dy2[:, off:off + n_i].t(), t[:, i * r:(i + 1) * r], beta=0.0,
-                                                       alpha=s)
-            off += n_i
-        da = torch.matmul(g.t(), x2)
+        g = torch.empty(dy2.shape[0], a.shape[0], dtype=dy2.dtype, device=dy2.device)
+        g.addmm_(dy2, b, beta=0.0, alpha=s)  # [T, n*r] (block-diagonal B)
+        # adapter grads: accumulate straight into the (flat) .grad buffers when
+        # they exist (trainer-managed), otherwise hand them to autograd
+        ga, gb = direct_grad(a) if ctx.needs_input_grad[2] else None, direct_grad(b) if ctx.needs_input_grad[3] else None
+        da = db = None
+        if ctx.needs_input_grad[2]:
+            if ga is not None:
+                ga.addmm_(g.t(), x2)
+                mark_ready(a)
+            else:
+                da = torch.matmul(g.t(), x2)
+        if ctx.needs_input_grad[3]:
+            tgt = gb if gb is not None else torch.zeros_like(b)
+            off = 0
+            for i, n_i in enumerate(ctx.splits):
+                tgt[off:off + n_i, i * r:(i + 1) * r].addmm_(dy2[:, off:off + n_i].t(), t[:, i * r:(i + 1) * r],
+                                                            beta=1.0 if gb is not None else 0.0, alpha=s)
+                off += n_i
+            if gb is not None:
+                mark_ready(b)
+            else:
+                db = tgt
         dx = torch.matmul(g, a)
         dx.addmm_(dy2, w)  # base dX GEMM with C = g A (beta = 1)
         return dx.view(ctx.xshape), None, da, db, None, None, None

@@ -31,12 +31,13 @@ log = logging.getLogger("mxllm.ddp")
 
 
 class Bucket:
-    __slots__ = ("start", "end", "pending", "expected", "work", "index")
+    __slots__ = ("start", "end", "pending", "expected", "work", "index", "seen")
 
     def __init__(self, index: int, start: int, end: int, expected: int):
         self.index, self.start, self.end, self.expected = index, start, end, expected
         self.pending = expected
         self.work = None
+        self.seen = set()
 
 
 class DDP:
@@ -67,15 +68,23 @@ class DDP:
         self._hooks = []
         if self.enabled:
             for p, bi in zip(flat.param_list, self._param_bucket):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
+                hook = self._make_hook(bi)
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                p._mx_on_grad_ready = hook  # ops that accumulate grads themselves (fused LoRA)
         log.debug("DDP: %d buckets over %d params (%.1f MB), world=%d", len(self.buckets), len(slots),
                   flat.numel * esz / 2 ** 20, self.world)
 
     def _make_hook(self, bi: int):
+        # idempotent per parameter per step: a parameter whose gradient an op
+        # accumulated itself (mark_ready) may ALSO trigger the post-accumulate
+        # hook (autograd runs it even for a None gradient)
         def hook(p):
             if not self._sync:
                 return
             b = self.buckets[bi]
+            if id(p) in b.seen:
+                return
+            b.seen.add(id(p))
             b.pending -= 1
             if b.pending == 0:
                 self._launch(b)
@@ -108,12 +117,14 @@ class DDP:
                 b.work.wait()
             b.work = None
             b.pending = b.expected
+            b.seen.clear()
         return 1.0 / self.world
 
     def reset(self):
         for b in self.buckets:
             b.work = None
             b.pending = b.expected
+            b.seen.clear()
 
     def broadcast_params(self, src: int = 0):
         """Make every rank start from rank ``src``'s trainable parameters."""
@@ -126,3 +137,6 @@ class DDP:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for p in self.flat.param_list:
+            if hasattr(p, "_mx_on_grad_ready"):
+                del p._mx_on_grad_ready
