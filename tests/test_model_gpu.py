@@ -145,3 +145,27 @@ def test_bench_contract_tiny(gpu, tmp_path):
               "vs_baseline", "dtype", "data", "config"):
         assert k in j
     assert j["value"] > 0 and j["n_gpus"] == 1
+
+
+def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
+    """Rehearse the multi-rank bench path (DDP hooks, bucketed all-reduce of GPU
+    grads, barrier, max-over-ranks timing) with 2 ranks sharing the one GPU of
+    the test box over gloo (RCCL needs one GPU per rank)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "b2.json"
+    env = dict(os.environ, MXLLM_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--model", "tiny-d128", "--steps", "2", "--warmup", "1", "--seq-len", "256",
+                        "--json-out", str(out)], cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(out.read_text())
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["value"] > 0
