@@ -65,6 +65,8 @@ class RunConfig:
     resume: bool = True
     log_every: int = 10
     metrics_file: str = ""
+    check_sync_every: int = 0  # desync check of DDP replicas: 0 = once after init/resume, N = also every N steps, -1 = off
+    profile_ranges: bool = True  # roctx ranges around train-step phases (rocprofv3 --marker-trace)
     # fault injection (tests / drills)
     fault_rank: int = -1
     fault_step: int = -1

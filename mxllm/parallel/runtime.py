@@ -43,6 +43,7 @@ class DistEnv:
 
 
 _ENV: DistEnv | None = None
+_SMALL = None  # XgmiComm for latency-bound collectives (xgmi.py), when usable
 
 
 def env_int(name: str, default: int) -> int:
@@ -102,8 +103,19 @@ def init(backend: str | None = None, timeout_s: float | None = None, rank: int |
                 dist.barrier(device_ids=[device.index])
             else:
                 dist.barrier()
+        if backend == "nccl" and device.type == "cuda":
+            global _SMALL
+            from . import xgmi
+
+            _SMALL = xgmi.create(device)
+            log.debug("[rank %d] small-message collectives: %s", rank, "xGMI peer memory" if _SMALL else "RCCL")
     _ENV = e
     return e
+
+
+def small_comm():
+    """The xGMI peer-memory communicator (or None: use torch.distributed)."""
+    return _SMALL
 
 
 def _attempt_store(rank: int, world_size: int, timeout_s: float):
@@ -125,7 +137,13 @@ def get_env() -> DistEnv:
 
 def cleanup() -> None:
     """Destroy the process group if one exists (idempotent)."""
-    global _ENV
+    global _ENV, _SMALL
+    if _SMALL is not None:
+        try:
+            _SMALL.close()
+        except Exception as e:  # noqa: BLE001
+            log.warning("closing xGMI communicator failed: %s", e)
+        _SMALL = None
     if dist.is_available() and dist.is_initialized():
         try:
             dist.destroy_process_group()
@@ -148,7 +166,25 @@ def all_reduce_scalars(vals: list[float], op: str = "sum", device=None) -> list[
     if not dist.is_initialized():
         return list(vals)
     e = get_env()
+    if _SMALL is not None and len(vals) <= _SMALL.max_elems:
+        t = torch.tensor(vals, dtype=torch.float32, device=e.device)
+        _SMALL.all_reduce_(t, op)
+        out = t.tolist()
+        _SMALL.check()
+        return out
     t = torch.tensor(vals, dtype=torch.float64 if e.backend == "gloo" else torch.float32,
                      device=device or e.device)
     dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
     return t.tolist()
+
+
+def all_reduce_small_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """In-place all-reduce of a small device tensor without a host sync
+    (xGMI one-shot kernel when available, else torch.distributed)."""
+    if not dist.is_initialized():
+        return t
+    if (_SMALL is not None and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+            and t.numel() <= _SMALL.max_elems):
+        return _SMALL.all_reduce_(t, op)
+    dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+    return t

@@ -12,11 +12,21 @@ runs the MFMA flash-attention kernel; decode runs the split-K decode kernel
 (one workgroup streams 256 cached keys of one (sequence, kv-head) and serves
 all q-heads of that GQA group).  Scheduling is continuous batching: new
 requests are prefilled between decode steps and join the running batch.
+
+Decode is launch-bound at small batch (a 32-layer step is ~300 kernel
+launches), so on GPU each decode step is replayed from a hipGraph
+(``torch.cuda.CUDAGraph`` is hipGraph capture on ROCm).  One graph per
+(batch bucket, key-split bucket): the batch is padded to a power of two with
+entries that write into a scratch cache slot, the split-K decode kernel gets
+a power-of-two key bound (splits past a sequence's length exit at once), and
+the step's only host->device traffic is one [3, B] int64 copy of
+(token, position, slot).
 """
 from __future__ import annotations
 
 import itertools
 import logging
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -55,15 +65,23 @@ class Request:
 
 
 class Engine:
-    def __init__(self, model, max_batch: int = 8, max_seq: int = 4096, device=None, eos_ids=()):
+    def __init__(self, model, max_batch: int = 8, max_seq: int = 4096, device=None, eos_ids=(),
+                 use_graphs: bool | None = None):
         self.model = model
         self.cfg = model.cfg
         self.device = device or model.tok_emb.device
         self.max_batch = max_batch
         self.max_seq = min(max_seq, self.cfg.max_seq_len)
+        if use_graphs is None:
+            use_graphs = self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_GRAPHS", "1") != "0"
+        self.use_graphs = bool(use_graphs)
+        self._graphs: dict = {}
+        self._pool = None
+        self.scratch_slot = max_batch  # padding rows of a graphed step write here
         c = self.cfg
         dt = model.tok_emb.dtype
-        self.k_cache = [torch.zeros(max_batch, c.n_kv_heads, self.max_seq, c.head_dim, dtype=dt, device=self.device)
+        n_slots = max_batch + (1 if self.use_graphs else 0)
+        self.k_cache = [torch.zeros(n_slots, c.n_kv_heads, self.max_seq, c.head_dim, dtype=dt, device=self.device)
                         for _ in range(c.n_layers)]
         self.v_cache = [torch.zeros_like(k) for k in self.k_cache]
         self.eos_ids = tuple(eos_ids) if eos_ids else (c.eos_id,)
@@ -117,20 +135,81 @@ class Engine:
     @torch.no_grad()
     def decode(self, slots: list[int], tokens: torch.Tensor) -> torch.Tensor:
         """One token for each sequence in ``slots``; returns logits [B, V]."""
-        m, c = self.model, self.cfg
-        pos = torch.tensor([self.lens[s] for s in slots], dtype=torch.int32, device=self.device)
-        sl = torch.tensor(slots, dtype=torch.int32, device=self.device)
+        B = len(slots)
         max_len = max(self.lens[s] for s in slots) + 1
-        x = ops.embedding(tokens, m.tok_emb)
+        if self.use_graphs:
+            logits = self._decode_graphed(slots, tokens, max_len)
+        else:
+            inp = torch.stack([tokens.to(self.device, torch.long),
+                               torch.tensor([self.lens[s] for s in slots], device=self.device),
+                               torch.tensor(slots, device=self.device)])
+            logits = self._decode_body(inp, max_len)
+        for s in slots:
+            self.lens[s] += 1
+        return logits[:B]
+
+    def _decode_body(self, inp: torch.Tensor, max_len: int) -> torch.Tensor:
+        """inp int64 [3, B] = (token, position of the new token, cache slot)."""
+        m, c = self.model, self.cfg
+        pos = inp[1].to(torch.int32)
+        sl = inp[2].to(torch.int32)
+        x = ops.embedding(inp[0], m.tok_emb)
 
         def attn(i, qkv):
             return dops.decode_attention(qkv, m.rope_cos, m.rope_sin, self.k_cache[i], self.v_cache[i], pos, sl,
                                          c.n_heads, c.n_kv_heads, c.head_dim, max_len)
 
         xn = self._layers(x, attn)
-        for s in slots:
-            self.lens[s] += 1
         return torch.matmul(xn, m.head_weight.t())
+
+    def _buckets(self, B: int, max_len: int) -> tuple[int, int]:
+        bb = 1
+        while bb < B:
+            bb *= 2
+        bb = min(bb, self.max_batch)
+        ns, cap = (max_len + 255) // 256, (self.max_seq + 255) // 256
+        nb = 1
+        while nb < ns:
+            nb *= 2
+        return bb, min(nb, cap) * 256
+
+    def _decode_graphed(self, slots: list[int], tokens: torch.Tensor, max_len: int) -> torch.Tensor:
+        B = len(slots)
+        bb, kl = self._buckets(B, max_len)
+        entry = self._graphs.get((bb, kl))
+        if entry is None:
+            entry = self._capture(bb, kl)
+        inp, out, graph, host = entry
+        # the previous step's copy from ``host`` has completed: its logits were
+        # read back (sampling) before this step was scheduled
+        host[0, :B] = tokens.to("cpu", torch.long)
+        host[1, :B] = torch.tensor([self.lens[s] for s in slots])
+        host[2, :B] = torch.tensor(slots)
+        host[0, B:] = 0
+        host[1, B:] = 0
+        host[2, B:] = self.scratch_slot
+        inp.copy_(host, non_blocking=True)
+        graph.replay()
+        return out
+
+    def _capture(self, bb: int, kl: int):
+        inp = torch.zeros(3, bb, dtype=torch.long, device=self.device)
+        inp[2].fill_(self.scratch_slot)  # warm-up / capture traffic goes to the scratch slot
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # library handles / workspace set up outside capture
+                self._decode_body(inp, kl)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=self._pool, capture_error_mode="thread_local"):
+            out = self._decode_body(inp, kl)
+        host = torch.empty(3, bb, dtype=torch.long, pin_memory=True)
+        self._graphs[(bb, kl)] = (inp, out, graph, host)
+        log.debug("captured decode graph: batch %d, key bound %d", bb, kl)
+        return self._graphs[(bb, kl)]
 
     # ------------------------------------------------------------------ scheduling
     def submit(self, prompt: list[int], params: SamplingParams | None = None) -> Request:

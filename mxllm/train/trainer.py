@@ -18,6 +18,7 @@ from .. import ops
 from ..parallel.ddp import DDP
 from ..parallel.flat import FlatParams
 from ..parallel.runtime import DistEnv
+from ..utils.profiling import range_
 
 log = logging.getLogger("mxllm.train")
 
@@ -72,12 +73,20 @@ class Trainer:
             last = i == n - 1
             ctx = self.ddp.no_sync() if not last else _null()
             with ctx:
-                loss = self.model(ids, labels)
-                (loss / n if n > 1 else loss).backward()
+                with range_("forward"):
+                    loss = self.model(ids, labels)
+                with range_("backward"):
+                    (loss / n if n > 1 else loss).backward()
             total = loss.detach() if total is None else total + loss.detach()
         self.flat.sync_grads_from_params()
-        scale = self.ddp.finish() / n if n > 1 else self.ddp.finish()
+        with range_("grad_allreduce_wait"):
+            scale = self.ddp.finish() / n if n > 1 else self.ddp.finish()
         self.step_num += 1
+        with range_("optimizer"):
+            self._optimizer_step(scale)
+        return total / n
+
+    def _optimizer_step(self, scale: float):
         o = self.opt
         if o.grad_clip and o.grad_clip > 0:
             # global grad norm on device; the clip coefficient is applied inside
@@ -93,7 +102,6 @@ class Trainer:
                         beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
                         step=self.step_num, grad_scale=gscale)
         self.flat.zero_grad()
-        return total / n
 
     # ------------------------------------------------------------------ state
     def state_dict(self) -> dict:

@@ -95,6 +95,11 @@ def main(argv=None):
                 loader.restore(extra["loader"])
                 start = trainer.step_num
                 logging.info(f"Resumed at step {start}")
+        sync_check = run.check_sync_every >= 0 and run.parallel == "ddp"
+        if sync_check:
+            from mxllm.parallel.consistency import check_in_sync
+
+            check_in_sync(trainer.flat.params, what="initial trainable parameters")
         metrics = MetricsWriter(run.metrics_file or None, rank)
         tok_per_step = run.micro_batch * run.seq_len * run.grad_accum * world_size
         t_last, n_since = time.perf_counter(), 0
@@ -120,6 +125,8 @@ def main(argv=None):
                     logging.info(f"step {step} epoch {epoch} loss {lv:.4f} grad_norm {gn:.3f} tokens/s {tps:.0f}")
                 metrics.write(step=step, epoch=epoch, loss=lv, grad_norm=gn, tokens_per_s=tps)
                 t_last, n_since = time.perf_counter(), 0
+            if sync_check and run.check_sync_every > 0 and (step + 1) % run.check_sync_every == 0:
+                check_in_sync(trainer.flat.params, what=f"trainable parameters after step {step}")
             if run.ckpt_dir and run.save_every and (step + 1) % run.save_every == 0:
                 checkpoint.save(run.ckpt_dir, trainer, step + 1, extra={"loader": loader.state()},
                                 sharded=run.parallel == "zero3")
