@@ -158,6 +158,11 @@ def main(argv=None):
         "peak_hbm_gb": round(peak_gb, 1),
         "init_s": round(init_s, 1),
         "final_loss": round(loss_v, 4),
+        "allreduce_mb_per_step": (round(trainer.ddp.bytes_per_step / 2 ** 20, 1)
+                                  if a.parallel == "ddp" and trainer.ddp.enabled else 0.0),
+        "exposed_comm_ms_last_step": (round(trainer.ddp.exposed_comm_ms(), 3)
+                                      if a.parallel == "ddp" and trainer.ddp.enabled and a.steps
+                                      and trainer.ddp.exposed_comm_ms() is not None else None),
         "trainable_params": (cfg.n_params() if a.parallel == "zero3" else model.num_params(trainable_only=True)),
     }
     if env.is_main:

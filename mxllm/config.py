@@ -67,6 +67,9 @@ class RunConfig:
     metrics_file: str = ""
     check_sync_every: int = 0  # desync check of DDP replicas: 0 = once after init/resume, N = also every N steps, -1 = off
     profile_ranges: bool = True  # roctx ranges around train-step phases (rocprofv3 --marker-trace)
+    # inference driver: opt-in gather of every rank's results to rank 0
+    gather_results: bool = False
+    results_file: str = ""  # rank 0 writes the gathered records as JSONL
     # fault injection (tests / drills)
     fault_rank: int = -1
     fault_step: int = -1

@@ -65,6 +65,8 @@ class DDP:
                 b_start, b_count = nxt_end, 0
                 limit = int(bucket_mb * 2 ** 20 / esz)
             del end
+        self._timing = self.enabled
+        self._last_events = None
         self._hooks = []
         if self.enabled:
             for p, bi in zip(flat.param_list, self._param_bucket):
@@ -73,6 +75,10 @@ class DDP:
                 p._mx_on_grad_ready = hook  # ops that accumulate grads themselves (fused LoRA)
         log.debug("DDP: %d buckets over %d params (%.1f MB), world=%d", len(self.buckets), len(slots),
                   flat.numel * esz / 2 ** 20, self.world)
+
+    @property
+    def bytes_per_step(self) -> int:
+        return self.flat.numel * self.flat.grads.element_size() if self.enabled else 0
 
     def _make_hook(self, bi: int):
         # idempotent per parameter per step: a parameter whose gradient an op
@@ -112,13 +118,30 @@ class DDP:
         for b in self.buckets:
             if b.work is None and self._sync:
                 self._launch(b)
+        timing = self._timing and torch.cuda.is_available() and self.flat.grads.is_cuda
+        if timing:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
             b.work = None
             b.pending = b.expected
             b.seen.clear()
+        if timing:
+            e1.record()
+            self._last_events = (e0, e1)
         return 1.0 / self.world
+
+    def exposed_comm_ms(self) -> float | None:
+        """GPU time the compute stream stalled on gradient all-reduce in the
+        last step (communication NOT hidden behind backward).  Syncs on the
+        last step's end event, so read it only at logging points."""
+        if self._last_events is None:
+            return None
+        e0, e1 = self._last_events
+        e1.synchronize()
+        return e0.elapsed_time(e1)
 
     def reset(self):
         for b in self.buckets:

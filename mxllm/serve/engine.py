@@ -96,6 +96,15 @@ class Engine:
         self._stop = False
         self.steps = 0
         self.tokens_generated = 0
+        # latency / throughput counters: exported by the server's
+        # /metrics and by stats()
+        self.prefill_tokens = 0
+        self.prefill_s = 0.0
+        self.decode_s = 0.0
+        self.decode_tokens = 0
+        self.ttft_sum = 0.0
+        self.latency_sum = 0.0
+        self.finished = 0
 
     # ------------------------------------------------------------------ model pieces
     @torch.no_grad()
@@ -219,9 +228,23 @@ class Engine:
             self._cv.notify()
         return r
 
+    def stats(self) -> dict:
+        """Cumulative serving metrics: TTFT / request latency means, prefill and
+        decode throughput (tokens/s of engine wall time)."""
+        n = max(self.finished, 1)
+        return {"requests_finished": self.finished, "tokens_generated": self.tokens_generated,
+                "mean_ttft_s": self.ttft_sum / n, "mean_latency_s": self.latency_sum / n,
+                "prefill_tokens_per_s": self.prefill_tokens / self.prefill_s if self.prefill_s else 0.0,
+                "decode_tokens_per_s": self.decode_tokens / self.decode_s if self.decode_s else 0.0,
+                "decode_steps": self.steps}
+
     def _finish(self, r: Request, reason: str):
         r.finish_reason = reason
         r.t_done = time.perf_counter()
+        self.finished += 1
+        self.latency_sum += r.t_done - r.t_submit
+        if r.t_first is not None:
+            self.ttft_sum += r.t_first - r.t_submit
         if r.slot >= 0:
             self.free_slots.append(r.slot)
             self.active.pop(r.slot, None)
@@ -252,10 +275,13 @@ class Engine:
                 admit.append(r)
         for r in admit:
             try:
+                t0 = time.perf_counter()
                 logits = self.prefill(r.slot, r.prompt)
                 self.active[r.slot] = r
                 tok = int(dops.sample(logits.view(1, -1), r.params.temperature, r.params.seed, 0,
                                       r.params.top_p, r.params.top_k)[0])
+                self.prefill_s += time.perf_counter() - t0
+                self.prefill_tokens += len(r.prompt)
                 self._accept(r, tok)
             except Exception as e:  # noqa: BLE001
                 log.exception("prefill failed")
@@ -265,7 +291,8 @@ class Engine:
             return bool(admit)
         slots = sorted(self.active)
         reqs = [self.active[s] for s in slots]
-        tokens = torch.tensor([r.output[-1] for r in reqs], dtype=torch.long, device=self.device)
+        t0 = time.perf_counter()
+        tokens = torch.tensor([r.output[-1] for r in reqs], dtype=torch.long)
         logits = self.decode(slots, tokens)
         self.steps += 1
         if all(r.params.temperature <= 0 and r.params.top_p >= 1.0 and r.params.top_k == 0 for r in reqs):
@@ -273,6 +300,8 @@ class Engine:
         else:  # per-request RNG stream: (seed, token index) -> reproducible regardless of batching
             nxt = [int(dops.sample(logits[i:i + 1], r.params.temperature, r.params.seed, len(r.output),
                                    r.params.top_p, r.params.top_k)[0]) for i, r in enumerate(reqs)]
+        self.decode_s += time.perf_counter() - t0  # includes the sampling read-back (a sync)
+        self.decode_tokens += len(reqs)
         for r, t in zip(reqs, nxt):
             self._accept(r, int(t))
         return True

@@ -87,7 +87,15 @@ def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = 
         lines = [f"mxllm_requests_total {stats['requests']}", f"mxllm_errors_total {stats['errors']}",
                  f"mxllm_prompt_tokens_total {stats['prompt_tokens']}",
                  f"mxllm_completion_tokens_total {stats['completion_tokens']}",
-                 f"mxllm_engine_steps_total {engine.steps}", f"mxllm_active_sequences {len(engine.active)}"]
+                 f"mxllm_engine_steps_total {engine.steps}", f"mxllm_active_sequences {len(engine.active)}",
+                 f"mxllm_waiting_requests {len(engine.waiting)}",
+                 f"mxllm_ttft_seconds_sum {engine.ttft_sum:.6f}", f"mxllm_ttft_seconds_count {engine.finished}",
+                 f"mxllm_request_latency_seconds_sum {engine.latency_sum:.6f}",
+                 f"mxllm_request_latency_seconds_count {engine.finished}",
+                 f"mxllm_prefill_tokens_total {engine.prefill_tokens}",
+                 f"mxllm_prefill_seconds_total {engine.prefill_s:.6f}",
+                 f"mxllm_decode_tokens_total {engine.decode_tokens}",
+                 f"mxllm_decode_seconds_total {engine.decode_s:.6f}"]
         return PlainTextResponse("\n".join(lines) + "\n")
 
     @app.post("/v1/chat/completions")

@@ -123,7 +123,13 @@ def main(argv=None):
                 gn = float(trainer.last_grad_norm) if getattr(trainer, "last_grad_norm", None) is not None else 0.0
                 if rank == 0:
                     logging.info(f"step {step} epoch {epoch} loss {lv:.4f} grad_norm {gn:.3f} tokens/s {tps:.0f}")
-                metrics.write(step=step, epoch=epoch, loss=lv, grad_norm=gn, tokens_per_s=tps)
+                extra = {}
+                ddp = getattr(trainer, "ddp", None)
+                if ddp is not None and ddp.enabled:
+                    extra = {"allreduce_bytes": ddp.bytes_per_step, "exposed_comm_ms": ddp.exposed_comm_ms()}
+                if env.device.type == "cuda":
+                    extra["peak_hbm_gb"] = torch.cuda.max_memory_allocated(env.device) / 1e9
+                metrics.write(step=step, epoch=epoch, loss=lv, grad_norm=gn, tokens_per_s=tps, **extra)
                 t_last, n_since = time.perf_counter(), 0
             if sync_check and run.check_sync_every > 0 and (step + 1) % run.check_sync_every == 0:
                 check_in_sync(trainer.flat.params, what=f"trainable parameters after step {step}")

@@ -98,6 +98,26 @@ def _configure_client(device):
                             RUN.checkpoint, RUN.seed)
 
 
+def _gather_results(records, rank, world_size):
+    """Opt-in (``--gather-results``): collect every rank's records on rank 0.
+    The reference logs only rank 0's own shard (reference
+    src/distributed_inference.py:71); that stays the default."""
+    if dist.is_initialized() and world_size > 1:
+        allr = [None] * world_size if rank == 0 else None
+        dist.gather_object(records, allr, dst=0)
+    else:
+        allr = [records]
+    if rank == 0:
+        flat = [r for part in allr for r in part]
+        logging.info(f"Gathered {len(flat)} results from {world_size} ranks")
+        if RUN.results_file:
+            import json
+
+            with open(RUN.results_file, "w") as f:
+                for r in flat:
+                    f.write(json.dumps(r) + "\n")
+
+
 def main():
     setup_logging()
     code = 0
@@ -117,6 +137,7 @@ def main():
             custom_dataset, num_replicas=world_size, rank=rank, seed=RUN.seed)
         train_dataloader = DataLoader(custom_dataset, batch_size=RUN.batch_size, sampler=train_sampler)
 
+        records = []
         step = 0
         for epoch in range(RUN.epochs):
             logging.info(f"Starting epoch {epoch}")
@@ -136,7 +157,14 @@ def main():
                         logging.info(f"Response: {response[:n]}...")
                         logging.info(f"Label: {label}")
                         logging.info(f"GPU Result: {gpu_result}\n")
+                if RUN.gather_results:
+                    n = RUN.truncate
+                    records.extend({"rank": rank, "epoch": epoch, "prompt": p[:n], "response": r[:n],
+                                    "label": int(lb), "gpu_result": float(g)}
+                                   for p, r, lb, g in zip(prompts, responses, labels, gpu_results))
                 step += 1
+        if RUN.gather_results:
+            _gather_results(records, rank, world_size)
         if dist.is_initialized():
             runtime.barrier()
     except Exception as e:

@@ -101,18 +101,26 @@ def test_checkpoint_roundtrip(tmp_path, monkeypatch):
 
 
 @pytest.mark.slow
-def test_inference_plumbing_two_ranks():
+def test_inference_plumbing_two_ranks(tmp_path):
     """BASELINE config 1: distributed_inference on the tiny stub, gloo, world 2:
-    every rank sees 125 prompts x 3 epochs; rank 0 logs 375 records."""
+    every rank sees 125 prompts x 3 epochs; rank 0 logs 375 records; the
+    opt-in gather (C9) brings all 750 records, disjoint per epoch, to rank 0."""
+    out = tmp_path / "results.jsonl"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
                         "127.0.0.1", "--master-port", str(_port()), "src/distributed_inference.py"], cwd=ROOT,
-                       env=_env(MXLLM_MAX_NEW_TOKENS=2, MXLLM_MAX_SEQ=256), capture_output=True, text=True,
-                       timeout=600)
+                       env=_env(MXLLM_MAX_NEW_TOKENS=2, MXLLM_MAX_SEQ=256, MXLLM_GATHER_RESULTS=1,
+                                MXLLM_RESULTS_FILE=str(out)), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     log = r.stdout + r.stderr
     assert log.count("Prompt: ") == 375
     assert log.count("Starting epoch") == 6
     assert "An error occurred" not in log
+    assert "Gathered 750 results from 2 ranks" in log
+    import json
+
+    recs = [json.loads(x) for x in out.read_text().splitlines()]
+    assert len(recs) == 750
+    assert sum(1 for x in recs if x["rank"] == 1) == 375
 
 
 def test_two_node_emulation_finetune():

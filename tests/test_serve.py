@@ -43,6 +43,15 @@ def test_continuous_batching_is_order_independent(tiny_engine):
     assert batched == single
 
 
+def test_engine_serving_stats(tiny_engine):
+    before = tiny_engine.stats()["requests_finished"]
+    tiny_engine.generate([[1, 2, 3], [4, 5]], max_new_tokens=4)
+    st = tiny_engine.stats()
+    assert st["requests_finished"] == before + 2
+    assert st["mean_ttft_s"] > 0 and st["mean_latency_s"] >= st["mean_ttft_s"]
+    assert st["decode_tokens_per_s"] > 0 and st["prefill_tokens_per_s"] > 0
+
+
 def test_sampling_temperature_reproducible(tiny_engine):
     a = tiny_engine.generate([[3, 4, 5]], max_new_tokens=8, temperature=1.0, seed=7)
     b = tiny_engine.generate([[3, 4, 5]], max_new_tokens=8, temperature=1.0, seed=7)
