@@ -288,7 +288,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
 std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q,
                                                              const at::Tensor& k, const at::Tensor& v,
                                                              const at::Tensor& o, const at::Tensor& lse, int causal,
-                                                             double scale) {
+                                                             double scale, bool deterministic = false) {
   check_bf16(dout, "dout");
   check_bf16(o, "o");
   check_f32(lse, "lse");
@@ -297,21 +297,32 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
   MX_CHECK(dout.numel() == B * S * Hq * D && o.numel() == dout.numel(), "dout/o shape");
   DevGuard g(q.device());
   const int64_t S_pad = (S + 63) / 64 * 64;
-  auto dq_pad = at::zeros({B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
   auto dkp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
   auto dvp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  if (deterministic && causal >= 0) {
+    // per-key-block dQ partials, summed in a fixed order (no atomics)
+    const int64_t nkb = (Sk + 127) / 128;
+    auto part = at::empty({nkb, B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
+    auto dq = at::empty({B, Hq, S, D}, q.options().dtype(at::kFloat));
+    MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                      dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
+                      (int)S, (int)Sk, (int)D, causal, (float)scale, part.data_ptr<float>(), cur_stream()));
+    return {dq, dkp, dvp};
+  }
+  auto dq_pad = at::zeros({B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
   MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                     dq_pad.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                    (int)S, (int)Sk, (int)D, causal, (float)scale, cur_stream()));
+                    (int)S, (int)Sk, (int)D, causal, (float)scale, nullptr, cur_stream()));
   auto dq = S_pad == S ? dq_pad : dq_pad.narrow(2, 0, S).contiguous();
   return {dq, dkp, dvp};
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q,
                                                         const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
-                                                        const at::Tensor& lse, bool causal, double scale) {
-  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale);
+                                                        const at::Tensor& lse, bool causal, double scale,
+                                                        bool deterministic) {
+  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, deterministic);
 }
 
 // timing-only ablation variants (mode: -1 = causal without dQ atomics)
@@ -394,7 +405,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale) -> (Tensor, Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, bool deterministic=False) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {

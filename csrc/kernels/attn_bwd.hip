@@ -66,7 +66,11 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
   }
 }
 
-template <int D, bool CAUSAL, bool ATOMIC = true>
+// DQM: dQ hand-off mode. 1 = f32 atomics into dQ [B,Hq,S_pad,D] (default);
+// 2 = deterministic: plain stores of this key block's dQ partial into
+//     dQ + kb * B*Hq*S_pad*D, summed in key-block order by attn_bwd_dq_reduce;
+// 0 = dropped (ablation timing only).
+template <int D, bool CAUSAL, int DQM = 1>
 __global__ void __launch_bounds__(256, 1)
 attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -102,7 +106,8 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const uint16_t* dOp = dO + (size_t)b * S * dstride + (size_t)h * D;
   const float* lsep = LSE + (size_t)(b * Hq + h) * S;
   const float* delp = DELTA + (size_t)(b * Hq + h) * S;
-  float* dQp = dQ + (size_t)(b * Hq + h) * S_pad * D;  // rows padded to S_pad: atomics need no guard
+  // rows padded to S_pad: the tail tile's atomics / stores need no guard
+  float* dQp = dQ + (DQM == 2 ? (size_t)kb * BH * S_pad * D : 0) + (size_t)(b * Hq + h) * S_pad * D;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -163,7 +168,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   f32x16 pend[NT];  // dQ tile of the previous iteration, added after the next barrier
   int pend_q0 = -1;
   auto flush_dq = [&]() {
-    if (!ATOMIC || pend_q0 < 0) return;
+    if (DQM == 0 || pend_q0 < 0) return;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int tile = w + 4 * t;
@@ -172,7 +177,8 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int q = pend_q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
-          atomicAdd(dQp + (size_t)q * D + db * 32 + r, pend[t][j]);
+          if constexpr (DQM == 2) dQp[(size_t)q * D + db * 32 + r] = pend[t][j];
+          else atomicAdd(dQp + (size_t)q * D + db * 32 + r, pend[t][j]);
         }
       }
     }
@@ -283,7 +289,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
                         u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc);
         }
         pend[t] = acc * scale;
-        if constexpr (!ATOMIC) asm volatile("" ::"v"(pend[t][0]));
+        if constexpr (DQM == 0) asm volatile("" ::"v"(pend[t][0]));
       }
     }
     pend_q0 = q0;
@@ -308,15 +314,41 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   }
 }
 
+// Deterministic dQ: dq[b,h,q,:] = sum over the key blocks that visited q (ascending kb)
+// of the partials written by attn_bwd_kernel<.., DQM=2>.  One thread per 4 floats.
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_bwd_dq_reduce(const float* __restrict__ part, float* __restrict__ dq,
+                                                          int BH, int S, int S_pad, int nkb, int off) {
+  constexpr int V = D / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)BH * S * V) return;
+  const int c = (int)(i % V);
+  const int64_t row = i / V;
+  const int q = (int)(row % S);
+  const int64_t bh = row / S;
+  const size_t kstride = (size_t)BH * S_pad * D;
+  const float* p = part + ((size_t)bh * S_pad + q) * D + 4 * c;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (CAUSAL && max(0, (kb * 128 - off) / 64 * 64) > q) break;  // key blocks past q never visited it
+    acc += *reinterpret_cast<const f32x4*>(p + kb * kstride);
+  }
+  *reinterpret_cast<f32x4*>(dq + row * D + 4 * c) = acc;
+}
+
 }  // namespace mx
 
 using namespace mx;
 
 // dq [B,Hq,ceil(S/64)*64,D] f32 must be ZEROED by the caller (f32 atomics; padded rows absorb
 // the unguarded tail atomics).  delta: workspace [B,Hq,S].
+// Deterministic mode (dq_part != nullptr): dq_part is a workspace of
+// ceil(Sk/128) * B*Hq*ceil(S/64)*64*D floats (no zeroing needed) and dq receives the
+// result unpadded, [B,Hq,S,D], reduced in a fixed order (bitwise reproducible).
 extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
                            const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
-                           int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream) {
+                           int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, float* dq_part,
+                           hipStream_t stream) {
   if (B <= 0 || S <= 0 || Sk <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int64_t rows = (int64_t)B * S * Hq;
@@ -331,18 +363,39 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
   const int S_pad = (S + 63) / 64 * 64;  // dq rows are padded (see mx_attn_bwd contract)
-#define BWD(DD, C)                                                                                          \
-  attn_bwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv, S, Sk, \
-                                                   off, sl, scale, S_pad)
   if (causal < 0) {  // ablation: no dQ atomics (timing experiments only; dq left zero)
-    attn_bwd_kernel<128, true, false><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv,
-                                                                S, Sk, off, sl, scale, S_pad);
+    attn_bwd_kernel<128, true, 0><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv,
+                                                            S, Sk, off, sl, scale, S_pad);
     return (int)hipGetLastError();
   }
+  const bool det = dq_part != nullptr;
+  float* dqk = det ? dq_part : dq;
+#define BWD(DD, C)                                                                                                  \
+  do {                                                                                                              \
+    if (det)                                                                                                        \
+      attn_bwd_kernel<DD, C, 2><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dqk, dkp, dvp, B, Hq, Hkv, S,  \
+                                                          Sk, off, sl, scale, S_pad);                               \
+    else                                                                                                            \
+      attn_bwd_kernel<DD, C, 1><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dqk, dkp, dvp, B, Hq, Hkv, S,  \
+                                                          Sk, off, sl, scale, S_pad);                               \
+  } while (0)
   if (D == 128) { if (causal) BWD(128, true); else BWD(128, false); }
   else if (D == 64) { if (causal) BWD(64, true); else BWD(64, false); }
   else if (D == 32) { if (causal) BWD(32, true); else BWD(32, false); }
   else return -1;
 #undef BWD
+  if (det) {
+    const int64_t n = (int64_t)B * Hq * S * (D / 4);
+    const unsigned rg = (unsigned)((n + 255) / 256);
+#define RED(DD)                                                                                                   \
+  do {                                                                                                            \
+    if (causal) attn_bwd_dq_reduce<DD, true><<<rg, 256, 0, stream>>>(dq_part, dq, B * Hq, S, S_pad, nkb, off);    \
+    else attn_bwd_dq_reduce<DD, false><<<rg, 256, 0, stream>>>(dq_part, dq, B * Hq, S, S_pad, nkb, off);          \
+  } while (0)
+    if (D == 128) RED(128);
+    else if (D == 64) RED(64);
+    else RED(32);
+#undef RED
+  }
   return (int)hipGetLastError();
 }

@@ -180,6 +180,27 @@ def test_attention_fwd_bwd(gpu, B, Hq, Hkv, S, Sk, D, causal):
     assert rel_err(dv, vf.grad) < 3e-2
 
 
+@pytest.mark.parametrize("causal,S", [(True, 2048), (True, 200), (False, 333)])
+def test_attention_bwd_deterministic(gpu, causal, S):
+    """Deterministic dQ (per-key-block partials, ordered reduction): bitwise
+    identical across runs, and equal to the atomic path up to f32 reordering."""
+    torch.manual_seed(21)
+    B, Hq, Hkv, D = 1, 8, 2, 128
+    q = torch.randn(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    sc = 1 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, causal, sc)
+    do = torch.randn(B, S, Hq * D, device=gpu, dtype=torch.bfloat16)
+    r1 = _ops().attn_bwd(do, q, k, v, o, lse, causal, sc, True)
+    r2 = _ops().attn_bwd(do, q, k, v, o, lse, causal, sc, True)
+    ra = _ops().attn_bwd(do, q, k, v, o, lse, causal, sc, False)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(r1[0], ra[0], rtol=1e-4, atol=1e-4)
+    assert torch.equal(r1[1], ra[1]) and torch.equal(r1[2], ra[2])
+
+
 def test_attention_block_autograd(gpu):
     """Full split+rope+attention autograd node vs the reference path."""
     from mxllm.ops.attention import attention_block
