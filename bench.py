@@ -118,6 +118,11 @@ def main(argv=None):
     runtime.barrier()
     sync()
     elapsed = time.perf_counter() - t_start
+    gpu_sample = {}
+    if dev.type == "cuda" and os.environ.get("MXLLM_BENCH_SMI", "1") != "0":
+        from mxllm.utils.gpumon import sample_device
+
+        gpu_sample = sample_device(dev.index)  # clocks / power right after the timed steps
     elapsed = runtime.all_reduce_scalars([elapsed], op="max")[0]
     loss_v = float(loss.float().item()) if a.steps or a.warmup else float("nan")
     tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size
@@ -163,6 +168,8 @@ def main(argv=None):
         "exposed_comm_ms_last_step": (round(trainer.ddp.exposed_comm_ms(), 3)
                                       if a.parallel == "ddp" and trainer.ddp.enabled and a.steps
                                       and trainer.ddp.exposed_comm_ms() is not None else None),
+        "gpu_after_timed_steps": {k: gpu_sample[k] for k in ("gfx_clock_mhz", "socket_power_w", "temp_hotspot_c")
+                                  if k in gpu_sample},
         "trainable_params": (cfg.n_params() if a.parallel == "zero3" else model.num_params(trainable_only=True)),
     }
     if env.is_main:

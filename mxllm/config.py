@@ -65,6 +65,7 @@ class RunConfig:
     resume: bool = True
     log_every: int = 10
     metrics_file: str = ""
+    gpu_monitor_s: float = 0.0  # AMD SMI sampling period into the metrics file (0 = off)
     check_sync_every: int = 0  # desync check of DDP replicas: 0 = once after init/resume, N = also every N steps, -1 = off
     profile_ranges: bool = True  # roctx ranges around train-step phases (rocprofv3 --marker-trace)
     # inference driver: opt-in gather of every rank's results to rank 0

@@ -101,6 +101,12 @@ def main(argv=None):
 
             check_in_sync(trainer.flat.params, what="initial trainable parameters")
         metrics = MetricsWriter(run.metrics_file or None, rank)
+        monitor = None
+        if run.gpu_monitor_s > 0 and run.metrics_file and env.device.type == "cuda":
+            from mxllm.utils.gpumon import GpuMonitor
+
+            gpu_log = MetricsWriter(run.metrics_file, rank, all_ranks=True)
+            monitor = GpuMonitor(env.device, run.gpu_monitor_s, lambda smp: gpu_log.write(kind="gpu", **smp)).start()
         tok_per_step = run.micro_batch * run.seq_len * run.grad_accum * world_size
         t_last, n_since = time.perf_counter(), 0
         for step in range(start, total):
@@ -137,6 +143,8 @@ def main(argv=None):
                 checkpoint.save(run.ckpt_dir, trainer, step + 1, extra={"loader": loader.state()},
                                 sharded=run.parallel == "zero3")
         loader.close()
+        if monitor is not None:
+            monitor.stop()
         runtime.barrier()
     except Exception as e:
         logging.error(f"An error occurred in the main function: {e}")

@@ -213,3 +213,27 @@ def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(out.read_text())
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["value"] > 0
+
+
+def test_gpu_monitor_samples(gpu):
+    """AMD SMI monitor (A7): the bound device is found by PCI id and reports
+    memory / activity fields; the background sampler delivers samples."""
+    import threading
+
+    from mxllm.utils.gpumon import GpuMonitor, sample_device
+
+    s = sample_device(gpu.index)
+    print("gpu sample:", s)
+    assert s and ("vram_total_mb" in s or "gfx_activity_pct" in s), s
+    got = []
+    ev = threading.Event()
+
+    def cb(x):
+        got.append(x)
+        if len(got) >= 2:
+            ev.set()
+
+    mon = GpuMonitor(gpu, 0.05, cb).start()
+    ev.wait(10)
+    mon.stop()
+    assert len(got) >= 2 and "hbm_allocated_gb" in got[0]
