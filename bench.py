@@ -70,6 +70,9 @@ def main(argv=None):
     from mxllm.train.trainer import OptimConfig, Trainer
     from mxllm.data import SyntheticTokens
 
+    # the timed step issues no small collectives, so the bench keeps RCCL for its
+    # two bookkeeping reductions (MXLLM_XGMI=1 opts into the peer-memory path)
+    os.environ.setdefault("MXLLM_XGMI", "0")
     env = runtime.init()
     dev = env.device
     from mxllm.utils import gemm_tuning

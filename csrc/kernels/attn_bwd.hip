@@ -167,6 +167,11 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 
   f32x16 pend[NT];  // dQ tile of the previous iteration, added after the next barrier
   int pend_q0 = -1;
+  // dQ hand-off through a buffer descriptor: the per-lane part of the address is
+  // loop-invariant (voff), the tile / row-group part is wave-uniform (soffset,
+  // SALU) and the row-in-group part an immediate -> no VALU address math per atomic
+  const __amdgpu_buffer_rsrc_t dq_rsrc = __builtin_amdgcn_make_buffer_rsrc(dQp, 0, 0x7fffffff, 0x00020000);
+  const int dq_voff = ((4 * hh) * D + r) * 4;
   auto flush_dq = [&]() {
     if (DQM == 0 || pend_q0 < 0) return;
 #pragma unroll
@@ -176,9 +181,14 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         const int m = tile / DB, db = tile % DB;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const int q = pend_q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
-          if constexpr (DQM == 2) dQp[(size_t)q * D + db * 32 + r] = pend[t][j];
-          else atomicAdd(dQp + (size_t)q * D + db * 32 + r, pend[t][j]);
+          // q = pend_q0 + 32m + (j&3) + 8(j>>2) + 4hh ; column db*32 + r
+          const int soff = ((pend_q0 + 32 * m + 8 * (j >> 2)) * D + db * 32) * 4;
+          const int ioff = (j & 3) * D * 4;
+          if constexpr (DQM == 2)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pend[t][j]), dq_rsrc,
+                                                      dq_voff + ioff, soff, 0);
+          else
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(pend[t][j], dq_rsrc, dq_voff + ioff, soff, 0);
         }
       }
     }
