@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--act-ckpt", action="store_true", help="activation checkpointing per layer")
+    ap.add_argument("--sp", type=int, default=1,
+                    help="sequence-parallel degree (Ulysses all-to-all around attention; long-context runs)")
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--device", default=None, help="force 'cpu' for a plumbing run")
     ap.add_argument("--layers", type=int, default=None, help="override n_layers (NOT valid for the headline)")
@@ -96,13 +98,23 @@ def main(argv=None):
         model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
                       activation_checkpointing=a.act_ckpt)
         trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb)
-    data = SyntheticTokens(cfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1, rank=env.rank)
+    sp_group, data_rank = None, env.rank
+    if a.sp > 1:
+        if a.parallel != "ddp":
+            raise SystemExit("--sp is supported with --parallel ddp")
+        from mxllm.parallel.sequence import new_groups, shard_sequence
+
+        sp_group, data_rank, _ = new_groups(a.sp)
+        model.set_sequence_parallel(sp_group)
+    data = SyntheticTokens(cfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1, rank=data_rank)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     init_s = time.perf_counter() - t0
 
     def step():
         mbs = [data.next() for _ in range(a.grad_accum)]
+        if sp_group is not None:  # every rank of an SP group gets the same sequences, keeps its slice
+            mbs = [(shard_sequence(i, sp_group), shard_sequence(l, sp_group)) for i, l in mbs]
         return trainer.train_step(mbs)
 
     def sync():
@@ -128,7 +140,7 @@ def main(argv=None):
         gpu_sample = sample_device(dev.index)  # clocks / power right after the timed steps
     elapsed = runtime.all_reduce_scalars([elapsed], op="max")[0]
     loss_v = float(loss.float().item()) if a.steps or a.warmup else float("nan")
-    tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size
+    tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size // a.sp
     tps = tokens_per_step * a.steps / elapsed if a.steps else 0.0
     ms = 1e3 * elapsed / max(1, a.steps)
     peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else 0.0
@@ -149,9 +161,10 @@ def main(argv=None):
         "data": "synthetic (random token ids, random-init weights)",
         "config": {
             "model": PRETTY.get(cfg.name, cfg.name) + (f" ({cfg.n_layers} layers)" if a.layers else ""),
-            "global_batch": a.micro_batch * a.grad_accum * env.world_size,
+            "global_batch": a.micro_batch * a.grad_accum * env.world_size // a.sp,
             "seq_len": a.seq_len,
-            "parallelism": (f"zero3-dp{env.world_size}" if a.parallel == "zero3" else f"dp{env.world_size}"),
+            "parallelism": (f"zero3-dp{env.world_size}" if a.parallel == "zero3" else
+                            (f"dp{env.world_size // a.sp}-sp{a.sp}" if a.sp > 1 else f"dp{env.world_size}")),
             "finetune": (f"lora r={lora_r} alpha={a.lora_alpha} on q,k,v,o,gate,up,down; frozen bf16 base"
                          if a.finetune == "lora" else "full (bf16 params+grads, fp32 master/Adam)"),
             "micro_batch": a.micro_batch,

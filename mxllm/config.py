@@ -48,6 +48,7 @@ class RunConfig:
     model: str = "tiny"
     finetune: str = "lora"  # lora | full
     parallel: str = "ddp"  # ddp | zero3
+    sequence_parallel: int = 1  # Ulysses SP degree (ranks per sequence); world = dp x sp
     lora_r: int = 16
     lora_alpha: float = 32.0
     lr: float = 1e-4

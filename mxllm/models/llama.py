@@ -91,6 +91,7 @@ class Llama(nn.Module):
         self.lora = lora_r > 0
         train_base = not self.lora
         self.activation_checkpointing = activation_checkpointing
+        self.seq_parallel = None  # UlyssesAttention when the sequence is sharded (set_sequence_parallel)
         self.tok_emb = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, dtype=dtype, device=device),
                                     requires_grad=train_base)
         self.layers = nn.ModuleList([
@@ -130,8 +131,8 @@ class Llama(nn.Module):
         cfg = self.cfg
         layer = self.layers[i]
         qkv = layer.wqkv(x)
-        o = ops.attention_block(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads,
-                                cfg.head_dim, causal=True)
+        attn = self.seq_parallel or ops.attention_block
+        o = attn(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, causal=True)
         a = layer.wo(o)
         x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps)
         m = ops.swiglu(layer.wgu(x))
@@ -162,6 +163,17 @@ class Llama(nn.Module):
         if labels is not None:
             return ops.linear_cross_entropy(x, self.head_weight, labels.reshape(-1), ignore_index)
         return torch.matmul(x, self.head_weight.t()).view(B, S, -1)
+
+    def set_sequence_parallel(self, group) -> None:
+        """Shard sequences over ``group`` (Ulysses all-to-all around attention,
+        mxllm/parallel/sequence.py); ``None`` turns it off.  Inputs passed to
+        forward are then this rank's [B, S/P] token slice."""
+        if group is None:
+            self.seq_parallel = None
+            return
+        from ..parallel.sequence import UlyssesAttention
+
+        self.seq_parallel = UlyssesAttention(group)
 
     # ------------------------------------------------------------------ utilities
     def trainable_parameters(self):

@@ -81,11 +81,19 @@ def main(argv=None):
         from mxllm.train import checkpoint
 
         trainer = build_trainer(run, env)
+        sp_group, data_rank, data_world = None, rank, world_size
+        if run.sequence_parallel > 1:
+            if run.parallel != "ddp":
+                raise ValueError("--sequence-parallel is supported with --parallel ddp")
+            from mxllm.parallel.sequence import new_groups, shard_sequence
+
+            sp_group, data_rank, data_world = new_groups(run.sequence_parallel)
+            trainer.model.set_sequence_parallel(sp_group)
         mcfg = get_config(run.model)
         tok = get_tokenizer(mcfg.vocab_size, run.tokenizer or None, mcfg.bos_id, mcfg.eos_id)
         texts, _ = load_text_dataset(run.dataset, run.split, run.n_rows, run.seed)
         tokens = pack_texts(texts, tok, getattr(tok, "eos_id", mcfg.eos_id))
-        loader = TokenLoader(tokens, run.seq_len, run.micro_batch, rank, world_size, run.seed, env.device)
+        loader = TokenLoader(tokens, run.seq_len, run.micro_batch, data_rank, data_world, run.seed, env.device)
         steps_per_epoch = max(1, loader.batches_per_epoch // run.grad_accum)
         total = run.steps or run.epochs * steps_per_epoch
         start = 0
@@ -107,13 +115,15 @@ def main(argv=None):
 
             gpu_log = MetricsWriter(run.metrics_file, rank, all_ranks=True)
             monitor = GpuMonitor(env.device, run.gpu_monitor_s, lambda smp: gpu_log.write(kind="gpu", **smp)).start()
-        tok_per_step = run.micro_batch * run.seq_len * run.grad_accum * world_size
+        tok_per_step = run.micro_batch * run.seq_len * run.grad_accum * data_world
         t_last, n_since = time.perf_counter(), 0
         for step in range(start, total):
             maybe_inject(run, rank, step)
             mbs = []
             for _ in range(run.grad_accum):
                 ids, lab, epoch, _i = loader.next_device()
+                if sp_group is not None:
+                    ids, lab = shard_sequence(ids, sp_group), shard_sequence(lab, sp_group)
                 mbs.append((ids, lab))
             loss = trainer.train_step(mbs)
             n_since += 1
