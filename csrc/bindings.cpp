@@ -36,6 +36,19 @@ void check_bf16(const at::Tensor& t, const char* name) {
   MX_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
   MX_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
+// a 2-D row-strided bf16 view (rows may be the left part of a wider buffer)
+int64_t check_rows_bf16(const at::Tensor& t, const char* name) {
+  MX_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  MX_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+  MX_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) >= t.size(1) && t.stride(0) % 8 == 0, name,
+           " must be a row-major [T, H] view with a row stride that is a multiple of 8");
+  return t.stride(0);
+}
+// [T, H] output whose rows live in a [T, H + pad] buffer (pad extra columns left to the caller)
+at::Tensor empty_rows(int64_t T, int64_t H, int64_t pad, const at::TensorOptions& o) {
+  if (pad <= 0) return at::empty({T, H}, o);
+  return at::empty({T, H + pad}, o).narrow(1, 0, H);
+}
 void check_f32(const at::Tensor& t, const char* name) {
   MX_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   MX_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
@@ -43,16 +56,18 @@ void check_f32(const at::Tensor& t, const char* name) {
 }
 
 // ---------------------------------------------------------------- RMSNorm
+// out_pad > 0: y is returned as the [T, H] left part of a [T, H + out_pad] buffer
 std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x,
                                                            const c10::optional<at::Tensor>& res,
-                                                           const at::Tensor& w, double eps) {
+                                                           const at::Tensor& w, double eps, int64_t out_pad) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   DevGuard g(x.device());
   const int64_t H = x.size(-1);
   const int64_t T = x.numel() / H;
   MX_CHECK(w.numel() == H, "weight size mismatch");
-  auto y = at::empty_like(x);
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
+  at::Tensor y = out_pad > 0 ? empty_rows(T, H, out_pad, x.options()) : at::empty_like(x);
   auto rstd = at::empty({T}, x.options().dtype(at::kFloat));
   at::Tensor h;
   const uint16_t* rp = nullptr;
@@ -65,16 +80,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x,
     hp = bfm(h);
   }
   if (T > 0)
-    MX_OK(mx_rmsnorm_fwd(bf(x), rp, bf(w), bfm(y), hp, rstd.data_ptr<float>(), (int)T, (int)H,
+    MX_OK(mx_rmsnorm_fwd(bf(x), rp, bf(w), bfm(y), hp, rstd.data_ptr<float>(), (int)T, (int)H, (int)(H + out_pad),
                          (float)eps, cur_stream()));
   if (!res.has_value()) h = x;
   return {y, rstd, h};
 }
 
-// returns (dx, dw_f32 or empty)
+// returns (dx, dw_f32 or empty).  dres may be a row-strided [T, H] view;
+// out_pad > 0: dx is the left part of a [T, H + out_pad] buffer.
 std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x,
                                                const at::Tensor& w, const at::Tensor& rstd,
-                                               const c10::optional<at::Tensor>& dres, bool need_dw) {
+                                               const c10::optional<at::Tensor>& dres, bool need_dw,
+                                               int64_t out_pad) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -82,10 +99,17 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
   DevGuard g(x.device());
   const int64_t H = x.size(-1);
   const int64_t T = x.numel() / H;
-  auto dx = at::empty_like(x);
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
+  at::Tensor dx = out_pad > 0 ? empty_rows(T, H, out_pad, x.options()) : at::empty_like(x);
   const uint16_t* drp = nullptr;
+  int64_t ldr = H;
   if (dres.has_value()) {
-    check_bf16(*dres, "dres");
+    if (dres->is_contiguous()) {
+      check_bf16(*dres, "dres");
+    } else {
+      ldr = check_rows_bf16(*dres, "dres");
+      MX_CHECK(dres->size(0) == T && dres->size(1) == H, "dres shape mismatch");
+    }
     drp = bf(*dres);
   }
   // rows per block: keep >= ~2 blocks per CU on 256 CUs, amortise the dγ partial
@@ -103,8 +127,8 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     dwpp = dwp.data_ptr<float>();
   }
   if (T > 0) {
-    MX_OK(mx_rmsnorm_bwd(bf(dy), bf(x), bf(w), rstd.data_ptr<float>(), drp, bfm(dx), dwpp, (int)T,
-                         (int)H, rpb, cur_stream()));
+    MX_OK(mx_rmsnorm_bwd(bf(dy), bf(x), bf(w), rstd.data_ptr<float>(), drp, bfm(dx), dwpp, (int)T, (int)H,
+                         (int)ldr, (int)(H + out_pad), rpb, cur_stream()));
     if (need_dw) MX_OK(mx_colsum_f32(dwpp, dw.data_ptr<float>(), (int)nblk, (int)H, cur_stream()));
   } else if (need_dw) {
     dw.zero_();
@@ -113,6 +137,14 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
 }
 
 // ---------------------------------------------------------------- misc
+// desc: int64 [n, 7] on the device (see misc.hip); total_blocks = sum of per-descriptor blocks
+void copy2d_batched(const at::Tensor& desc, int64_t total_blocks) {
+  MX_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 7 &&
+               desc.is_contiguous(), "desc must be int64 [n, 7] on the GPU");
+  DevGuard g(desc.device());
+  MX_OK(mx_copy2d_batched(desc.data_ptr<int64_t>(), (int)desc.size(0), total_blocks, cur_stream()));
+}
+
 at::Tensor segmented_mean(const at::Tensor& codes, const at::Tensor& offsets) {
   MX_CHECK(codes.is_cuda() && codes.scalar_type() == at::kInt, "codes must be int32 GPU");
   MX_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kLong, "offsets must be int64 GPU");
@@ -134,28 +166,36 @@ at::Tensor sqnorm_f32(const at::Tensor& x) {
 }
 
 // ---------------------------------------------------------------- SwiGLU
-at::Tensor swiglu_fwd(const at::Tensor& gu) {
+// out_pad > 0: outputs are [T, n] views into [T, n + out_pad] buffers
+at::Tensor swiglu_fwd(const at::Tensor& gu, int64_t out_pad) {
   check_bf16(gu, "gu");
   DevGuard g(gu.device());
   const int64_t F2 = gu.size(-1);
   MX_CHECK(F2 % 16 == 0, "2F must be a multiple of 16");
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
   const int64_t T = gu.numel() / F2;
-  auto sizes = gu.sizes().vec();
-  sizes.back() = F2 / 2;
-  auto m = at::empty(sizes, gu.options());
-  if (T > 0) MX_OK(mx_swiglu_fwd(bf(gu), bfm(m), T, (int)(F2 / 2), cur_stream()));
+  at::Tensor m;
+  if (out_pad > 0) {
+    m = empty_rows(T, F2 / 2, out_pad, gu.options());
+  } else {
+    auto sizes = gu.sizes().vec();
+    sizes.back() = F2 / 2;
+    m = at::empty(sizes, gu.options());
+  }
+  if (T > 0) MX_OK(mx_swiglu_fwd(bf(gu), bfm(m), T, (int)(F2 / 2), F2 / 2 + out_pad, cur_stream()));
   return m;
 }
 
-at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu) {
+at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu, int64_t out_pad) {
   check_bf16(dm, "dm");
   check_bf16(gu, "gu");
   DevGuard g(gu.device());
   const int64_t F2 = gu.size(-1);
   const int64_t T = gu.numel() / F2;
   MX_CHECK(dm.numel() == T * (F2 / 2), "dm shape mismatch");
-  auto dgu = at::empty_like(gu);
-  if (T > 0) MX_OK(mx_swiglu_bwd(bf(dm), bf(gu), bfm(dgu), T, (int)(F2 / 2), cur_stream()));
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
+  at::Tensor dgu = out_pad > 0 ? empty_rows(T, F2, out_pad, gu.options()) : at::empty_like(gu);
+  if (T > 0) MX_OK(mx_swiglu_bwd(bf(dm), bf(gu), bfm(dgu), T, (int)(F2 / 2), F2 + out_pad, cur_stream()));
   return dgu;
 }
 
@@ -253,23 +293,27 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_split(const at::Tensor& qkv,
 }
 
 at::Tensor rope_merge_bwd(const at::Tensor& dq, const at::Tensor& dkp, const at::Tensor& dvp, const at::Tensor& cos,
-                          const at::Tensor& sin, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D) {
+                          const at::Tensor& sin, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D,
+                          int64_t out_pad) {
   check_f32(dq, "dq");
   check_f32(dkp, "dkp");
   check_f32(dvp, "dvp");
   DevGuard g(dq.device());
   const int64_t kvin = dkp.size(1);
   MX_CHECK(dkp.dim() == 4 && dkp.size(0) == B && dkp.size(2) == S && dkp.size(3) == D, "dk partial shape");
-  auto dqkv = at::empty({B * S, (Hq + 2 * Hkv) * D}, dq.options().dtype(at::kBFloat16));
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
+  const int64_t NHD = (Hq + 2 * Hkv) * D;
+  auto dqkv = empty_rows(B * S, NHD, out_pad, dq.options().dtype(at::kBFloat16));
   MX_OK(mx_rope_merge_bwd(dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), cos.data_ptr<float>(),
                           sin.data_ptr<float>(), bfm(dqkv), (int)B, (int)S, (int)Hq, (int)Hkv, (int)kvin, (int)D,
-                          cur_stream()));
+                          NHD + out_pad, cur_stream()));
   return dqkv;
 }
 
 // ---------------------------------------------------------------- attention
+// out_pad > 0: o [B, S, Hq*D] is a view into [B, S, Hq*D + out_pad] (row stride Hq*D + out_pad)
 std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                            bool causal, double scale) {
+                                            bool causal, double scale, int64_t out_pad) {
   check_bf16(q, "q");
   check_bf16(k, "k");
   check_bf16(v, "v");
@@ -278,10 +322,12 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   const int64_t Hkv = k.size(1), Sk = k.size(2);
   MX_CHECK(k.size(0) == B && k.size(3) == D && Hq % Hkv == 0, "attention shape mismatch");
   DevGuard g(q.device());
-  auto o = at::empty({B, S, Hq * D}, q.options());
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
+  auto o = out_pad > 0 ? at::empty({B, S, Hq * D + out_pad}, q.options()).narrow(2, 0, Hq * D)
+                       : at::empty({B, S, Hq * D}, q.options());
   auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   MX_OK(mx_attn_fwd(bf(q), bf(k), bf(v), bfm(o), lse.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv, (int)S, (int)Sk,
-                    (int)D, causal ? 1 : 0, (float)scale, cur_stream()));
+                    (int)D, causal ? 1 : 0, (float)scale, (int)(Hq * D + out_pad), cur_stream()));
   return {o, lse};
 }
 
@@ -290,11 +336,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
                                                              const at::Tensor& o, const at::Tensor& lse, int causal,
                                                              double scale, bool deterministic = false) {
   check_bf16(dout, "dout");
-  check_bf16(o, "o");
   check_f32(lse, "lse");
   const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(1), Sk = k.size(2);
   MX_CHECK(dout.numel() == B * S * Hq * D && o.numel() == dout.numel(), "dout/o shape");
+  // o: contiguous, or token rows with a row stride (the padded attention output)
+  int64_t ldo = Hq * D;
+  if (!o.is_contiguous()) {
+    MX_CHECK(o.is_cuda() && o.scalar_type() == at::kBFloat16 && o.dim() == 3 && o.stride(2) == 1 &&
+                 o.size(2) == Hq * D && o.stride(0) == S * o.stride(1) && o.stride(1) % 8 == 0,
+             "o must be [B, S, Hq*D] with unit inner stride");
+    ldo = o.stride(1);
+  } else {
+    check_bf16(o, "o");
+  }
   DevGuard g(q.device());
   const int64_t S_pad = (S + 63) / 64 * 64;
   auto dkp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
@@ -307,13 +362,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
     auto dq = at::empty({B, Hq, S, D}, q.options().dtype(at::kFloat));
     MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                       dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                      (int)S, (int)Sk, (int)D, causal, (float)scale, part.data_ptr<float>(), cur_stream()));
+                      (int)S, (int)Sk, (int)D, causal, (float)scale, part.data_ptr<float>(), ldo, cur_stream()));
     return {dq, dkp, dvp};
   }
   auto dq_pad = at::zeros({B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
   MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                     dq_pad.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                    (int)S, (int)Sk, (int)D, causal, (float)scale, nullptr, cur_stream()));
+                    (int)S, (int)Sk, (int)D, causal, (float)scale, nullptr, ldo, cur_stream()));
   auto dq = S_pad == S ? dq_pad : dq_pad.narrow(2, 0, S).contiguous();
   return {dq, dkp, dvp};
 }
@@ -388,19 +443,20 @@ at::Tensor sample(const at::Tensor& logits, double temperature, int64_t seed, in
 }  // namespace
 
 TORCH_LIBRARY(mxllm, m) {
-  m.def("rmsnorm_fwd(Tensor x, Tensor? res, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw) -> (Tensor, Tensor)");
+  m.def("rmsnorm_fwd(Tensor x, Tensor? res, Tensor w, float eps, int out_pad=0) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw, int out_pad=0) -> (Tensor, Tensor)");
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
+  m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
   m.def("sqnorm_f32(Tensor x) -> Tensor");
-  m.def("swiglu_fwd(Tensor gu) -> Tensor");
-  m.def("swiglu_bwd(Tensor dm, Tensor gu) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
+  m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
   m.def("adamw_step(Tensor(a!) master, Tensor grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor w) -> Tensor");
   m.def("embedding_bwd(Tensor dy, Tensor ids, int V) -> Tensor");
   m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
   m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
-  m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D) -> Tensor");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
   m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D) -> Tensor");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
@@ -412,6 +468,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("segmented_mean", &segmented_mean);
+  m.impl("copy2d_batched", &copy2d_batched);
   m.impl("sqnorm_f32", &sqnorm_f32);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);

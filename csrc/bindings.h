@@ -7,9 +7,9 @@
 extern "C" {
 // rmsnorm.hip
 int mx_rmsnorm_fwd(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* y,
-                   uint16_t* h_out, float* rstd, int T, int H, float eps, hipStream_t stream);
+                   uint16_t* h_out, float* rstd, int T, int H, int ldy, float eps, hipStream_t stream);
 int mx_rmsnorm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* w, const float* rstd,
-                   const uint16_t* dres, uint16_t* dx, float* dwp, int T, int H, int rpb,
+                   const uint16_t* dres, uint16_t* dx, float* dwp, int T, int H, int ldr, int ldx, int rpb,
                    hipStream_t stream);
 int mx_colsum_f32(const float* p, float* out, int nblk, int H, hipStream_t stream);
 
@@ -17,12 +17,14 @@ int mx_colsum_f32(const float* p, float* out, int nblk, int H, hipStream_t strea
 int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, float* out, int nseg,
                           hipStream_t stream);
 int mx_sqnorm_f32(const float* x, int64_t n, float* out, hipStream_t stream);
+int mx_copy2d_batched(const int64_t* desc, int n, int64_t total_blocks, hipStream_t stream);
 }
 
 extern "C" {
 // elementwise.hip
-int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, hipStream_t stream);
-int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, hipStream_t stream);
+int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream);
+int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
+                  hipStream_t stream);
 int mx_adamw(float* p, const void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
              float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t, float scale_f,
              hipStream_t stream);
@@ -37,13 +39,14 @@ int mx_ce_fwd_bwd(uint16_t* logits, const int64_t* labels, float* losses, float*
 int mx_rope_split(const uint16_t* qkv, const float* cosb, const float* sinb, const int32_t* positions, uint16_t* q,
                   uint16_t* k, uint16_t* v, int B, int S, int Hq, int Hkv, int D, hipStream_t stream);
 int mx_rope_merge_bwd(const float* dq, const float* dkp, const float* dvp, const float* cosb, const float* sinb,
-                      uint16_t* dqkv, int B, int S, int Hq, int Hkv, int kv_heads_in, int D, hipStream_t stream);
+                      uint16_t* dqkv, int B, int S, int Hq, int Hkv, int kv_heads_in, int D, int64_t ldq,
+                      hipStream_t stream);
 // attn_fwd.hip / attn_bwd.hip
 int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B, int Hq,
-                int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream);
+                int Hkv, int S, int Sk, int D, int causal, float scale, int ldo, hipStream_t stream);
 int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o, const uint16_t* dout,
                 const float* lse, float* delta, float* dq, float* dkp, float* dvp, int B, int Hq, int Hkv, int S,
-                int Sk, int D, int causal, float scale, float* dq_part, hipStream_t stream);
+                int Sk, int D, int causal, float scale, float* dq_part, int64_t ldo, hipStream_t stream);
 }
 
 extern "C" {

@@ -44,7 +44,8 @@ __device__ __forceinline__ int swzb(int row) {
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dO,
                                                              const uint16_t* __restrict__ O,
-                                                             float* __restrict__ delta, int B, int S, int Hq) {
+                                                             float* __restrict__ delta, int B, int S, int Hq,
+                                                             int64_t ldo) {
   constexpr int LPR = D / 8;  // lanes per row
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;  // over B*S*Hq (token-major order)
   const int sub = threadIdx.x % LPR;
@@ -52,7 +53,7 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
   float s = 0.f;
   if (valid) {
     const u16x8 a = *reinterpret_cast<const u16x8*>(dO + row * D + sub * 8);
-    const u16x8 c = *reinterpret_cast<const u16x8*>(O + row * D + sub * 8);
+    const u16x8 c = *reinterpret_cast<const u16x8*>(O + (row / Hq) * ldo + (row % Hq) * D + sub * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(c[j]);
   }
@@ -350,6 +351,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_reduce(const float* __restric
 
 using namespace mx;
 
+// o: token-major rows with row stride ldo (elements); dout contiguous [B, S, Hq*D].
 // dq [B,Hq,ceil(S/64)*64,D] f32 must be ZEROED by the caller (f32 atomics; padded rows absorb
 // the unguarded tail atomics).  delta: workspace [B,Hq,S].
 // Deterministic mode (dq_part != nullptr): dq_part is a workspace of
@@ -358,15 +360,15 @@ using namespace mx;
 extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
                            const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
                            int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, float* dq_part,
-                           hipStream_t stream) {
+                           int64_t ldo, hipStream_t stream) {
   if (B <= 0 || S <= 0 || Sk <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int64_t rows = (int64_t)B * S * Hq;
   const int64_t dthreads = rows * (D / 8);
   const unsigned dgrid = (unsigned)((dthreads + 255) / 256);
-  if (D == 128) attn_bwd_delta_kernel<128><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq);
-  else if (D == 64) attn_bwd_delta_kernel<64><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq);
-  else if (D == 32) attn_bwd_delta_kernel<32><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq);
+  if (D == 128) attn_bwd_delta_kernel<128><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq, ldo);
+  else if (D == 64) attn_bwd_delta_kernel<64><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq, ldo);
+  else if (D == 32) attn_bwd_delta_kernel<32><<<dgrid, 256, 0, stream>>>(dout, o, delta, B, S, Hq, ldo);
   else return -1;
   const int nkb = (Sk + 127) / 128;
   const int grid = nkb * B * Hq;

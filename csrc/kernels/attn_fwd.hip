@@ -47,7 +47,7 @@ template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, 2)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
-                int causal_off, float sl) {
+                int causal_off, float sl, int ldo) {
   constexpr int BM = 128, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int TILE = BN * ROWB;
   constexpr int LPT = BN * CH / 256;
@@ -199,7 +199,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qrow < S) {
-    uint16_t* op = O + ((size_t)b * S + qrow) * (size_t)(Hq * D) + (size_t)h * D;
+    uint16_t* op = O + ((size_t)b * S + qrow) * (size_t)ldo + (size_t)h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -218,15 +218,18 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 
 using namespace mx;
 
+// o: token-major [B, S, Hq*D] rows with row stride ldo (elements, >= Hq*D): the rows may
+// be the left part of the LoRA-augmented o-projection input (mxllm/ops/linear.py)
 extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B,
-                           int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, hipStream_t stream) {
+                           int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, int ldo,
+                           hipStream_t stream) {
   if (B <= 0 || S <= 0) return 0;
-  if (Hkv <= 0 || Hq % Hkv) return -1;
+  if (Hkv <= 0 || Hq % Hkv || ldo < Hq * D || ldo % 8) return -1;
   const int nqb = (S + 127) / 128;
   const int grid = nqb * B * Hq;
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
-#define FWD(DD, C) attn_fwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl)
+#define FWD(DD, C) attn_fwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo)
   if (D == 128) { if (causal) FWD(128, true); else FWD(128, false); }
   else if (D == 64) { if (causal) FWD(64, true); else FWD(64, false); }
   else if (D == 32) { if (causal) FWD(32, true); else FWD(32, false); }

@@ -12,7 +12,7 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x))
 
 // m[t, c] = silu(gu[t, c]) * gu[t, F + c]
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ m,
-                                                         int64_t T, int F) {
+                                                         int64_t T, int F, int64_t ldm) {
   const int64_t per_row = F / 8;
   const int64_t n = T * per_row;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -24,14 +24,15 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restr
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f2bf(silu_f(bf2f(g[j])) * bf2f(u[j]));
-    *reinterpret_cast<u16x8*>(m + t * (int64_t)F + c) = o;
+    *reinterpret_cast<u16x8*>(m + t * ldm + c) = o;
   }
 }
 
 // dg = dm * u * s * (1 + g (1 - s)),  du = dm * g * s,  s = sigmoid(g)
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ dm,
                                                          const uint16_t* __restrict__ gu,
-                                                         uint16_t* __restrict__ dgu, int64_t T, int F) {
+                                                         uint16_t* __restrict__ dgu, int64_t T, int F,
+                                                         int64_t ldg) {
   const int64_t per_row = F / 8;
   const int64_t n = T * per_row;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -49,7 +50,7 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
       og[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
       ou[j] = f2bf(df * gf * s);
     }
-    uint16_t* orow = dgu + t * (2 * (int64_t)F);
+    uint16_t* orow = dgu + t * ldg;
     *reinterpret_cast<u16x8*>(orow + c) = og;
     *reinterpret_cast<u16x8*>(orow + F + c) = ou;
   }
@@ -130,16 +131,18 @@ static int grid_for(int64_t items) {
   return (int)b;
 }
 
-extern "C" int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, hipStream_t stream) {
-  if (F % 8) return -1;
-  swiglu_fwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(gu, m, T, F);
+// ldm / ldg: output row strides (elements, multiples of 8): the outputs may be the left
+// part of the LoRA-augmented GEMM operand buffers (mxllm/ops/linear.py)
+extern "C" int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream) {
+  if (F % 8 || ldm < F || ldm % 8) return -1;
+  swiglu_fwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(gu, m, T, F, ldm);
   return (int)hipGetLastError();
 }
 
-extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F,
+extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
                              hipStream_t stream) {
-  if (F % 8) return -1;
-  swiglu_bwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(dm, gu, dgu, T, F);
+  if (F % 8 || ldg < 2 * (int64_t)F || ldg % 8) return -1;
+  swiglu_bwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(dm, gu, dgu, T, F, ldg);
   return (int)hipGetLastError();
 }
 

@@ -40,9 +40,42 @@ __global__ void __launch_bounds__(256) sqnorm_f32_kernel(const float* __restrict
   if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+// Batched strided 2-D copy of 16-bit elements: one launch refreshes every LoRA
+// adapter's copy inside the augmented GEMM weight buffers after an optimizer
+// step (mxllm/models/llama.py, FusedLinear).  desc[i] = {src, dst, rows, cols,
+// src_ld, dst_ld, first_block}; block b belongs to the descriptor with the
+// largest first_block <= b (binary search), each block copies 4096 elements.
+constexpr int kCopyBlockElems = 4096;
+
+__global__ void __launch_bounds__(256) copy2d_batched_kernel(const int64_t* __restrict__ desc, int n) {
+  int lo = 0, hi = n - 1;
+  const int64_t b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (desc[mid * 7 + 6] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* d = desc + lo * 7;
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(d[0]);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(d[1]);
+  const int64_t rows = d[2], cols = d[3], sld = d[4], dld = d[5];
+  const int64_t e0 = (b - d[6]) * kCopyBlockElems;
+  const int64_t total = rows * cols;
+  for (int64_t e = e0 + threadIdx.x; e < min(total, e0 + kCopyBlockElems); e += 256) {
+    const int64_t r = e / cols, c = e - r * cols;
+    dst[r * dld + c] = src[r * sld + c];
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
+
+extern "C" int mx_copy2d_batched(const int64_t* desc, int n, int64_t total_blocks, hipStream_t stream) {
+  if (n <= 0 || total_blocks <= 0) return 0;
+  copy2d_batched_kernel<<<(unsigned)total_blocks, 256, 0, stream>>>(desc, n);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, float* out, int nseg,
                                      hipStream_t stream) {

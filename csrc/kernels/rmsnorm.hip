@@ -17,7 +17,7 @@ template <int ITERS, bool RESID>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
     const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-    uint16_t* __restrict__ h_out, float* __restrict__ rstd_out, int H, float eps) {
+    uint16_t* __restrict__ h_out, float* __restrict__ rstd_out, int H, int ldy, float eps) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const size_t base = (size_t)row * H;
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(v[it][j] * rs * bf2f(g[j]));
-      *reinterpret_cast<u16x8*>(y + base + c) = o;
+      *reinterpret_cast<u16x8*>(y + (size_t)row * ldy + c) = o;
     }
   }
 }
@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ w, const float* __restrict__ rstd,
     const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
-    float* __restrict__ dwp, int T, int H, int rows_per_blk) {
+    float* __restrict__ dwp, int T, int H, int ldr, int ldx, int rows_per_blk) {
   __shared__ float scratch[16];
   float gw[ITERS][8];
   float acc[ITERS][8];
@@ -124,14 +124,14 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
       if (c < H) {
         u16x8 o;
         if constexpr (DRES) {
-          u16x8 r = *reinterpret_cast<const u16x8*>(dres + base + c);
+          u16x8 r = *reinterpret_cast<const u16x8*>(dres + (size_t)row * ldr + c);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = f2bf(rs * gv[it][j] - xv[it][j] * k + bf2f(r[j]));
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = f2bf(rs * gv[it][j] - xv[it][j] * k);
         }
-        *reinterpret_cast<u16x8*>(dx + base + c) = o;
+        *reinterpret_cast<u16x8*>(dx + (size_t)row * ldx + c) = o;
       }
     }
   }
@@ -176,9 +176,9 @@ using namespace mx;
 #define FWD_CASE(IT)                                                                                  \
   case IT:                                                                                            \
     if (res)                                                                                          \
-      rmsnorm_fwd_kernel<IT, true><<<T, 256, 0, stream>>>(x, res, w, y, h_out, rstd, H, eps);          \
+      rmsnorm_fwd_kernel<IT, true><<<T, 256, 0, stream>>>(x, res, w, y, h_out, rstd, H, ldy, eps);     \
     else                                                                                              \
-      rmsnorm_fwd_kernel<IT, false><<<T, 256, 0, stream>>>(x, res, w, y, h_out, rstd, H, eps);         \
+      rmsnorm_fwd_kernel<IT, false><<<T, 256, 0, stream>>>(x, res, w, y, h_out, rstd, H, ldy, eps);    \
     break;
 
 static int iters_for(int H) {
@@ -189,15 +189,17 @@ static int iters_for(int H) {
   return 8;
 }
 
+// ldy: row stride of y in elements (>= H, multiple of 8): y may be the left part of a
+// wider buffer (the LoRA-augmented GEMM input [x | s t], mxllm/ops/linear.py)
 extern "C" int mx_rmsnorm_fwd(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* y,
-                              uint16_t* h_out, float* rstd, int T, int H, float eps, hipStream_t stream) {
-  if (H % 8 != 0 || H > 8 * 256 * 8 || T <= 0) return -1;
+                              uint16_t* h_out, float* rstd, int T, int H, int ldy, float eps, hipStream_t stream) {
+  if (H % 8 != 0 || H > 8 * 256 * 8 || T <= 0 || ldy < H || ldy % 8) return -1;
   switch (iters_for(H)) { FWD_CASE(1) FWD_CASE(2) FWD_CASE(4) FWD_CASE(8) }
   return (int)hipGetLastError();
 }
 
 #define BWD_LAUNCH(IT, DR, DW_)                                                                       \
-  rmsnorm_bwd_kernel<IT, DR, DW_><<<nblk, 256, 0, stream>>>(dy, x, w, rstd, dres, dx, dwp, T, H, rpb)
+  rmsnorm_bwd_kernel<IT, DR, DW_><<<nblk, 256, 0, stream>>>(dy, x, w, rstd, dres, dx, dwp, T, H, ldr, ldx, rpb)
 #define BWD_CASE(IT)                                                                                  \
   case IT:                                                                                            \
     if (dres) {                                                                                       \
@@ -208,10 +210,12 @@ extern "C" int mx_rmsnorm_fwd(const uint16_t* x, const uint16_t* res, const uint
     break;
 
 // rows_per_blk chosen by the caller; dwp may be null (frozen γ).  Returns nblk.
+// ldr / ldx: row strides (elements) of dres and dx (>= H, multiple of 8)
 extern "C" int mx_rmsnorm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* w, const float* rstd,
-                              const uint16_t* dres, uint16_t* dx, float* dwp, int T, int H, int rpb,
-                              hipStream_t stream) {
-  if (H % 8 != 0 || H > 8 * 256 * 8 || T <= 0 || rpb <= 0) return -1;
+                              const uint16_t* dres, uint16_t* dx, float* dwp, int T, int H, int ldr, int ldx,
+                              int rpb, hipStream_t stream) {
+  if (H % 8 != 0 || H > 8 * 256 * 8 || T <= 0 || rpb <= 0 || ldx < H || ldx % 8 || (dres && (ldr < H || ldr % 8)))
+    return -1;
   const int nblk = (T + rpb - 1) / rpb;
   switch (iters_for(H)) { BWD_CASE(1) BWD_CASE(2) BWD_CASE(4) BWD_CASE(8) }
   return (int)hipGetLastError();

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(256) rope_merge_bwd_kernel(const float* __rest
                                                              const float* __restrict__ cosb,
                                                              const float* __restrict__ sinb,
                                                              uint16_t* __restrict__ dqkv, int B, int S, int Hq,
-                                                             int Hkv, int kv_heads_in) {
+                                                             int Hkv, int kv_heads_in, int64_t ldq) {
   constexpr int HALF = D / 2, CPH = HALF / 8;
   const int NH = Hq + 2 * Hkv;
   const int rep = kv_heads_in / Hkv;  // partials per kv head (Hq for per-q-head partials, Hkv if pre-summed)
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(256) rope_merge_bwd_kernel(const float* __rest
         a2[j] += w0[j]; a2[j + 4] += w1[j];
       }
     }
-    uint16_t* dst = dqkv + t * (int64_t)NH * D + (int64_t)head * D;
+    uint16_t* dst = dqkv + t * ldq + (int64_t)head * D;
     u16x8 y1, y2;
     if (head >= Hq + Hkv) {
 #pragma unroll
@@ -154,15 +154,17 @@ extern "C" int mx_rope_split(const uint16_t* qkv, const float* cosb, const float
   return (int)hipGetLastError();
 }
 
+// ldq: row stride of dqkv in elements (>= (Hq + 2 Hkv) D, multiple of 8); the rows may
+// be the left part of the LoRA-augmented backward GEMM operand (mxllm/ops/linear.py)
 extern "C" int mx_rope_merge_bwd(const float* dq, const float* dkp, const float* dvp, const float* cosb,
                                  const float* sinb, uint16_t* dqkv, int B, int S, int Hq, int Hkv, int kv_heads_in,
-                                 int D, hipStream_t stream) {
+                                 int D, int64_t ldq, hipStream_t stream) {
   const int64_t items = (int64_t)B * S * (Hq + 2 * Hkv) * (D / 16);
   if (items <= 0) return 0;
-  if (kv_heads_in % Hkv) return -1;
+  if (kv_heads_in % Hkv || ldq < (int64_t)(Hq + 2 * Hkv) * D || ldq % 8) return -1;
 #define MERGE(DD)                                                                                       \
   rope_merge_bwd_kernel<DD><<<grid_for(items), 256, 0, stream>>>(dq, dkp, dvp, cosb, sinb, dqkv, B, S, Hq, Hkv, \
-                                                                 kv_heads_in)
+                                                                 kv_heads_in, ldq)
   if (D == 128) MERGE(128);
   else if (D == 64) MERGE(64);
   else if (D == 32) MERGE(32);

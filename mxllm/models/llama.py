@@ -30,22 +30,38 @@ from .config import LlamaConfig
 
 
 class FusedLinear(nn.Module):
-    """y = x @ W^T with W = concat(splits) [sum(splits), in]; optional per-split LoRA."""
+    """y = x @ W^T with W = concat(splits) [sum(splits), in]; optional per-split LoRA.
+
+    With LoRA the frozen W lives inside an augmented buffer
+    ``wbuf [N + pad, in + pad] = [[W, B], [A, 0]]`` (``pad`` = n*r rounded up to
+    64) so each direction of the projection is ONE hipBLASLt GEMM
+    (mxllm/ops/linear.py ``_LoRAAugFn``); ``weight`` is a view of it.  The
+    adapter parameters stay ordinary (flat-buffer) parameters for DDP and the
+    fused optimizer; ``Llama.sync_adapters_`` copies them into ``wbuf`` after
+    every update (one batched HIP copy for the whole model).
+    """
 
     def __init__(self, in_features: int, splits: list[int], *, dtype, device, lora_r: int = 0,
                  lora_alpha: float = 16.0, train_base: bool = True):
         super().__init__()
         self.in_features = in_features
         self.splits = list(splits)
-        self.weight = nn.Parameter(torch.empty(sum(splits), in_features, dtype=dtype, device=device),
-                                   requires_grad=train_base)
+        N = sum(splits)
         self.lora_r = lora_r
+        self.pad = 0
         if lora_r > 0:
             n = len(splits)
             self.scaling = lora_alpha / lora_r
+            self.pad = (n * lora_r + 63) // 64 * 64
+            self.register_buffer("wbuf", torch.zeros(N + self.pad, in_features + self.pad, dtype=dtype,
+                                                     device=device), persistent=False)
+            self.weight = nn.Parameter(self.wbuf[:N, :in_features], requires_grad=train_base)
             # A: all splits' down-projections stacked; B: block-diagonal up-projection
             self.lora_a = nn.Parameter(torch.empty(n * lora_r, in_features, dtype=dtype, device=device))
-            self.lora_b = nn.Parameter(torch.zeros(sum(splits), n * lora_r, dtype=dtype, device=device))
+            self.lora_b = nn.Parameter(torch.zeros(N, n * lora_r, dtype=dtype, device=device))
+        else:
+            self.weight = nn.Parameter(torch.empty(N, in_features, dtype=dtype, device=device),
+                                       requires_grad=train_base)
 
     def lora_b_blocks(self):
         """Views of the diagonal blocks B_i [n_i, r] of the block-diagonal B."""
@@ -55,6 +71,21 @@ class FusedLinear(nn.Module):
             off += n_i
         return out
 
+    def augmented(self) -> bool:
+        """True while ``weight`` still aliases ``wbuf`` (module not moved / merged)."""
+        return (self.lora_r > 0 and hasattr(self, "wbuf")
+                and self.weight.data_ptr() == self.wbuf.data_ptr() and self.weight.dtype == self.wbuf.dtype)
+
+    def adapter_copies(self):
+        """(src, dst) pairs: adapter parameters -> their slots in ``wbuf``."""
+        N, K, R = sum(self.splits), self.in_features, self.lora_a.shape[0]
+        return [(self.lora_a.data, self.wbuf[N:N + R, :K]), (self.lora_b.data, self.wbuf[:N, K:K + R])]
+
+    @torch.no_grad()
+    def sync_adapter_(self):
+        for src, dst in self.adapter_copies():
+            dst.copy_(src)
+
     @torch.no_grad()
     def reset_parameters(self, std: float, gen: torch.Generator | None):
         self.weight.normal_(0.0, std, generator=gen)
@@ -62,9 +93,14 @@ class FusedLinear(nn.Module):
             bound = 1.0 / math.sqrt(self.in_features)
             self.lora_a.uniform_(-bound, bound, generator=gen)
             self.lora_b.zero_()
+            if self.augmented():
+                self.sync_adapter_()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.lora_r > 0:
+            if self.augmented():
+                return ops.lora_linear_aug(x, self.lora_a, self.lora_b, self.wbuf, self.splits, self.scaling,
+                                           self.pad)
             return ops.lora_linear(x, self.weight, self.lora_a, self.lora_b, self.splits, self.scaling)
         return ops.linear(x, self.weight)
 
@@ -127,25 +163,39 @@ class Llama(nn.Module):
         return self.tok_emb if self.lm_head is None else self.lm_head
 
     # ------------------------------------------------------------------ training forward
+    @staticmethod
+    def _pad(lin) -> int:
+        """Row padding a producer leaves for a LoRA projection's rank columns."""
+        return lin.pad if lin.augmented() else 0
+
     def _layer(self, i: int, x: torch.Tensor, h: torch.Tensor, B: int, S: int):
         cfg = self.cfg
         layer = self.layers[i]
         qkv = layer.wqkv(x)
-        attn = self.seq_parallel or ops.attention_block
-        o = attn(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, causal=True)
+        if self.seq_parallel is not None:
+            o = self.seq_parallel(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads,
+                                  cfg.head_dim, causal=True)
+        else:
+            o = ops.attention_block(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads,
+                                    cfg.head_dim, causal=True, out_pad=self._pad(layer.wo),
+                                    grad_pad=self._pad(layer.wqkv))
         a = layer.wo(o)
-        x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps)
-        m = ops.swiglu(layer.wgu(x))
+        x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps, out_pad=self._pad(layer.wgu),
+                                grad_pad=self._pad(layer.wo))
+        m = ops.swiglu(layer.wgu(x), out_pad=self._pad(layer.wd), grad_pad=self._pad(layer.wgu))
         d = layer.wd(m)
-        nxt = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
-        x, h = ops.add_rms_norm(d, h, nxt, cfg.norm_eps)
+        last = i + 1 == len(self.layers)
+        nxt = self.final_norm if last else self.layers[i + 1].attn_norm
+        x, h = ops.add_rms_norm(d, h, nxt, cfg.norm_eps, out_pad=0 if last else self._pad(self.layers[i + 1].wqkv),
+                                grad_pad=self._pad(layer.wd))
         return x, h
 
     def hidden_states(self, ids: torch.Tensor) -> torch.Tensor:
         """ids [B, S] -> final normed hidden [B*S, H]."""
         B, S = ids.shape
         h = ops.embedding(ids.reshape(-1), self.tok_emb)
-        x = ops.rms_norm(h, self.layers[0].attn_norm, self.cfg.norm_eps) if len(self.layers) else h
+        x = (ops.rms_norm(h, self.layers[0].attn_norm, self.cfg.norm_eps, out_pad=self._pad(self.layers[0].wqkv))
+             if len(self.layers) else h)
         for i in range(len(self.layers)):
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 x, h = ckpt.checkpoint(self._layer, i, x, h, B, S, use_reentrant=False)
@@ -163,6 +213,32 @@ class Llama(nn.Module):
         if labels is not None:
             return ops.linear_cross_entropy(x, self.head_weight, labels.reshape(-1), ignore_index)
         return torch.matmul(x, self.head_weight.t()).view(B, S, -1)
+
+    @torch.no_grad()
+    def sync_adapters_(self) -> None:
+        """Copy every LoRA adapter into its augmented GEMM buffer (after an
+        optimizer step / checkpoint load / broadcast).  GPU: ONE batched HIP
+        copy (csrc/kernels/misc.hip ``copy2d_batched``) for all projections."""
+        lins = [m for m in self.modules() if isinstance(m, FusedLinear) and m.augmented()]
+        if not lins:
+            return
+        pairs = [p for m in lins for p in m.adapter_copies()]
+        if not pairs[0][0].is_cuda or not ops.native_available():
+            for src, dst in pairs:
+                dst.copy_(src)
+            return
+        key = tuple((s.data_ptr(), d.data_ptr()) for s, d in pairs)
+        if getattr(self, "_adapter_desc_key", None) != key:
+            rows, total = [], 0
+            for s, d in pairs:
+                assert s.is_contiguous() and d.stride(1) == 1 and s.element_size() == 2
+                n = s.shape[0] * s.shape[1]
+                rows.append([s.data_ptr(), d.data_ptr(), s.shape[0], s.shape[1], s.stride(0), d.stride(0), total])
+                total += (n + 4095) // 4096
+            self._adapter_desc = torch.tensor(rows, dtype=torch.int64, device=pairs[0][0].device)
+            self._adapter_blocks = total
+            self._adapter_desc_key = key
+        ops.native().copy2d_batched(self._adapter_desc, self._adapter_blocks)
 
     def set_sequence_parallel(self, group) -> None:
         """Shard sequences over ``group`` (Ulysses all-to-all around attention,

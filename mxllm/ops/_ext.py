@@ -61,3 +61,12 @@ def use_native(t: torch.Tensor) -> bool:
     if os.environ.get("MXLLM_REFERENCE_OPS") == "1":
         return False
     return t.is_cuda
+
+
+def rows_view(t: torch.Tensor) -> torch.Tensor:
+    """``t`` if it is a 2-D row-strided view the kernels accept (unit inner
+    stride, row stride a multiple of 8: e.g. the left part of a padded
+    buffer), otherwise a contiguous copy."""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1] and t.stride(0) % 8 == 0:
+        return t
+    return t.contiguous()

@@ -12,17 +12,22 @@ from ._ext import native, use_native
 
 class _SwiGLUFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, out_pad, grad_pad):
         ctx.save_for_backward(gu)
-        return native().swiglu_fwd(gu)
+        ctx.grad_pad = grad_pad
+        return native().swiglu_fwd(gu, out_pad)
 
     @staticmethod
     def backward(ctx, dm):
         (gu,) = ctx.saved_tensors
-        return native().swiglu_bwd(dm.contiguous(), gu)
+        return native().swiglu_bwd(dm.contiguous(), gu, ctx.grad_pad), None, None
 
 
-def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
+def swiglu(gate_up: torch.Tensor, out_pad: int = 0, grad_pad: int = 0) -> torch.Tensor:
+    """``out_pad`` / ``grad_pad``: padded row layouts for LoRA-augmented GEMM
+    neighbours (see mxllm/ops/norm.py)."""
     if use_native(gate_up):
-        return _SwiGLUFn.apply(gate_up.contiguous())
+        if gate_up.dim() != 2:
+            out_pad = grad_pad = 0
+        return _SwiGLUFn.apply(gate_up.contiguous(), out_pad, grad_pad)
     return ref.swiglu(gate_up)

@@ -31,23 +31,23 @@ def split_heads_ref(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, D: int
 
 class _AttnBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal):
+    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal, out_pad, grad_pad):
         ops = native()
         q, k, v = ops.rope_split(qkv, cos, sin, B, S, Hq, Hkv, D)
-        o, lse = ops.attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D))
+        o, lse = ops.attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D), out_pad)
         ctx.save_for_backward(q, k, v, o, lse, cos, sin)
-        ctx.dims = (B, S, Hq, Hkv, D, causal)
+        ctx.dims = (B, S, Hq, Hkv, D, causal, grad_pad)
         return o.view(B * S, Hq * D)
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse, cos, sin = ctx.saved_tensors
-        B, S, Hq, Hkv, D, causal = ctx.dims
+        B, S, Hq, Hkv, D, causal, grad_pad = ctx.dims
         ops = native()
         dq, dkp, dvp = ops.attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D),
                                     deterministic())
-        dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D)
-        return dqkv, None, None, None, None, None, None, None, None
+        dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D, grad_pad)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
 def deterministic() -> bool:
@@ -58,10 +58,12 @@ def deterministic() -> bool:
 
 
 def attention_block(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, S: int, Hq: int,
-                    Hkv: int, D: int, causal: bool = True) -> torch.Tensor:
-    """qkv [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE at positions 0..S-1)."""
+                    Hkv: int, D: int, causal: bool = True, out_pad: int = 0, grad_pad: int = 0) -> torch.Tensor:
+    """qkv [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE at positions 0..S-1).
+    ``out_pad`` / ``grad_pad``: padded row layouts of the output and of d(qkv)
+    for LoRA-augmented GEMM neighbours (mxllm/ops/linear.py)."""
     if use_native(qkv):
-        return _AttnBlockFn.apply(qkv.contiguous(), cos, sin, B, S, Hq, Hkv, D, causal)
+        return _AttnBlockFn.apply(qkv.contiguous(), cos, sin, B, S, Hq, Hkv, D, causal, out_pad, grad_pad)
     q, k, v = split_heads_ref(qkv, B, S, Hq, Hkv, D)
     q = ref.apply_rope(q, cos, sin)
     k = ref.apply_rope(k, cos, sin)

@@ -110,3 +110,5 @@ def load_model_weights(model, path: str) -> None:
             for k, v in load_file(fp).items():
                 if k in named:
                     named[k].copy_(v.to(named[k].device, named[k].dtype))
+        if hasattr(model, "sync_adapters_"):
+            model.sync_adapters_()

@@ -54,6 +54,7 @@ class Trainer:
         self.ddp = DDP(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
         if broadcast_init:
             self.ddp.broadcast_params(0)
+        self._sync_adapters()
         self.m = torch.zeros_like(self.flat.master)
         self.v = torch.zeros_like(self.flat.master)
         self.step_num = 0
@@ -101,7 +102,14 @@ class Trainer:
         ops.adamw_step_(self.flat.master, self.flat.grads, self.m, self.v, self.lowp, lr=o.lr_at(self.step_num),
                         beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
                         step=self.step_num, grad_scale=gscale)
+        self._sync_adapters()
         self.flat.zero_grad()
+
+    def _sync_adapters(self):
+        """LoRA adapters -> their copies in the augmented GEMM weight buffers."""
+        fn = getattr(self.model, "sync_adapters_", None)
+        if fn is not None:
+            fn()
 
     # ------------------------------------------------------------------ state
     def state_dict(self) -> dict:
@@ -115,6 +123,7 @@ class Trainer:
         self.v.copy_(sd["v"])
         if self.flat.master is not self.flat.params:
             self.flat.params.copy_(self.flat.master)
+        self._sync_adapters()
 
 
 class _null:

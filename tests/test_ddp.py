@@ -73,6 +73,7 @@ def _single_grads(world, full, accum):
                 if getattr(mod, "lora_r", 0):
                     for blk in mod.lora_b_blocks():
                         blk.normal_(0, 0.02, generator=torch.Generator().manual_seed(i))
+        model.sync_adapters_()
     flat = FlatParams([(n, p) for n, p in model.named_parameters() if p.requires_grad])
     g = torch.Generator().manual_seed(11)
     ids = torch.randint(0, cfg.vocab_size, (world * 2 * accum, 32), generator=g)

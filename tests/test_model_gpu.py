@@ -30,6 +30,7 @@ def test_train_step_matches_reference_path(gpu, preset, lora, monkeypatch):
                 if getattr(mod, "lora_r", 0):
                     for blk in mod.lora_b_blocks():
                         blk.normal_(0, 0.02)
+            m.sync_adapters_()
     ids = torch.randint(0, cfg.vocab_size, (2, 192), device=gpu)
     loss = m(ids, ids)
     loss.backward()
@@ -237,3 +238,28 @@ def test_gpu_monitor_samples(gpu):
     ev.wait(10)
     mon.stop()
     assert len(got) >= 2 and "hbm_allocated_gb" in got[0]
+
+
+def test_lora_producers_pad_in_place(gpu, monkeypatch):
+    """Every LoRA GEMM operand (x and dy) arrives already padded by its producer
+    kernel: the augmented path never falls back to a copy on GPU."""
+    import importlib
+
+    from mxllm.models import Llama, get_config
+
+    L = importlib.import_module("mxllm.ops.linear")  # (mxllm.ops.linear the attribute is the function)
+
+    calls = {"padded": 0, "copied": 0}
+    orig = L._padded_rows
+
+    def spy(t, pad):
+        r = orig(t, pad)
+        calls["padded" if r is not None else "copied"] += 1
+        return r
+
+    monkeypatch.setattr(L, "_padded_rows", spy)
+    m = Llama(get_config("tiny-d128"), device=gpu, lora_r=8, seed=2)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu)
+    m(ids, ids).backward()
+    n_lin = 4 * len(m.layers)
+    assert calls == {"padded": 2 * n_lin, "copied": 0}, calls

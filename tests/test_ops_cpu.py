@@ -97,3 +97,32 @@ def test_flops_model():
     assert abs(c.n_params() / 1e9 - 70.55) < 0.05
     assert abs(get_config("llama3.1-8b").n_params() / 1e9 - 8.03) < 0.01
     assert math.isclose(c.train_flops_per_token(2048) / 1e9, 431.4, rel_tol=0.02)
+
+
+def test_lora_augmented_gemm_matches_two_gemm_form():
+    """One augmented GEMM per direction == the two-GEMM LoRA (forward, dx, dA, dB)."""
+    from mxllm.models.llama import FusedLinear
+    from mxllm.ops.linear import lora_linear
+
+    torch.manual_seed(0)
+    lin = FusedLinear(48, [40, 24], dtype=torch.float32, device="cpu", lora_r=4, lora_alpha=8.0, train_base=False)
+    lin.reset_parameters(0.05, None)
+    with torch.no_grad():
+        for blk in lin.lora_b_blocks():
+            blk.normal_(0, 0.1)
+    lin.sync_adapter_()
+    assert lin.augmented() and lin.pad == 64
+    x = torch.randn(10, 48, requires_grad=True)
+    dy = torch.randn(10, 64)
+    y = lin(x)
+    y.backward(dy)
+    got = (y.detach(), x.grad.clone(), lin.lora_a.grad.clone(), lin.lora_b.grad.clone())
+    x.grad = None
+    lin.lora_a.grad = lin.lora_b.grad = None
+    y2 = lora_linear(x, lin.weight, lin.lora_a, lin.lora_b, lin.splits, lin.scaling)
+    y2.backward(dy)
+    want = (y2.detach(), x.grad, lin.lora_a.grad, lin.lora_b.grad)
+    for g, w in zip(got, want):
+        torch.testing.assert_close(g, w, rtol=1e-5, atol=1e-5)
+    # off-diagonal blocks of B get exactly zero gradient
+    assert float(lin.lora_b.grad[:40, 4:].abs().max()) == 0.0
