@@ -38,8 +38,9 @@ def main():
     fl = 2 * 2 * B * Hq * S * S * D / 2
     res = {"shape": [B, Hq, Hkv, S, D]}
     res["fwd_ms"] = timeit(lambda: ops.attn_fwd(q, k, v, True, sc))
-    res["bwd_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc))
-    res["bwd_deterministic_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, True))
+    res["bwd_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc))  # default (split) mode
+    res["bwd_atomic_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 1))
+    res["bwd_partials_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 2))
     res["bwd_noatomic_ms"] = timeit(lambda: ops.attn_bwd_ablate(do, q, k, v, o, lse, -1, sc))
     res["fwd_TF"] = fl / res["fwd_ms"] / 1e9
     res["bwd_TF"] = 2.5 * fl / res["bwd_ms"] / 1e9

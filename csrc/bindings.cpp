@@ -331,15 +331,18 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   return {o, lse};
 }
 
+// dq_mode: 1 = f32 atomics, 2 = deterministic per-key-block partials + ordered reduce,
+// 3 = split (dS^T to HBM + separate dQ kernel; default, deterministic)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q,
                                                              const at::Tensor& k, const at::Tensor& v,
                                                              const at::Tensor& o, const at::Tensor& lse, int causal,
-                                                             double scale, bool deterministic = false) {
+                                                             double scale, int64_t dq_mode) {
   check_bf16(dout, "dout");
   check_f32(lse, "lse");
   const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(1), Sk = k.size(2);
   MX_CHECK(dout.numel() == B * S * Hq * D && o.numel() == dout.numel(), "dout/o shape");
+  MX_CHECK(dq_mode >= 1 && dq_mode <= 3, "dq_mode must be 1, 2 or 3");
   // o: contiguous, or token rows with a row stride (the padded attention output)
   int64_t ldo = Hq * D;
   if (!o.is_contiguous()) {
@@ -352,23 +355,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
   }
   DevGuard g(q.device());
   const int64_t S_pad = (S + 63) / 64 * 64;
+  const int64_t nkb = (Sk + 127) / 128;
   auto dkp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
   auto dvp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  if (deterministic && causal >= 0) {
-    // per-key-block dQ partials, summed in a fixed order (no atomics)
-    const int64_t nkb = (Sk + 127) / 128;
-    auto part = at::empty({nkb, B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
+  if (causal >= 0 && dq_mode != 1) {
+    at::Tensor work = dq_mode == 2 ? at::empty({nkb, B, Hq, S_pad, D}, q.options().dtype(at::kFloat))
+                                   : at::empty({B * Hq, nkb * 128, S_pad}, q.options());
     auto dq = at::empty({B, Hq, S, D}, q.options().dtype(at::kFloat));
     MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                       dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                      (int)S, (int)Sk, (int)D, causal, (float)scale, part.data_ptr<float>(), ldo, cur_stream()));
+                      (int)S, (int)Sk, (int)D, causal, (float)scale, (int)dq_mode, work.data_ptr(), ldo,
+                      cur_stream()));
     return {dq, dkp, dvp};
   }
   auto dq_pad = at::zeros({B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
   MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                     dq_pad.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                    (int)S, (int)Sk, (int)D, causal, (float)scale, nullptr, ldo, cur_stream()));
+                    (int)S, (int)Sk, (int)D, causal, (float)scale, 1, nullptr, ldo, cur_stream()));
   auto dq = S_pad == S ? dq_pad : dq_pad.narrow(2, 0, S).contiguous();
   return {dq, dkp, dvp};
 }
@@ -376,8 +380,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
 std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q,
                                                         const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
                                                         const at::Tensor& lse, bool causal, double scale,
-                                                        bool deterministic) {
-  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, deterministic);
+                                                        int64_t dq_mode) {
+  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, dq_mode);
 }
 
 // timing-only ablation variants (mode: -1 = causal without dQ atomics)
@@ -385,7 +389,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_ablate(const at::Tensor&
                                                                const at::Tensor& k, const at::Tensor& v,
                                                                const at::Tensor& o, const at::Tensor& lse,
                                                                int64_t mode, double scale) {
-  return attn_bwd_impl(dout, q, k, v, o, lse, (int)mode, scale);
+  return attn_bwd_impl(dout, q, k, v, o, lse, (int)mode, scale, 1);
 }
 
 // ---------------------------------------------------------------- decode
@@ -461,7 +465,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, bool deterministic=False) -> (Tensor, Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {

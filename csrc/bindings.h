@@ -46,7 +46,7 @@ int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
                 int Hkv, int S, int Sk, int D, int causal, float scale, int ldo, hipStream_t stream);
 int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o, const uint16_t* dout,
                 const float* lse, float* delta, float* dq, float* dkp, float* dvp, int B, int Hq, int Hkv, int S,
-                int Sk, int D, int causal, float scale, float* dq_part, int64_t ldo, hipStream_t stream);
+                int Sk, int D, int causal, float scale, int dq_mode, void* work, int64_t ldo, hipStream_t stream);
 }
 
 extern "C" {

@@ -34,6 +34,18 @@ __device__ __forceinline__ f32x16 mfma32b(const u16x8& a, const u16x8& b, const 
 __device__ __forceinline__ u16x4 trd(const char* p) {
   return __builtin_bit_cast(u16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_b*)(p)));
 }
+// ds_read_b64_tr_b16 as inline asm with an immediate offset: invisible to hipcc's
+// waitcnt pass, which otherwise drains every in-flight LDS-DMA (vmcnt(0)) before a
+// builtin tr-read (it cannot tell that the read misses the DMA's buffer).  The caller
+// waits with lds_wait() and pins each result behind the wait with pin().
+template <int OFF>
+__device__ __forceinline__ u16x4 trd_asm(uint32_t lds_addr) {
+  u16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(lds_addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void pin(u16x4& v) { asm volatile("" : "+v"(v)); }
 template <int CH>
 __device__ __forceinline__ int swzb(int row) {
   return (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
@@ -67,9 +79,13 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
   }
 }
 
-// DQM: dQ hand-off mode. 1 = f32 atomics into dQ [B,Hq,S_pad,D] (default);
+// DQM: dQ hand-off mode. 1 = f32 atomics into dQ [B,Hq,S_pad,D];
 // 2 = deterministic: plain stores of this key block's dQ partial into
 //     dQ + kb * B*Hq*S_pad*D, summed in key-block order by attn_bwd_dq_reduce;
+// 3 = split (default): no dQ work here; dS^T is stored (bf16) to a [BH, S_pad/64, Sk_pad, 64]
+//     buffer passed in place of dQ and attn_bwd_dq_kernel computes dQ = dS K per q block
+//     (no atomics, deterministic, and the key-block kernel loses 1/5 of its MFMAs and
+//     its dS LDS round trip);
 // 0 = dropped (ablation timing only).
 template <int D, bool CAUSAL, int DQM = 1>
 __global__ void __launch_bounds__(256, 1)
@@ -109,6 +125,9 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const float* delp = DELTA + (size_t)(b * Hq + h) * S;
   // rows padded to S_pad: the tail tile's atomics / stores need no guard
   float* dQp = dQ + (DQM == 2 ? (size_t)kb * BH * S_pad * D : 0) + (size_t)(b * Hq + h) * S_pad * D;
+  // DQM 3: dS^T of this q head, blocked by 64-q tiles: [S_pad/64][Sk_pad keys][64 q] bf16,
+  // so one (64-q tile, key range) piece is contiguous for both the writer and the reader
+  uint16_t* dstp = reinterpret_cast<uint16_t*>(dQ) + (size_t)(b * Hq + h) * (nkb * BN) * S_pad;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -195,6 +214,22 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     }
   };
 
+  // DQM 3: this wave's dS^T (32 keys x 64 q, bf16) of the previous q tile, stored after
+  // the next barrier so the stores drain during a whole tile of compute
+  u16x4 dsv[2][4];
+  int ds_q0 = -1;
+  auto flush_ds = [&]() {
+    if constexpr (DQM == 3) {
+      if (ds_q0 < 0) return;
+      uint16_t* rowp = dstp + ((size_t)(ds_q0 / BQ) * (nkb * BN) + (k0 + 32 * w + r)) * BQ;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          *reinterpret_cast<u16x4*>(rowp + 32 * m + 8 * gq + 4 * hh) = dsv[m][gq];
+    }
+  };
+
   if (nqt > 0) glds(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): prologue loads retired (visible to the waitcnt pass)
   __syncthreads();
@@ -207,6 +242,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     const float* del_s = lse_s + BQ;
     if (it + 1 < nqt) glds(it + 1, buf ^ 1);  // prefetch next tile (its buffer was last read before the barrier)
     flush_dq();                              // previous tile's dQ atomics overlap this tile's MFMAs
+    flush_ds();
     const bool need_mask = (q0 + BQ > S) || (k0 + BN > Sk) || (CAUSAL && (k0 + 32 * w + 31 > q0 + off));
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -273,8 +309,16 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         const int q = 32 * m + 8 * gq + 4 * hh;  // local q, multiple of 4
         const int chunk = q >> 3;
         u16x4 v4 = u16x4{f2bf(dp[4 * gq]), f2bf(dp[4 * gq + 1]), f2bf(dp[4 * gq + 2]), f2bf(dp[4 * gq + 3])};
-        *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swzb<8>(krow)) + 8 * hh) = v4;
+        if constexpr (DQM == 3)
+          dsv[m][gq] = v4;
+        else
+          *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swzb<8>(krow)) + 8 * hh) = v4;
       }
+    }
+    if constexpr (DQM == 3) {
+      ds_q0 = q0;
+      __syncthreads();  // this tile's Q/dO buffer consumed; next tile's DMA landed
+      continue;
     }
     __syncthreads();  // dS image complete (also retires the DMA + atomics issued above)
     // dQ[q0 .. q0+63][:] = scale * dS[64 x 128] . K[128 x D]  -> kept in `pend`, added next iteration
@@ -307,6 +351,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     __syncthreads();  // dS image consumed; next tile's DMA landed
   }
   flush_dq();
+  flush_ds();
   // write per-q-head dK/dV partials: C rows = d, col = key (lane)
   if (key < Sk) {
     float* dkq = dKp + ((size_t)(b * Hq + h) * Sk + key) * D;
@@ -347,22 +392,166 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_reduce(const float* __restric
   *reinterpret_cast<f32x4*>(dq + row * D + 4 * c) = acc;
 }
 
+
+// dQ for the split backward (DQM 3): one workgroup per (64-row q block, q head),
+// dQ[q0..q0+63][:] = scale * sum over key blocks of dS[64 x 64] . K[64 x D], with
+// dS^T tiles ([key][q] bf16, written by attn_bwd_kernel<.., 3>) and K tiles streamed
+// through LDS by LDS-DMA in a 3-stage ring (two tiles in flight while one is
+// consumed; counted vmcnt waits + bare s_barrier, so no barrier drains the ring),
+// tr-reads for both MFMA operands, f32 accumulators in registers, one plain store of
+// the result: no atomics.
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2)
+attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict__ K, float* __restrict__ dQ,
+                   int B, int Hq, int Hkv, int S, int Sk, int off, int S_pad, int Sk_pad, float scale) {
+  constexpr int BK = 64, BQ = 64, CH = D / 8, ROWB = D * 2, DB = D / 32, NSTAGE = 3;
+  constexpr int DSROWB = BQ * 2;     // dS^T image row: 64 q = 128 B
+  constexpr int KT = BK * ROWB;      // K tile [64][D]
+  constexpr int DT = BK * DSROWB;    // dS^T tile [64][64]
+  constexpr int BUF = KT + DT;
+  constexpr int NT = (2 * DB + 3) / 4;
+  constexpr int KSEG = KT / 1024, DSEG = DT / 1024;  // 1-KiB LDS-DMA segments
+  constexpr int PER_WAVE = (KSEG + DSEG) / 4;        // glds instructions per wave per stage
+  static_assert((KSEG + DSEG) % 4 == 0, "stage must split evenly over 4 waves");
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * BUF];
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+
+  const int nqb = (S + BQ - 1) / BQ;
+  const int BH = B * Hq;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = nqb - 1 - bid / BH;  // causal: last q blocks see the most keys -> first
+  const int bh = bid % BH;
+  const int b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
+  const int q0 = qb * BQ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const uint16_t* dsp = dST + (size_t)bh * Sk_pad * S_pad;
+  const uint16_t* Kp = K + (size_t)(b * Hkv + hk) * Sk * D;
+  // key blocks of 64 that the key-block kernel visited for this q block
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BQ + off);
+  const int nkt = (kend + BK - 1) / BK;
+
+  auto glds = [&](int it) {
+    char* kt = smem + (it % NSTAGE) * BUF;
+    char* dt = kt + KT;
+    const int kb0 = it * BK;
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int seg = w * PER_WAVE + i;
+      if (seg < KSEG) {
+        const int byte = seg * 1024 + lane * 16;
+        const int row = byte / ROWB, slot = (byte % ROWB) / 16;
+        const int ch = slot ^ swzb<CH>(row);
+        const int kk = min(kb0 + row, Sk - 1);
+        __builtin_amdgcn_global_load_lds((gptr_t)(Kp + (size_t)kk * D + ch * 8), (lptr_t)(kt + seg * 1024), 16, 0,
+                                         0);
+      } else {
+        const int sg = seg - KSEG;
+        const int byte = sg * 1024 + lane * 16;
+        const int row = byte / DSROWB, slot = (byte % DSROWB) / 16;
+        const int ch = slot ^ swzb<8>(row);
+        __builtin_amdgcn_global_load_lds((gptr_t)(dsp + ((size_t)qb * Sk_pad + kb0 + row) * BQ + ch * 8),
+                                         (lptr_t)(dt + sg * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+  // per-lane byte offsets of this wave's MFMA fragments inside one stage buffer
+  // (the k-step s only adds a compile-time 16-row offset: the swizzle of rows
+  // 16s + r0 does not depend on s)
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  uint32_t aA[NT], aB[NT], bA[NT], bB[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tile = min(w + 4 * t, 2 * DB - 1);
+    const int m = tile / DB, db = tile % DB;
+    const int rA0 = 4 * hh + tq, rB0 = rA0 + 8;
+    const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
+    const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+    aA[t] = KT + rA0 * DSROWB + 16 * (qchunk ^ swzb<8>(rA0)) + 8 * (tp & 1);
+    aB[t] = KT + rB0 * DSROWB + 16 * (qchunk ^ swzb<8>(rB0)) + 8 * (tp & 1);
+    bA[t] = rA0 * ROWB + 16 * (dchunk ^ swzb<CH>(rA0)) + 8 * (tp & 1);
+    bB[t] = rB0 * ROWB + 16 * (dchunk ^ swzb<CH>(rB0)) + 8 * (tp & 1);
+  }
+
+  if (nkt > 0) glds(0);
+  if (nkt > 1) glds(1);
+  for (int it = 0; it < nkt; ++it) {
+    // this wave's DMA for stage `it` retired (stage it+1 may stay in flight), then all waves'
+    if (it + 1 < nkt) __builtin_amdgcn_s_waitcnt(0x0F70 | (PER_WAVE & 0xF) | ((PER_WAVE >> 4) << 14));
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_barrier();  // also: every wave finished stage it-1, whose buffer is refilled below
+    if (it + 2 < nkt) glds(it + 2);
+    const uint32_t sb = lds0 + (uint32_t)((it % NSTAGE) * BUF);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (w + 4 * t < 2 * DB) {
+        u16x4 fa[4][2], fb[4][2];
+#define MX_DQ_READ(S)                                                  \
+  fa[S][0] = trd_asm<S * 16 * DSROWB>(sb + aA[t]);                     \
+  fa[S][1] = trd_asm<S * 16 * DSROWB>(sb + aB[t]);                     \
+  fb[S][0] = trd_asm<S * 16 * ROWB>(sb + bA[t]);                       \
+  fb[S][1] = trd_asm<S * 16 * ROWB>(sb + bB[t]);
+        MX_DQ_READ(0) MX_DQ_READ(1) MX_DQ_READ(2) MX_DQ_READ(3)
+#undef MX_DQ_READ
+        lds_wait();
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          pin(fa[s2][0]); pin(fa[s2][1]); pin(fb[s2][0]); pin(fb[s2][1]);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < BK / 16; ++s2) {
+          const u16x4 a0 = fa[s2][0], a1 = fa[s2][1], b0 = fb[s2][0], b1 = fb[s2][1];
+          acc[t] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]},
+                           u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc[t]);
+        }
+      }
+    }
+  }
+  // C layout: row = q0 + 32m + (j&3) + 8(j>>2) + 4hh, col = db*32 + r
+  float* dqp = dQ + (size_t)bh * S * D;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tile = w + 4 * t;
+    if (tile < 2 * DB) {
+      const int m = tile / DB, db = tile % DB;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (q < S) dqp[(size_t)q * D + db * 32 + r] = acc[t][j] * scale;
+      }
+    }
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
 
 // o: token-major rows with row stride ldo (elements); dout contiguous [B, S, Hq*D].
-// dq [B,Hq,ceil(S/64)*64,D] f32 must be ZEROED by the caller (f32 atomics; padded rows absorb
-// the unguarded tail atomics).  delta: workspace [B,Hq,S].
-// Deterministic mode (dq_part != nullptr): dq_part is a workspace of
-// ceil(Sk/128) * B*Hq*ceil(S/64)*64*D floats (no zeroing needed) and dq receives the
-// result unpadded, [B,Hq,S,D], reduced in a fixed order (bitwise reproducible).
+// dq_mode 1 (atomic): dq [B,Hq,ceil(S/64)*64,D] f32 must be ZEROED by the caller (padded
+//   rows absorb the unguarded tail atomics).
+// dq_mode 2 (deterministic): work = ceil(Sk/128) * B*Hq*ceil(S/64)*64*D floats (no
+//   zeroing); dq receives the result unpadded [B,Hq,S,D], reduced in a fixed order.
+// dq_mode 3 (split, default): work = B*Hq * ceil(Sk/128)*128 * ceil(S/64)*64 bf16 (dS^T,
+//   no zeroing); dq receives [B,Hq,S,D] from attn_bwd_dq_kernel.  Deterministic.
+// delta: workspace [B,Hq,S].
 extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
                            const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
-                           int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, float* dq_part,
-                           int64_t ldo, hipStream_t stream) {
+                           int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, int dq_mode,
+                           void* work, int64_t ldo, hipStream_t stream) {
   if (B <= 0 || S <= 0 || Sk <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return -1;
+  if (dq_mode < 1 || dq_mode > 3 || (dq_mode > 1 && !work)) return -1;
   const int64_t rows = (int64_t)B * S * Hq;
   const int64_t dthreads = rows * (D / 8);
   const unsigned dgrid = (unsigned)((dthreads + 255) / 256);
@@ -374,17 +563,19 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   const int grid = nkb * B * Hq;
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
-  const int S_pad = (S + 63) / 64 * 64;  // dq rows are padded (see mx_attn_bwd contract)
-  if (causal < 0) {  // ablation: no dQ atomics (timing experiments only; dq left zero)
+  const int S_pad = (S + 63) / 64 * 64;  // dq / dS^T rows are padded (see contract above)
+  if (causal < 0) {  // ablation: no dQ work at all (timing experiments only; dq left untouched)
     attn_bwd_kernel<128, true, 0><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv,
                                                             S, Sk, off, sl, scale, S_pad);
     return (int)hipGetLastError();
   }
-  const bool det = dq_part != nullptr;
-  float* dqk = det ? dq_part : dq;
+  float* dqk = dq_mode == 1 ? dq : reinterpret_cast<float*>(work);
 #define BWD(DD, C)                                                                                                  \
   do {                                                                                                              \
-    if (det)                                                                                                        \
+    if (dq_mode == 3)                                                                                               \
+      attn_bwd_kernel<DD, C, 3><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dqk, dkp, dvp, B, Hq, Hkv, S,  \
+                                                          Sk, off, sl, scale, S_pad);                               \
+    else if (dq_mode == 2)                                                                                          \
       attn_bwd_kernel<DD, C, 2><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dqk, dkp, dvp, B, Hq, Hkv, S,  \
                                                           Sk, off, sl, scale, S_pad);                               \
     else                                                                                                            \
@@ -396,18 +587,33 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   else if (D == 32) { if (causal) BWD(32, true); else BWD(32, false); }
   else return -1;
 #undef BWD
-  if (det) {
+  if (dq_mode == 2) {
     const int64_t n = (int64_t)B * Hq * S * (D / 4);
     const unsigned rg = (unsigned)((n + 255) / 256);
-#define RED(DD)                                                                                                   \
-  do {                                                                                                            \
-    if (causal) attn_bwd_dq_reduce<DD, true><<<rg, 256, 0, stream>>>(dq_part, dq, B * Hq, S, S_pad, nkb, off);    \
-    else attn_bwd_dq_reduce<DD, false><<<rg, 256, 0, stream>>>(dq_part, dq, B * Hq, S, S_pad, nkb, off);          \
+    float* part = reinterpret_cast<float*>(work);
+#define RED(DD)                                                                                                 \
+  do {                                                                                                          \
+    if (causal) attn_bwd_dq_reduce<DD, true><<<rg, 256, 0, stream>>>(part, dq, B * Hq, S, S_pad, nkb, off);     \
+    else attn_bwd_dq_reduce<DD, false><<<rg, 256, 0, stream>>>(part, dq, B * Hq, S, S_pad, nkb, off);           \
   } while (0)
     if (D == 128) RED(128);
     else if (D == 64) RED(64);
     else RED(32);
 #undef RED
+  } else if (dq_mode == 3) {
+    const int qgrid = ((S + 63) / 64) * B * Hq;
+    const uint16_t* dst = reinterpret_cast<const uint16_t*>(work);
+#define DQK(DD)                                                                                                  \
+  do {                                                                                                           \
+    if (causal) attn_bwd_dq_kernel<DD, true><<<qgrid, 256, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, \
+                                                                         nkb * 128, scale);                        \
+    else attn_bwd_dq_kernel<DD, false><<<qgrid, 256, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,       \
+                                                                   nkb * 128, scale);                              \
+  } while (0)
+    if (D == 128) DQK(128);
+    else if (D == 64) DQK(64);
+    else DQK(32);
+#undef DQK
   }
   return (int)hipGetLastError();
 }

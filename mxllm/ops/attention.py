@@ -9,8 +9,8 @@ re-layout tensors and no autograd shape constraints between them.
 GPU path (csrc/kernels/rope.hip, attn_fwd.hip, attn_bwd.hip):
   forward : qkv [T,(Hq+2Hkv)D] --rope_split--> q [B,Hq,S,D], k,v [B,Hkv,S,D]
             --attn_fwd (MFMA 32x32x16 bf16)--> o [B,S,Hq*D] token-major, lse [B,Hq,S]
-  backward: attn_bwd -> dq f32 [B,Hq,S,D] (f32 atomics, or per-key-block
-            partials + ordered reduction in deterministic mode), dk/dv partials
+  backward: attn_bwd -> dq f32 [B,Hq,S,D] (dS^T through HBM + a dQ kernel by
+            default; f32-atomic and partial-sum modes selectable), dk/dv partials
             [B,Hq,S,D] f32 --rope_merge_bwd--> d(qkv) bf16 [T,(Hq+2Hkv)D]
 """
 from __future__ import annotations
@@ -44,17 +44,21 @@ class _AttnBlockFn(torch.autograd.Function):
         q, k, v, o, lse, cos, sin = ctx.saved_tensors
         B, S, Hq, Hkv, D, causal, grad_pad = ctx.dims
         ops = native()
-        dq, dkp, dvp = ops.attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D),
-                                    deterministic())
+        dq, dkp, dvp = ops.attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D), dq_mode())
         dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D, grad_pad)
         return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
-def deterministic() -> bool:
-    """Ordered dQ reduction instead of f32 atomics (bitwise-reproducible
-    backward): on with ``torch.use_deterministic_algorithms(True)`` or
-    ``MXLLM_DETERMINISTIC=1``."""
-    return torch.are_deterministic_algorithms_enabled() or os.environ.get("MXLLM_DETERMINISTIC") == "1"
+def dq_mode() -> int:
+    """How the attention backward forms dQ (csrc/kernels/attn_bwd.hip):
+    3 = split (dS^T to HBM, separate dQ kernel; fastest and deterministic, default),
+    2 = per-key-block partials + ordered reduction, 1 = f32 atomics (non-deterministic).
+    ``MXLLM_ATTN_DQ_MODE`` overrides; with ``torch.use_deterministic_algorithms(True)``
+    or ``MXLLM_DETERMINISTIC=1`` mode 1 is never used."""
+    m = int(os.environ.get("MXLLM_ATTN_DQ_MODE", "3"))
+    if m == 1 and (torch.are_deterministic_algorithms_enabled() or os.environ.get("MXLLM_DETERMINISTIC") == "1"):
+        m = 3
+    return m
 
 
 def attention_block(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, S: int, Hq: int,
