@@ -393,51 +393,61 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_reduce(const float* __restric
 }
 
 
-// dQ for the split backward (DQM 3): one workgroup per (64-row q block, q head),
-// dQ[q0..q0+63][:] = scale * sum over key blocks of dS[64 x 64] . K[64 x D], with
-// dS^T tiles ([key][q] bf16, written by attn_bwd_kernel<.., 3>) and K tiles streamed
-// through LDS by LDS-DMA in a 3-stage ring (two tiles in flight while one is
-// consumed; counted vmcnt waits + bare s_barrier, so no barrier drains the ring),
-// tr-reads for both MFMA operands, f32 accumulators in registers, one plain store of
-// the result: no atomics.
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2)
+// dQ for the split backward (DQM 3): one workgroup per (QB x 64 q rows, q head), 4 waves
+// per 64-row sub-block, all sharing each streamed K tile (QB=2 halves K traffic):
+// dQ[q][:] = scale * sum over 64-key tiles of dS[64 x 64] . K[64 x D], with dS^T tiles
+// ([key][q] bf16, written by attn_bwd_kernel<.., 3>, blocked per 64-q tile) and K tiles
+// streamed through LDS by LDS-DMA in an NSTAGE ring (NSTAGE-1 tiles in flight while one
+// is consumed; counted vmcnt waits + bare s_barrier so no barrier drains the ring),
+// inline-asm tr-reads for both MFMA operands (a builtin tr-read would make hipcc drain
+// the in-flight DMA), f32 accumulators in registers, one plain store: no atomics.
+template <int D, bool CAUSAL, int QB>
+__global__ void __launch_bounds__(256 * QB, 1)
 attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict__ K, float* __restrict__ dQ,
                    int B, int Hq, int Hkv, int S, int Sk, int off, int S_pad, int Sk_pad, float scale) {
-  constexpr int BK = 64, BQ = 64, CH = D / 8, ROWB = D * 2, DB = D / 32, NSTAGE = 3;
+  constexpr int BK = 64, BQ = 64, CH = D / 8, ROWB = D * 2, DB = D / 32;
   constexpr int DSROWB = BQ * 2;     // dS^T image row: 64 q = 128 B
   constexpr int KT = BK * ROWB;      // K tile [64][D]
-  constexpr int DT = BK * DSROWB;    // dS^T tile [64][64]
-  constexpr int BUF = KT + DT;
+  constexpr int DT = BK * DSROWB;    // one dS^T tile [64 keys][64 q]
+  constexpr int BUF = KT + QB * DT;
+  constexpr int NSTAGE = QB == 1 ? 3 : 4;
   constexpr int NT = (2 * DB + 3) / 4;
-  constexpr int KSEG = KT / 1024, DSEG = DT / 1024;  // 1-KiB LDS-DMA segments
-  constexpr int PER_WAVE = (KSEG + DSEG) / 4;        // glds instructions per wave per stage
-  static_assert((KSEG + DSEG) % 4 == 0, "stage must split evenly over 4 waves");
+  constexpr int KSEG = KT / 1024, DSEG = DT / 1024;     // 1-KiB LDS-DMA segments
+  constexpr int NW = 4 * QB;                            // waves
+  constexpr int PER_WAVE = (KSEG + QB * DSEG) / NW;     // glds instructions per wave per stage
+  static_assert((KSEG + QB * DSEG) % NW == 0, "stage must split evenly over the waves");
+  static_assert(PER_WAVE <= 15, "vmcnt immediate");
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * BUF];
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
 
-  const int nqb = (S + BQ - 1) / BQ;
+  const int nqb = (S + BQ * QB - 1) / (BQ * QB);
   const int BH = B * Hq;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = nqb - 1 - bid / BH;  // causal: last q blocks see the most keys -> first
   const int bh = bid % BH;
   const int b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
-  const int q0 = qb * BQ;
+  const int q0 = qb * BQ * QB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sub = w / 4, wl = w % 4;  // 64-row sub-block of this wave, wave index within it
   const int r = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
   const uint16_t* dsp = dST + (size_t)bh * Sk_pad * S_pad;
   const uint16_t* Kp = K + (size_t)(b * Hkv + hk) * Sk * D;
-  // key blocks of 64 that the key-block kernel visited for this q block
-  int kend = Sk;
-  if (CAUSAL) kend = min(Sk, q0 + BQ + off);
+  // 64-key tiles the key-block kernel wrote for this workgroup (last sub-block) and for
+  // this wave's sub-block (tiles past it were never written: skipped)
+  int kend = Sk, kend_w = Sk;
+  if (CAUSAL) {
+    kend = min(Sk, q0 + BQ * QB + off);
+    kend_w = min(Sk, q0 + BQ * (sub + 1) + off);
+  }
   const int nkt = (kend + BK - 1) / BK;
+  const int nkt_w = (kend_w + BK - 1) / BK;
+  const int qsub0 = q0 + BQ * sub;
 
   auto glds = [&](int it) {
     char* kt = smem + (it % NSTAGE) * BUF;
-    char* dt = kt + KT;
     const int kb0 = it * BK;
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) {
@@ -450,12 +460,15 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
         __builtin_amdgcn_global_load_lds((gptr_t)(Kp + (size_t)kk * D + ch * 8), (lptr_t)(kt + seg * 1024), 16, 0,
                                          0);
       } else {
-        const int sg = seg - KSEG;
-        const int byte = sg * 1024 + lane * 16;
+        const int sg = seg - KSEG;          // over QB dS^T tiles
+        const int jt = sg / DSEG, sgl = sg % DSEG;
+        const int byte = sgl * 1024 + lane * 16;
         const int row = byte / DSROWB, slot = (byte % DSROWB) / 16;
         const int ch = slot ^ swzb<8>(row);
-        __builtin_amdgcn_global_load_lds((gptr_t)(dsp + ((size_t)qb * Sk_pad + kb0 + row) * BQ + ch * 8),
-                                         (lptr_t)(dt + sg * 1024), 16, 0, 0);
+        const int qt64 = q0 / BQ + jt;  // 64-q tile index; clamp a tail tile past S_pad
+        const int qtc = min(qt64, S_pad / BQ - 1);
+        __builtin_amdgcn_global_load_lds((gptr_t)(dsp + ((size_t)qtc * Sk_pad + kb0 + row) * BQ + ch * 8),
+                                         (lptr_t)(kt + KT + jt * DT + sgl * 1024), 16, 0, 0);
       }
     }
   };
@@ -472,61 +485,67 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
   uint32_t aA[NT], aB[NT], bA[NT], bB[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int tile = min(w + 4 * t, 2 * DB - 1);
+    const int tile = min(wl + 4 * t, 2 * DB - 1);
     const int m = tile / DB, db = tile % DB;
     const int rA0 = 4 * hh + tq, rB0 = rA0 + 8;
     const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
     const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
-    aA[t] = KT + rA0 * DSROWB + 16 * (qchunk ^ swzb<8>(rA0)) + 8 * (tp & 1);
-    aB[t] = KT + rB0 * DSROWB + 16 * (qchunk ^ swzb<8>(rB0)) + 8 * (tp & 1);
+    aA[t] = KT + sub * DT + rA0 * DSROWB + 16 * (qchunk ^ swzb<8>(rA0)) + 8 * (tp & 1);
+    aB[t] = KT + sub * DT + rB0 * DSROWB + 16 * (qchunk ^ swzb<8>(rB0)) + 8 * (tp & 1);
     bA[t] = rA0 * ROWB + 16 * (dchunk ^ swzb<CH>(rA0)) + 8 * (tp & 1);
     bB[t] = rB0 * ROWB + 16 * (dchunk ^ swzb<CH>(rB0)) + 8 * (tp & 1);
   }
 
-  if (nkt > 0) glds(0);
-  if (nkt > 1) glds(1);
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p)
+    if (p < nkt) glds(p);
   for (int it = 0; it < nkt; ++it) {
-    // this wave's DMA for stage `it` retired (stage it+1 may stay in flight), then all waves'
-    if (it + 1 < nkt) __builtin_amdgcn_s_waitcnt(0x0F70 | (PER_WAVE & 0xF) | ((PER_WAVE >> 4) << 14));
+    // this wave's DMA for stage `it` retired (up to NSTAGE-2 later stages may stay in
+    // flight), then every wave's
+    const int ahead = min(NSTAGE - 2, nkt - 1 - it);
+    if (ahead >= 2) __builtin_amdgcn_s_waitcnt(0x0F70 | ((2 * PER_WAVE) & 0xF) | (((2 * PER_WAVE) >> 4) << 14));
+    else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | (PER_WAVE & 0xF) | ((PER_WAVE >> 4) << 14));
     else __builtin_amdgcn_s_waitcnt(0x0F70);
     __builtin_amdgcn_s_barrier();  // also: every wave finished stage it-1, whose buffer is refilled below
-    if (it + 2 < nkt) glds(it + 2);
-    const uint32_t sb = lds0 + (uint32_t)((it % NSTAGE) * BUF);
+    if (it + NSTAGE - 1 < nkt) glds(it + NSTAGE - 1);
+    if (it < nkt_w) {
+      const uint32_t sb = lds0 + (uint32_t)((it % NSTAGE) * BUF);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if (w + 4 * t < 2 * DB) {
-        u16x4 fa[4][2], fb[4][2];
+      for (int t = 0; t < NT; ++t) {
+        if (wl + 4 * t < 2 * DB) {
+          u16x4 fa[4][2], fb[4][2];
 #define MX_DQ_READ(S)                                                  \
   fa[S][0] = trd_asm<S * 16 * DSROWB>(sb + aA[t]);                     \
   fa[S][1] = trd_asm<S * 16 * DSROWB>(sb + aB[t]);                     \
   fb[S][0] = trd_asm<S * 16 * ROWB>(sb + bA[t]);                       \
   fb[S][1] = trd_asm<S * 16 * ROWB>(sb + bB[t]);
-        MX_DQ_READ(0) MX_DQ_READ(1) MX_DQ_READ(2) MX_DQ_READ(3)
+          MX_DQ_READ(0) MX_DQ_READ(1) MX_DQ_READ(2) MX_DQ_READ(3)
 #undef MX_DQ_READ
-        lds_wait();
+          lds_wait();
 #pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          pin(fa[s2][0]); pin(fa[s2][1]); pin(fb[s2][0]); pin(fb[s2][1]);
-        }
+          for (int s2 = 0; s2 < 4; ++s2) {
+            pin(fa[s2][0]); pin(fa[s2][1]); pin(fb[s2][0]); pin(fb[s2][1]);
+          }
 #pragma unroll
-        for (int s2 = 0; s2 < BK / 16; ++s2) {
-          const u16x4 a0 = fa[s2][0], a1 = fa[s2][1], b0 = fb[s2][0], b1 = fb[s2][1];
-          acc[t] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]},
-                           u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc[t]);
+          for (int s2 = 0; s2 < BK / 16; ++s2) {
+            const u16x4 a0 = fa[s2][0], a1 = fa[s2][1], b0 = fb[s2][0], b1 = fb[s2][1];
+            acc[t] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]},
+                             u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, acc[t]);
+          }
         }
       }
     }
   }
-  // C layout: row = q0 + 32m + (j&3) + 8(j>>2) + 4hh, col = db*32 + r
+  // C layout: row = qsub0 + 32m + (j&3) + 8(j>>2) + 4hh, col = db*32 + r
   float* dqp = dQ + (size_t)bh * S * D;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int tile = w + 4 * t;
+    const int tile = wl + 4 * t;
     if (tile < 2 * DB) {
       const int m = tile / DB, db = tile % DB;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const int q = q0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        const int q = qsub0 + 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
         if (q < S) dqp[(size_t)q * D + db * 32 + r] = acc[t][j] * scale;
       }
     }
@@ -601,14 +620,19 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     else RED(32);
 #undef RED
   } else if (dq_mode == 3) {
-    const int qgrid = ((S + 63) / 64) * B * Hq;
+    // 128 q rows per workgroup (every K tile feeds two 64-row sub-blocks); D=32 keeps 64
+    const int qbs = D == 32 ? 1 : 2;
+    const int qgrid = ((S + 64 * qbs - 1) / (64 * qbs)) * B * Hq;
     const uint16_t* dst = reinterpret_cast<const uint16_t*>(work);
-#define DQK(DD)                                                                                                  \
-  do {                                                                                                           \
-    if (causal) attn_bwd_dq_kernel<DD, true><<<qgrid, 256, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, \
-                                                                         nkb * 128, scale);                        \
-    else attn_bwd_dq_kernel<DD, false><<<qgrid, 256, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,       \
-                                                                   nkb * 128, scale);                              \
+#define DQK(DD)                                                                                                   \
+  do {                                                                                                            \
+    constexpr int QB = DD == 32 ? 1 : 2;                                                                          \
+    if (causal)                                                                                                   \
+      attn_bwd_dq_kernel<DD, true, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,  \
+                                                                       nkb * 128, scale);                         \
+    else                                                                                                          \
+      attn_bwd_dq_kernel<DD, false, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, \
+                                                                        nkb * 128, scale);                        \
   } while (0)
     if (D == 128) DQK(128);
     else if (D == 64) DQK(64);
