@@ -410,7 +410,7 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
   constexpr int KT = BK * ROWB;      // K tile [64][D]
   constexpr int DT = BK * DSROWB;    // one dS^T tile [64 keys][64 q]
   constexpr int BUF = KT + QB * DT;
-  constexpr int NSTAGE = QB == 1 ? 3 : 4;
+  constexpr int NSTAGE = QB == 2 ? 4 : 3;
   constexpr int NT = (2 * DB + 3) / 4;
   constexpr int KSEG = KT / 1024, DSEG = DT / 1024;     // 1-KiB LDS-DMA segments
   constexpr int NW = 4 * QB;                            // waves
@@ -621,12 +621,12 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
 #undef RED
   } else if (dq_mode == 3) {
     // 128 q rows per workgroup (every K tile feeds two 64-row sub-blocks); D=32 keeps 64
-    const int qbs = D == 32 ? 1 : 2;
+    const int qbs = D == 128 ? 4 : (D == 64 ? 2 : 1);
     const int qgrid = ((S + 64 * qbs - 1) / (64 * qbs)) * B * Hq;
     const uint16_t* dst = reinterpret_cast<const uint16_t*>(work);
 #define DQK(DD)                                                                                                   \
   do {                                                                                                            \
-    constexpr int QB = DD == 32 ? 1 : 2;                                                                          \
+    constexpr int QB = DD == 128 ? 4 : (DD == 64 ? 2 : 1);                                                        \
     if (causal)                                                                                                   \
       attn_bwd_dq_kernel<DD, true, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,  \
                                                                        nkb * 128, scale);                         \
