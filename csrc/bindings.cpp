@@ -157,11 +157,16 @@ at::Tensor segmented_mean(const at::Tensor& codes, const at::Tensor& offsets) {
   return out;
 }
 
-at::Tensor sqnorm_f32(const at::Tensor& x) {
-  check_f32(x, "x");
+// sum(x^2) of a contiguous f32 or bf16 GPU tensor -> f32 [1]; fixed-order reduction
+at::Tensor sqnorm(const at::Tensor& x) {
+  MX_CHECK(x.is_cuda() && x.is_contiguous(), "x must be a contiguous GPU tensor");
+  MX_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   DevGuard g(x.device());
-  auto out = at::zeros({1}, x.options());
-  MX_OK(mx_sqnorm_f32(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), cur_stream()));
+  auto opts = x.options().dtype(at::kFloat);
+  auto out = at::empty({1}, opts);
+  auto work = at::empty({2048}, opts);
+  MX_OK(mx_sqnorm(x.data_ptr(), x.scalar_type() == at::kBFloat16 ? 1 : 0, x.numel(), out.data_ptr<float>(),
+                  work.data_ptr<float>(), cur_stream()));
   return out;
 }
 
@@ -451,7 +456,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw, int out_pad=0) -> (Tensor, Tensor)");
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
-  m.def("sqnorm_f32(Tensor x) -> Tensor");
+  m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
   m.def("adamw_step(Tensor(a!) master, Tensor grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f) -> ()");
@@ -473,7 +478,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("segmented_mean", &segmented_mean);
   m.impl("copy2d_batched", &copy2d_batched);
-  m.impl("sqnorm_f32", &sqnorm_f32);
+  m.impl("sqnorm", &sqnorm);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("adamw_step", &adamw_step);

@@ -16,7 +16,7 @@ int mx_colsum_f32(const float* p, float* out, int nblk, int H, hipStream_t strea
 // misc.hip
 int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, float* out, int nseg,
                           hipStream_t stream);
-int mx_sqnorm_f32(const float* x, int64_t n, float* out, hipStream_t stream);
+int mx_sqnorm(const void* x, int bf16, int64_t n, float* out, float* work, hipStream_t stream);
 int mx_copy2d_batched(const int64_t* desc, int n, int64_t total_blocks, hipStream_t stream);
 }
 

@@ -22,22 +22,51 @@ __global__ void __launch_bounds__(256) segmented_mean_kernel(const int32_t* __re
   if (lane == 0) out[seg] = (e > b) ? (float)(s / (double)(e - b)) : NAN;
 }
 
-// sum of squares of an f32 vector into out[slot] (atomic, one per block).
-__global__ void __launch_bounds__(256) sqnorm_f32_kernel(const float* __restrict__ x, int64_t n,
-                                                         float* __restrict__ out) {
+// sum of squares of an f32 or bf16 vector: per-block partials, then ONE block sums
+// them in a fixed order -> bitwise identical on every DDP rank (the grad-clip
+// coefficient must not differ between replicas), no atomics.
+constexpr int kSqBlocks = 2048;
+
+template <typename T>
+__global__ void __launch_bounds__(256) sqnorm_partial_kernel(const T* __restrict__ x, int64_t n,
+                                                             float* __restrict__ part) {
   __shared__ float scratch[16];
   float s = 0.f;
-  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
-    if (i + 3 < n) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
-      s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  constexpr int V = 16 / sizeof(T);  // elements per 16-B load
+  const int64_t stride = (int64_t)gridDim.x * 256 * V;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V; i < n; i += stride) {
+    if (i + V - 1 < n) {
+      if constexpr (sizeof(T) == 4) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+        s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      } else {
+        u16x8 v = *reinterpret_cast<const u16x8*>(x + i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f(v[j]);
+          s += f * f;
+        }
+      }
     } else {
-      for (int64_t j = i; j < n; ++j) s += x[j] * x[j];
+      for (int64_t j = i; j < n; ++j) {
+        float f;
+        if constexpr (sizeof(T) == 4) f = x[j];
+        else f = bf2f(x[j]);
+        s += f * f;
+      }
     }
   }
   s = block_sum(s, scratch);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, int n,
+                                                           float* __restrict__ out) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) out[0] = s;
 }
 
 // Batched strided 2-D copy of 16-bit elements: one launch refreshes every LoRA
@@ -84,10 +113,20 @@ extern "C" int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, 
   return (int)hipGetLastError();
 }
 
-extern "C" int mx_sqnorm_f32(const float* x, int64_t n, float* out, hipStream_t stream) {
-  if (n <= 0) return 0;
-  int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  sqnorm_f32_kernel<<<(int)blocks, 256, 0, stream>>>(x, n, out);
+// out: 1 float; work: kSqBlocks floats.  bf16 != 0: x is bf16.
+extern "C" int mx_sqnorm(const void* x, int bf16, int64_t n, float* out, float* work, hipStream_t stream) {
+  if (n <= 0) {
+    hipMemsetAsync(out, 0, sizeof(float), stream);
+    return (int)hipGetLastError();
+  }
+  const int V = bf16 ? 8 : 4;
+  int64_t blocks = (n / V + 255) / 256;
+  if (blocks > kSqBlocks) blocks = kSqBlocks;
+  if (blocks < 1) blocks = 1;
+  if (bf16)
+    sqnorm_partial_kernel<uint16_t><<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<const uint16_t*>(x), n, work);
+  else
+    sqnorm_partial_kernel<float><<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<const float*>(x), n, work);
+  sum_partials_kernel<<<1, 256, 0, stream>>>(work, (int)blocks, out);
   return (int)hipGetLastError();
 }

@@ -173,7 +173,38 @@ def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: tor
     return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad)
 
 
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T whose weight gradient is accumulated by the dW GEMM itself into
+    the preallocated flat .grad (beta = 1) — no separate dW tensor and no
+    AccumulateGrad add pass over it (full fine-tuning: ~16 GB of weight
+    gradient per 8B step) — and DDP is told via ``mark_ready``."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(x2, w)
+        ctx.xshape = x.shape
+        return torch.mm(x2, w.t()).view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0])
+        dx = torch.mm(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            g = direct_grad(w)
+            if g is not None:
+                g.addmm_(dy2.t(), x2)
+                mark_ready(w)
+            else:
+                dw = torch.mm(dy2.t(), x2)
+        return dx, dw
+
+
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if w.requires_grad and torch.is_grad_enabled():
+        return _LinearFn.apply(x, w)
     return F.linear(x, w)
 
 

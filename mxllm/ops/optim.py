@@ -35,7 +35,9 @@ def adamw_step_(master: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: to
 
 
 def sq_norm(x: torch.Tensor) -> torch.Tensor:
-    """sum(x^2) as a 1-element fp32 tensor (no host sync)."""
-    if use_native(x) and x.dtype == torch.float32 and x.is_contiguous():
-        return native().sqnorm_f32(x)
+    """sum(x^2) as a 1-element fp32 tensor (no host sync).  GPU: one read of x
+    (f32 or bf16) with a fixed-order reduction, so every DDP replica computes the
+    bitwise-same clip coefficient."""
+    if use_native(x) and x.dtype in (torch.float32, torch.bfloat16) and x.is_contiguous():
+        return native().sqnorm(x)
     return x.float().pow(2).sum().reshape(1)

@@ -232,3 +232,16 @@ def test_segmented_mean(gpu):
     out = _ops().segmented_mean(codes, offs).cpu()
     for i, t in enumerate(texts):
         assert abs(out[i].item() - torch.tensor([ord(c) for c in t], dtype=torch.float32).mean().item()) < 1e-3
+
+
+@pytest.mark.parametrize("dtype,n", [(torch.float32, 1_000_003), (torch.bfloat16, 3_000_001), (torch.bfloat16, 7)])
+def test_sq_norm_deterministic(gpu, dtype, n):
+    """sum(x^2) for f32 and bf16 (one read, fixed-order reduction): matches fp64,
+    and is bitwise identical across calls (DDP replicas must agree on the clip)."""
+    from mxllm.ops import sq_norm
+
+    x = torch.randn(n, device=gpu).to(dtype)
+    a, b = sq_norm(x), sq_norm(x)
+    assert torch.equal(a, b)
+    ref = x.double().pow(2).sum().item()
+    assert abs(a.item() - ref) / ref < 1e-5
