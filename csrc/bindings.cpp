@@ -420,7 +420,8 @@ at::Tensor rope_append(const at::Tensor& qkv, const at::Tensor& cos, const at::T
 }
 
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
-                       const at::Tensor& lens, const c10::optional<at::Tensor>& slots, int64_t max_len, double scale) {
+                       const at::Tensor& lens, const c10::optional<at::Tensor>& slots, int64_t max_len, double scale,
+                       int64_t len_off) {
   check_bf16(q, "q");
   MX_CHECK(lens.scalar_type() == at::kInt, "lens int32");
   const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
@@ -432,7 +433,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   auto out = at::empty({B, Hq * D}, q.options());
   const int32_t* sl = nullptr;
   if (slots.has_value()) sl = slots->data_ptr<int32_t>();
-  MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), sl, ml.data_ptr<float>(),
+  MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), (int)len_off, sl, ml.data_ptr<float>(),
                        po.data_ptr<float>(), bfm(out), (int)B, (int)Hq, (int)Hkv, (int)D, (int)max_seq, (int)nsplit,
                        (float)scale, cur_stream()));
   return out;
@@ -467,7 +468,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
   m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D) -> Tensor");
-  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale) -> Tensor");
+  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3) -> (Tensor, Tensor, Tensor)");

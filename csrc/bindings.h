@@ -54,7 +54,7 @@ extern "C" {
 int mx_rope_append(const uint16_t* qkv, const float* cosb, const float* sinb, const int32_t* pos, const int32_t* slots,
                    uint16_t* q, uint16_t* kc, uint16_t* vc, int B, int Hq, int Hkv, int D, int max_seq,
                    hipStream_t stream);
-int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens,
+int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens, int len_off,
                    const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B, int Hq, int Hkv, int D,
                    int max_seq, int nsplit, float scale, hipStream_t stream);
 int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature, uint32_t seed,

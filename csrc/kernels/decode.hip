@@ -67,7 +67,7 @@ template <int D>
 __global__ void __launch_bounds__(256) decode_attn_kernel(const uint16_t* __restrict__ q,
                                                           const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
-                                                          const int32_t* __restrict__ lens,
+                                                          const int32_t* __restrict__ lens, int len_off,
                                                           const int32_t* __restrict__ slots,
                                                           float* __restrict__ part_ml, float* __restrict__ part_o,
                                                           int Hq, int Hkv, int max_seq, int nsplit, float sl) {
@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const uint16_t* __rest
   __shared__ __attribute__((aligned(16))) uint16_t vs[kSplit * D];
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int rep = Hq / Hkv;
-  const int len = lens[b];
+  const int len = lens[b] + len_off;
   const int slot = slots ? slots[b] : b;
   const int k_lo = split * kSplit;
   const int k_hi = min(len, k_lo + kSplit);
@@ -175,6 +175,192 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const uint16_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// MFMA decode attention, D = 128 (every Llama-3.x model).  Memory-bound: the
+// whole point is to stream each (seq, kv-head)'s cached K/V rows once at HBM
+// rate, so
+//   * a workgroup = 4 waves = 256 keys of one (seq, kv-head); each wave owns 64
+//     keys and keeps its own online-softmax state (no barrier in the key loop);
+//   * scores for ALL q-heads of the GQA group at once with
+//     v_mfma_f32_16x16x32_bf16: S^T[key][head] = K . Q^T, K rows loaded straight
+//     from HBM into the A fragments (16 B per lane), Q^T (heads padded to 16)
+//     as the B fragment;
+//   * the S^T accumulator (head on the lane, keys in registers) converted to
+//     bf16 IS the B operand of O^T[d][head] += V^T . P (keys permuted inside
+//     each 32-key k-step to match the accumulator's row order);
+//   * V^T fragments come from a row-major V image in LDS through
+//     ds_read_b64_tr_b16; the image is filled by LDS-DMA (global_load_lds,
+//     source-swizzled so the transposed reads are conflict-free);
+//   * the four waves' partials are merged through LDS (each wave reuses its own
+//     V region) into one (m, l, o) partial per split, the format of
+//     decode_combine_kernel.
+// 64 KiB LDS and < 128 VGPRs: two workgroups (8 waves) per CU, 256 KiB of K/V
+// in flight per CU.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                 c, 0, 0, 0);
+}
+
+__device__ __forceinline__ u16x4 tr_read16(const char* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(u16x4, v);
+}
+
+// 16-B chunk swizzle of a 256-B row (conflict-free row and transposed reads)
+__device__ __forceinline__ int dswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+__global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t* __restrict__ q,
+                                                                  const uint16_t* __restrict__ kc,
+                                                                  const uint16_t* __restrict__ vc,
+                                                                  const int32_t* __restrict__ lens, int len_off,
+                                                                  const int32_t* __restrict__ slots,
+                                                                  float* __restrict__ part_ml,
+                                                                  float* __restrict__ part_o, int Hq, int Hkv,
+                                                                  int max_seq, int nsplit, float sl) {
+  constexpr int D = 128, ROWB = 256, WKEYS = 64, WTILE = WKEYS * ROWB;  // 16 KiB per wave
+  __shared__ __attribute__((aligned(16))) char smem[4 * WTILE];
+  __shared__ float mls[4][2][16];
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int rep = Hq / Hkv;
+  const int len = lens[b] + len_off;
+  const int slot = slots ? slots[b] : b;
+  const int k_lo = split * kSplit;
+  const int k_hi = min(len, k_lo + kSplit);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  float* pml = part_ml + (((int64_t)b * Hq + hk * rep) * nsplit + split) * 2;
+  if (k_lo >= k_hi) {  // empty split (workgroup-uniform): neutral partial
+    if (tid < rep) {
+      pml[(int64_t)tid * nsplit * 2] = -INFINITY;
+      pml[(int64_t)tid * nsplit * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  const uint16_t* kbase = kc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
+  const uint16_t* vbase = vc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
+  const int wk0 = k_lo + WKEYS * w;
+  char* vs = smem + w * WTILE;
+
+  // V rows of this wave -> LDS (16 x 1-KiB lane-linear DMA pieces; swizzle by
+  // permuting each lane's SOURCE chunk).  Rows past k_hi duplicate a valid row
+  // (finite; their probabilities are exactly 0).
+#pragma unroll
+  for (int seg = 0; seg < 16; ++seg) {
+    const int row = seg * 4 + (lane >> 4), slt = lane & 15;
+    const int ch = slt ^ dswz(row);
+    const int key = min(wk0 + row, k_hi - 1);
+    __builtin_amdgcn_global_load_lds((gptr_t)(vbase + (int64_t)key * D + ch * 8), (lptr_t)(vs + seg * 1024), 16, 0,
+                                     0);
+  }
+  // Q^T fragments (B operand): lane (c, g) holds Q[head c][32 s + 8 g .. +7]
+  u16x8 qf[4];
+  const uint16_t* qrow = q + ((int64_t)b * Hq + hk * rep + min(c, rep - 1)) * D;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *reinterpret_cast<const u16x8*>(qrow + 32 * s + 8 * g);
+    if (c >= rep) qf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  // K fragments (A operand), straight from HBM: block j, k-step s ->
+  // K[wk0 + 16 j + c][32 s + 8 g .. +7]
+  u16x8 kf[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int key = min(wk0 + 16 * j + c, k_hi - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[j][s] = *reinterpret_cast<const u16x8*>(kbase + (int64_t)key * D + 32 * s + 8 * g);
+  }
+  f32x4 sacc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc[j] = mfma16(kf[j][s], qf[s], sacc[j]);
+  }
+  // softmax over this wave's 64 keys, per head (= lane column c); lane (c, g)
+  // holds keys wk0 + 16 j + 4 g + i
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = wk0 + 16 * j + 4 * g + i;
+      const float x = key < k_hi ? sacc[j][i] * sl : -INFINITY;
+      sacc[j][i] = x;
+      mx = fmaxf(mx, x);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float mref = mx == -INFINITY ? 0.f : mx;  // wave with no valid key: all p = 0
+  float ls = 0.f;
+  u16x8 pb[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = __builtin_amdgcn_exp2f(sacc[j][i] - mref);
+      ls += p;
+      pb[j >> 1][4 * (j & 1) + i] = f2bf(p);
+    }
+  ls += __shfl_xor(ls, 16, 64);
+  ls += __shfl_xor(ls, 32, 64);
+
+  // O^T[d][head] += V^T . P; k-step t covers keys 32 t + {16 h + 4 g + i}
+  f32x4 oacc[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's V DMA has landed (only it reads vs)
+  const int qq = c >> 2, pp = c & 3;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int r0 = 32 * t + 4 * g + qq, r1 = r0 + 16;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      const int ch = 2 * db + (pp >> 1);
+      const u16x4 va = tr_read16(vs + r0 * ROWB + 16 * (ch ^ dswz(r0)) + 8 * (pp & 1));
+      const u16x4 vb = tr_read16(vs + r1 * ROWB + 16 * (ch ^ dswz(r1)) + 8 * (pp & 1));
+      const u16x8 a = u16x8{va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+      oacc[db] = mfma16(a, pb[t], oacc[db]);
+    }
+  }
+  // merge the four waves: each wave parks (m, l, O^T) in its own V region
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's transposed reads retired
+  float* so = reinterpret_cast<float*>(vs);  // [d][16 heads]
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) so[(16 * db + 4 * g + i) * 16 + c] = oacc[db][i];
+  if (g == 0) {
+    mls[w][0][c] = mx;
+    mls[w][1][c] = ls;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < rep * D; idx += 256) {
+    const int h = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, mls[ww][0][h]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float mw = mls[ww][0][h];
+      const float f = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);
+      L += f * mls[ww][1][h];
+      acc += f * reinterpret_cast<const float*>(smem + ww * WTILE)[d * 16 + h];
+    }
+    part_o[(((int64_t)b * Hq + hk * rep + h) * nsplit + split) * D + d] = acc;
+    if (d == 0) {
+      pml[(int64_t)h * nsplit * 2] = M;
+      pml[(int64_t)h * nsplit * 2 + 1] = L;
+    }
+  }
+}
+
 // merge splits: out[b, h, :] = sum_s exp2(m_s - M) o_s / sum_s exp2(m_s - M) l_s
 template <int D>
 __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restrict__ part_ml,
@@ -255,17 +441,23 @@ extern "C" int mx_rope_append(const uint16_t* qkv, const float* cosb, const floa
 }
 
 extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens,
-                              const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B, int Hq,
-                              int Hkv, int D, int max_seq, int nsplit, float scale, hipStream_t stream) {
+                              int len_off, const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B,
+                              int Hq, int Hkv, int D, int max_seq, int nsplit, float scale, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > kMaxRep) return -1;
   dim3 grid(nsplit, Hkv, B);
   const float sl = scale * 1.4426950408889634f;
-#define DA(DD)                                                                                                 \
-  decode_attn_kernel<DD><<<grid, 256, 0, stream>>>(q, kc, vc, lens, slots, part_ml, part_o, Hq, Hkv, max_seq, \
-                                                   nsplit, sl);                                                \
+  if (D == 128) {
+    decode_attn_mfma_kernel<<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv,
+                                                      max_seq, nsplit, sl);
+    decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
+    return (int)hipGetLastError();
+  }
+#define DA(DD)                                                                                                  \
+  decode_attn_kernel<DD><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv, \
+                                                   max_seq, nsplit, sl);                                        \
   decode_combine_kernel<DD><<<B * Hq, DD, 0, stream>>>(part_ml, part_o, out, nsplit)
-  if (D == 128) { DA(128); } else if (D == 64) { DA(64); } else if (D == 32) { DA(32); } else return -1;
+  if (D == 64) { DA(64); } else if (D == 32) { DA(32); } else return -1;
 #undef DA
   return (int)hipGetLastError();
 }

@@ -40,7 +40,7 @@ def decode_attention(qkv: torch.Tensor, cos, sin, k_cache, v_cache, pos: torch.T
     if use_native(qkv):
         ops = native()
         q = ops.rope_append(qkv.contiguous(), cos, sin, pos, slots, k_cache, v_cache, Hq, Hkv, D)
-        return ops.decode_attn(q, k_cache, v_cache, pos + 1, slots, max_len, 1.0 / math.sqrt(D))
+        return ops.decode_attn(q, k_cache, v_cache, pos, slots, max_len, 1.0 / math.sqrt(D), 1)
     B = qkv.shape[0]
     x = qkv.view(B, Hq + 2 * Hkv, D).float()
     outs = []

@@ -46,22 +46,26 @@ def test_train_step_matches_reference_path(gpu, preset, lora, monkeypatch):
             assert e < 6e-2, (n, e)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 32, 8), (32, 8, 2)])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (128, 32, 8), (128, 64, 8), (128, 16, 1), (64, 32, 8), (32, 8, 2)])
 def test_decode_kernels(gpu, D, Hq, Hkv):
+    """rope_append + decode attention (D=128: the MFMA kernel) vs an fp32 reference:
+    GQA group sizes 4 / 8 / 16, key counts at and around the 64-key wave and
+    256-key split boundaries, permuted cache slots."""
     from mxllm.ops import native
 
     torch.manual_seed(1)
-    B, max_seq = 3, 700
-    lens = [5, 300, 640]
-    kc = torch.randn(4, Hkv, max_seq, D, device=gpu, dtype=torch.bfloat16)
+    max_seq = 700
+    lens = [0, 5, 63, 255, 256, 300, 640]
+    B = len(lens)
+    kc = torch.randn(B + 1, Hkv, max_seq, D, device=gpu, dtype=torch.bfloat16)
     vc = torch.randn_like(kc)
-    slots = torch.tensor([2, 0, 3], dtype=torch.int32, device=gpu)
+    slots = torch.tensor([2, 0, 3, 7, 1, 6, 4], dtype=torch.int32, device=gpu)
     pos = torch.tensor(lens, dtype=torch.int32, device=gpu)
     cos, sin = ref.rope_tables(1024, D, 500000.0, None, gpu)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=gpu, dtype=torch.bfloat16)
     kc_ref, vc_ref = kc.clone(), vc.clone()
     q = native().rope_append(qkv, cos, sin, pos, slots, kc, vc, Hq, Hkv, D)
-    out = native().decode_attn(q, kc, vc, pos + 1, slots, max(lens) + 1, 1.0 / math.sqrt(D))
+    out = native().decode_attn(q, kc, vc, pos, slots, max(lens) + 1, 1.0 / math.sqrt(D), 1)
     x = qkv.float().view(B, Hq + 2 * Hkv, D)
     for i in range(B):
         p, s = lens[i], int(slots[i])
