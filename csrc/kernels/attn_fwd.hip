@@ -15,8 +15,13 @@
 //  * K/V tiles live in LDS as 16-B-chunk XOR-swizzled images
 //    (chunk ^ ((row&3)<<2 | (row>>2)&3)): conflict-free for both the
 //    ds_read_b128 row reads of K and the transposed reads of V;
-//  * register-staged double buffer with the async-STAGE split (T14): tile t+1's
-//    global loads issue before tile t's MFMAs, the LDS write lands after them;
+//  * K/V tiles double-buffered in LDS by LDS-DMA (tile t+1 issued before tile t's
+//    MFMAs); V^T read with inline-asm tr-reads so hipcc does not drain the
+//    in-flight DMA before them; tile loop unrolled by two so every LDS address
+//    is a per-lane base + immediate;
+//  * softmax: raw-score row max, scale folded into the exp2 argument (one FMA per
+//    element), cross-half max/sum by v_permlane32_swap, deferred O rescale
+//    (only when a row max grows by > 2^8: guide T13);
 //  * causal blocks scheduled heaviest-first, XCD-aware block remap so the
 //    q-heads sharing one KV head run on the same XCD (shared L2).
 #include "common.h"
@@ -104,10 +109,24 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   for (int d = 0; d < DB; ++d)
 #pragma unroll
     for (int j = 0; j < 16; ++j) o[d][j] = 0.f;
+  // m_i: the (deferred) running max of this row in the log2 domain of the scaled
+  // scores; l_i: running sum of exp2(s*sl - m_i)
   float m_i = -1e30f, l_i = 0.f;
 
-  // per-lane constants for the transposed V reads
+  // Loop-invariant LDS byte addresses.  The XOR swizzle of a row depends only on
+  // row & 15, so for every (n, s2) k-step and both ring buffers a fragment address
+  // is one per-lane base + a compile-time immediate (the tile loop is unrolled by
+  // two so the buffer index is static): no VALU address math in the loop.
   const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t va_base[DB][2];
+#pragma unroll
+  for (int db = 0; db < DB; ++db) {
+    const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+    const int rA = 4 * hh + tq, rB = 8 + 4 * hh + tq;
+    va_base[db][0] = lds0 + TILE + rA * ROWB + 16 * (chunk ^ swz<CH>(rA)) + 8 * (tp & 1);
+    va_base[db][1] = lds0 + TILE + rB * ROWB + 16 * (chunk ^ swz<CH>(rB)) + 8 * (tp & 1);
+  }
 
   if (ntiles > 0) glds(0, 0);
   // Retire the prologue's Q loads and tile-0 DMA with a wait the compiler's
@@ -116,11 +135,12 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   const int wq_hi = q0 + 32 * w + 31;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntiles) glds(kt + 1, (kt + 1) & 1);  // prefetch next tile into the other buffer
-    const char* kb = smem + cur * 2 * TILE;
-    const char* vb = kb + TILE;
+
+  // One 64-key tile out of ring buffer CUR (compile-time).
+  auto tile = [&](auto cur_c, int kt) {
+    constexpr int CUR = decltype(cur_c)::value;
+    if (kt + 1 < ntiles) glds(kt + 1, CUR ^ 1);  // prefetch next tile into the other buffer
+    const char* kb = smem + CUR * 2 * TILE;
     const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
     if (active) {
       f32x16 sacc[2];
@@ -135,6 +155,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           sacc[n] = mfma32(a, qf[s], sacc[n]);
         }
       }
+      // row max of the RAW scores (the scale is folded into the exp2 argument below)
       float mx = -INFINITY;
       const bool need_mask = (kt * BN + BN > Sk) || (CAUSAL && (kt * BN + BN - 1 > q0 + 32 * w + causal_off));
       if (need_mask) {  // wave-uniform: diagonal / tail tiles only; branch-free select per element
@@ -144,7 +165,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           for (int j = 0; j < 16; ++j) {
             const int key = kt * BN + n * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;
             const bool dead = (key >= Sk) | (CAUSAL & (key > qrow + causal_off));
-            const float x = dead ? -INFINITY : sacc[n][j] * sl;
+            const float x = dead ? -INFINITY : sacc[n][j];
             sacc[n][j] = x;
             mx = fmaxf(mx, x);
           }
@@ -152,28 +173,37 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 #pragma unroll
         for (int n = 0; n < 2; ++n)
 #pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const float x = sacc[n][j] * sl;
-            sacc[n][j] = x;
-            mx = fmaxf(mx, x);
-          }
+          for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sacc[n][j]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m_i, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_i - mnew);
+      {  // max with the other half-wave (same query column): one permlane32 swap
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      // Deferred rescale (guide T13): O and l are rescaled only when some row's
+      // tile max exceeds its running max by more than kThr (log2 units), so
+      // probabilities stay <= 2^kThr; the decision is wave-uniform and taken before
+      // this tile's P is formed, so everything at the old scale is rescaled once.
+      constexpr float kThr = 8.f;
+      const float mt = mx * sl;
+      if (__any(mt > m_i + kThr)) {
+        const float mnew = fmaxf(m_i, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m_i - mnew);
+        l_i *= alpha;
+        m_i = mnew;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) o[d] *= alpha;
+      }
+      const float nm = -m_i;
       float ls = 0.f;
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float p = __builtin_amdgcn_exp2f(sacc[n][j] - mnew);
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][j], sl, nm));
           sacc[n][j] = p;
           ls += p;
         }
-      l_i = l_i * alpha + ls;
-      m_i = mnew;
-#pragma unroll
-      for (int d = 0; d < DB; ++d) o[d] *= alpha;
+      l_i += ls;
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -181,22 +211,37 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           u16x8 pb;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[n][8 * s2 + j]);
-          const int keyb = n * 32 + 16 * s2 + 4 * hh;
-          const int rowA = keyb + tq, rowB = keyb + 8 + tq;
+          // V^T fragments by inline-asm transposed reads (a builtin tr-read makes hipcc
+          // drain the next tile's in-flight LDS-DMA here), consumed behind counted waits
+          u16x4 fv[DB][2];
 #pragma unroll
           for (int db = 0; db < DB; ++db) {
-            const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
-            const u16x4 va = tr_read(vb + rowA * ROWB + 16 * (chunk ^ swz<CH>(rowA)) + 8 * (tp & 1));
-            const u16x4 vc = tr_read(vb + rowB * ROWB + 16 * (chunk ^ swz<CH>(rowB)) + 8 * (tp & 1));
+            fv[db][0] = trd_off(va_base[db][0], CUR * 2 * TILE + (32 * n + 16 * s2) * ROWB);
+            fv[db][1] = trd_off(va_base[db][1], CUR * 2 * TILE + (32 * n + 16 * s2) * ROWB);
+          }
+#pragma unroll
+          for (int db = 0; db < DB; ++db) {
+            lds_wait_le(2 * (DB - 1 - db));
+            pin(fv[db][0]);
+            pin(fv[db][1]);
+            const u16x4 va = fv[db][0], vc = fv[db][1];
             const u16x8 a = u16x8{va[0], va[1], va[2], va[3], vc[0], vc[1], vc[2], vc[3]};
             o[db] = mfma32(a, pb, o[db]);
           }
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for tile kt+1 landed
-    __syncthreads();                     // ... and every other wave's; buffer cur free again
+    __syncthreads();                     // ... and every other wave's; buffer CUR free again
+  };
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < ntiles) tile(std::integral_constant<int, 1>{}, kt + 1);
   }
-  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
+  float l_tot;
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_i), __float_as_uint(l_i), false, false);
+    l_tot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qrow < S) {
     uint16_t* op = O + ((size_t)b * S + qrow) * (size_t)ldo + (size_t)h * D;

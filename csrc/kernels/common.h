@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace mx {
 
@@ -79,6 +80,49 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// ---- LDS-DMA-friendly transposed reads (used by the attention kernels) ----
+// ds_read_b64_tr_b16 as inline asm with an immediate offset: invisible to hipcc's
+// waitcnt pass, which otherwise drains every in-flight LDS-DMA (vmcnt(0)) before a
+// builtin tr-read (it cannot tell that the read misses the DMA's buffer).  The caller
+// waits with lds_wait() / lds_wait_le() and pins each result behind the wait with pin().
+// LDS operations of a wave complete in order, so counted lgkmcnt waits are exact for
+// the asm reads and conservative for anything the compiler interleaves.
+template <int OFF>
+__device__ __forceinline__ u16x4 trd_asm(uint32_t lds_addr) {
+  u16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(lds_addr), "i"(OFF));
+  return v;
+}
+// transposed read at base + off; `off` folds into the instruction's immediate when it
+// is a compile-time constant < 64 KiB
+__device__ __forceinline__ u16x4 trd_off(uint32_t base, int off) {
+  u16x4 v;
+  if (__builtin_constant_p(off) && off >= 0 && off < 65536)
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(off));
+  else
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(base + (uint32_t)off));
+  return v;
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// at most n LDS operations of this wave still outstanding (n folds to a constant after unrolling)
+__device__ __forceinline__ void lds_wait_le(int n) {
+  switch (n) {
+    case 14: asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); break;
+  }
+}
+__device__ __forceinline__ void pin(u16x4& v) { asm volatile("" : "+v"(v)); }
+// byte address of a __shared__ object in the LDS aperture
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(__attribute__((address_space(3))) const char*)p;
 }
 
 }  // namespace mx

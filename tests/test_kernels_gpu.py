@@ -180,6 +180,39 @@ def test_attention_fwd_bwd(gpu, B, Hq, Hkv, S, Sk, D, causal):
     assert rel_err(dv, vf.grad) < 3e-2
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_fwd_growing_max(gpu, causal):
+    """Exercise the forward's deferred-rescale branch (rescale only when a row's
+    tile max exceeds its running max by > 2^8): scores grow with the key index,
+    steeply for some rows (a rescale on nearly every 64-key tile, max jumps of
+    tens of log2 units) and gently for others (growth below the threshold, so
+    probabilities > 1 are carried), mixed inside every wave."""
+    torch.manual_seed(3)
+    B, Hq, Hkv, S, D = 1, 4, 1, 640, 128
+    keypos = torch.arange(S, device=gpu, dtype=torch.float32) / S
+    k = torch.randn(B, Hkv, S, D, device=gpu) * 0.3
+    k[..., 0] = keypos * 8.0  # a key feature that grows along the sequence
+    q = torch.randn(B, Hq, S, D, device=gpu) * 0.3
+    # per row: steep (~20 log2 units of max growth per tile: rescale every tile),
+    # medium (~4 per tile: deferred max lags by up to 8) and flat rows
+    slope = torch.tensor([200.0, 40.0, 3.0], device=gpu)[torch.arange(S, device=gpu) % 3]
+    q[..., 0] = slope
+    q, k = q.to(torch.bfloat16), k.to(torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, causal, scale)
+    qf, kf, vf = q.float(), k.float(), v.float()
+    orf = ref.attention(qf.transpose(1, 2), kf.transpose(1, 2), vf.transpose(1, 2), causal=causal)
+    assert rel_err(o.view(B, S, Hq, D), orf) < 2e-2
+    s = torch.matmul(qf, kf.repeat_interleave(Hq // Hkv, 1).transpose(-1, -2)) * scale
+    if causal:
+        i = torch.arange(S, device=gpu).view(S, 1)
+        j = torch.arange(S, device=gpu).view(1, S)
+        s = s.masked_fill(j > i, float("-inf"))
+    lse_ref = torch.logsumexp(s, -1) / math.log(2)
+    assert (lse - lse_ref).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("causal,S", [(True, 2048), (True, 200), (False, 333)])
 def test_attention_bwd_deterministic(gpu, causal, S):
     """Deterministic dQ modes (2: per-key-block partials + ordered reduction,
