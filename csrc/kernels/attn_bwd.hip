@@ -34,6 +34,7 @@ __device__ __forceinline__ f32x16 mfma32b(const u16x8& a, const u16x8& b, const 
 __device__ __forceinline__ u16x4 trd(const char* p) {
   return __builtin_bit_cast(u16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_b*)(p)));
 }
+// (trd_asm / lds_wait / pin: common.h)
 template <int CH>
 __device__ __forceinline__ int swzb(int row) {
   return (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
@@ -218,7 +219,6 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     }
   };
 
-  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
   if (nqt > 0) glds(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): prologue loads retired (visible to the waitcnt pass)
   __syncthreads();
@@ -269,12 +269,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           dp[j] = p * (dp[j] - dl[j >> 2][j & 3]);
         }
       }
-      // dV^T += dO^T P ; dK^T += Q^T dS   (k index = q rows of this m-subtile).
-      // dO^T / Q^T fragments by inline-asm transposed reads: a builtin tr-read makes
-      // hipcc drain the in-flight LDS-DMA prefetch of the next q tile (vmcnt(0)) in
-      // the middle of this one.  All 4*DB reads of an s2 step are issued at once and
-      // consumed behind counted lgkmcnt waits (LDS returns in order).
-      const uint32_t qt_l = lds0 + (uint32_t)(KIMG + buf * BUF), dot_l = qt_l + QT;
+      // dV^T += dO^T P ; dK^T += Q^T dS   (k index = q rows of this m-subtile)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         u16x8 pb, sb;
@@ -285,23 +280,14 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         }
         const int rb = 32 * m + 16 * s2 + 4 * hh;
         const int rowA = rb + tq, rowB = rb + 8 + tq;
-        u16x4 fa[DB][2], fb[DB][2];
 #pragma unroll
         for (int db = 0; db < DB; ++db) {
           const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
-          const uint32_t oA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
-          const uint32_t oB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
-          fa[db][0] = trd_asm<0>(dot_l + oA);
-          fa[db][1] = trd_asm<0>(dot_l + oB);
-          fb[db][0] = trd_asm<0>(qt_l + oA);
-          fb[db][1] = trd_asm<0>(qt_l + oB);
-        }
-#pragma unroll
-        for (int db = 0; db < DB; ++db) {
-          lds_wait_le(4 * (DB - 1 - db));
-          pin(fa[db][0]); pin(fa[db][1]); pin(fb[db][0]); pin(fb[db][1]);
-          const u16x4 a0 = fa[db][0], a1 = fa[db][1], b0 = fb[db][0], b1 = fb[db][1];
+          const int oA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
+          const int oB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
+          const u16x4 a0 = trd(dot + oA), a1 = trd(dot + oB);
           dv[db] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]}, pb, dv[db]);
+          const u16x4 b0 = trd(qt + oA), b1 = trd(qt + oB);
           dk[db] = mfma32b(u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, sb, dk[db]);
         }
       }
@@ -318,13 +304,12 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swzb<8>(krow)) + 8 * hh) = v4;
       }
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA of the next q tile landed
     if constexpr (DQM == 3) {
       ds_q0 = q0;
-      __syncthreads();  // this tile's Q/dO buffer consumed; every wave's next-tile DMA landed
+      __syncthreads();  // this tile's Q/dO buffer consumed; next tile's DMA landed
       continue;
     }
-    __syncthreads();  // dS image complete (the DMA + atomics issued above retired)
+    __syncthreads();  // dS image complete (also retires the DMA + atomics issued above)
     // dQ[q0 .. q0+63][:] = scale * dS[64 x 128] . K[128 x D]  -> kept in `pend`, added next iteration
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
