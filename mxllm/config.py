@@ -38,7 +38,11 @@ class RunConfig:
     engine_model: str = ""  # "" = tiny on CPU, llama3.1-8b on GPU
     max_new_tokens: int = 32
     temperature: float = 0.0
-    max_batch: int = 8
+    max_batch: int = 32
+    # inference driver: DataLoader batches kept in flight on the local engine (their
+    # prompts are generated together by continuous batching; results are still
+    # logged batch by batch, in order).  0 = one batch at a time, as the reference.
+    lookahead_batches: int = 8
     max_seq: int = 2048
     tokenizer: str = ""
     checkpoint: str = ""

@@ -103,6 +103,31 @@ def batch_local(model: str, prompts: list[str], max_tokens: int = 32, temperatur
     return [tok.decode([t for t in o if t not in eng.eos_ids]) for o in outs]
 
 
+def submit_local(model: str, prompts: list[str], max_tokens: int = 32, temperature: float = 0.0) -> list:
+    """Queue user prompts on the in-process engine WITHOUT waiting (the engine's
+    background loop batches them with everything else in flight); returns
+    request handles for ``collect_local``."""
+    from .engine import SamplingParams
+
+    eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+    eng.start()
+    ids = [tok.apply_chat_template([{"role": "user", "content": p}]) for p in prompts]
+    return [eng.submit(i, SamplingParams(max_new_tokens=max_tokens, temperature=temperature)) for i in ids]
+
+
+def collect_local(model: str, requests: list, timeout: float | None = None) -> list[str]:
+    """Wait for requests from ``submit_local`` and detokenize (raises on an engine error)."""
+    eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+    out = []
+    for r in requests:
+        if not r.done.wait(timeout):
+            raise CompletionError("local engine request timed out")
+        if r.error:
+            raise CompletionError(f"local engine: {r.error}")
+        out.append(tok.decode([t for t in r.output if t not in eng.eos_ids]))
+    return out
+
+
 def _http(model, messages, base, key, timeout, max_tokens, temperature, **kw) -> ModelResponse:
     import httpx
 

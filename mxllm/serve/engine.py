@@ -11,7 +11,9 @@ tokens = 43 GB beside the 141 GB of weights on one 288 GB MI355X.  Prefill
 runs the MFMA flash-attention kernel; decode runs the split-K decode kernel
 (one workgroup streams 256 cached keys of one (sequence, kv-head) and serves
 all q-heads of that GQA group).  Scheduling is continuous batching: new
-requests are prefilled between decode steps and join the running batch.
+requests are prefilled between decode steps (all prompts admitted together in
+one pass: concatenated tokens through the GEMMs, attention per sequence) and
+join the running batch.
 
 Decode is launch-bound at small batch (a 32-layer step is ~300 kernel
 launches), so on GPU each decode step is replayed from a hipGraph
@@ -66,8 +68,9 @@ class Request:
 
 class Engine:
     def __init__(self, model, max_batch: int = 8, max_seq: int = 4096, device=None, eos_ids=(),
-                 use_graphs: bool | None = None):
+                 use_graphs: bool | None = None, prefill_tokens: int = 16384):
         self.model = model
+        self.prefill_tokens = max(1, prefill_tokens)
         self.cfg = model.cfg
         self.device = device or model.tok_emb.device
         self.max_batch = max_batch
@@ -140,6 +143,34 @@ class Engine:
         xn = self._layers(x, attn)
         self.lens[slot] = S
         return torch.matmul(xn[-1:], m.head_weight.t()).float()[0]
+
+    @torch.no_grad()
+    def prefill_batch(self, slots: list[int], prompts: list[list[int]]) -> torch.Tensor:
+        """Prefill several prompts in ONE pass: their tokens are concatenated so
+        every GEMM / norm / SwiGLU runs once over all of them (each weight is
+        read once per batch instead of once per prompt); attention runs per
+        sequence into its own cache slot.  Returns last-position logits [n, V] f32."""
+        m, c = self.model, self.cfg
+        lens = [len(p) for p in prompts]
+        if any(S >= self.max_seq for S in lens):
+            raise ValueError(f"prompt exceeds max_seq {self.max_seq}")
+        t = torch.tensor([tok for p in prompts for tok in p], dtype=torch.long, device=self.device)
+        x = ops.embedding(t, m.tok_emb)
+        offs = [0]
+        for S in lens:
+            offs.append(offs[-1] + S)
+
+        def attn(i, qkv):
+            outs = [dops.prefill_attention(qkv[offs[j]:offs[j + 1]], m.rope_cos, m.rope_sin, self.k_cache[i],
+                                           self.v_cache[i], slots[j], lens[j], c.n_heads, c.n_kv_heads, c.head_dim)
+                    for j in range(len(prompts))]
+            return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+
+        xn = self._layers(x, attn)
+        for s_, S in zip(slots, lens):
+            self.lens[s_] = S
+        last = torch.tensor([o - 1 for o in offs[1:]], device=self.device)
+        return torch.matmul(xn.index_select(0, last), m.head_weight.t()).float()
 
     @torch.no_grad()
     def decode(self, slots: list[int], tokens: torch.Tensor) -> torch.Tensor:
@@ -273,20 +304,36 @@ class Engine:
                 r = self.waiting.pop(0)
                 r.slot = self.free_slots.pop(0)
                 admit.append(r)
+        # admitted prompts are prefilled together, in groups of at most
+        # prefill_tokens tokens (bounds the activation memory of one pass)
+        groups, cur, ntok = [], [], 0
         for r in admit:
+            if cur and ntok + len(r.prompt) > self.prefill_tokens:
+                groups.append(cur)
+                cur, ntok = [], 0
+            cur.append(r)
+            ntok += len(r.prompt)
+        if cur:
+            groups.append(cur)
+        for grp in groups:
             try:
                 t0 = time.perf_counter()
-                logits = self.prefill(r.slot, r.prompt)
-                self.active[r.slot] = r
-                tok = int(dops.sample(logits.view(1, -1), r.params.temperature, r.params.seed, 0,
-                                      r.params.top_p, r.params.top_k)[0])
+                logits = self.prefill_batch([r.slot for r in grp], [r.prompt for r in grp])
+                toks = []
+                for i, r in enumerate(grp):
+                    self.active[r.slot] = r
+                    toks.append(int(dops.sample(logits[i:i + 1], r.params.temperature, r.params.seed, 0,
+                                                r.params.top_p, r.params.top_k)[0]))
                 self.prefill_s += time.perf_counter() - t0
-                self.prefill_tokens += len(r.prompt)
-                self._accept(r, tok)
+                for r, tok in zip(grp, toks):
+                    self.prefill_tokens += len(r.prompt)
+                    self._accept(r, tok)
             except Exception as e:  # noqa: BLE001
                 log.exception("prefill failed")
-                r.error = str(e)
-                self._finish(r, "error")
+                for r in grp:
+                    self.active.pop(r.slot, None)
+                    r.error = str(e)
+                    self._finish(r, "error")
         if not self.active:
             return bool(admit)
         slots = sorted(self.active)

@@ -81,6 +81,29 @@ def get_model_responses(prompts):
     return [get_model_response(p) for p in prompts]
 
 
+def _local_engine():
+    return litellm.api_base in (None, "", "local", "inproc") and bool(litellm._LOCAL)
+
+
+def _submit(prompts):
+    try:
+        return litellm.submit_local(CONFIG['MODEL_NAME'], list(prompts), max_tokens=RUN.max_new_tokens,
+                                    temperature=RUN.temperature)
+    except Exception as e:
+        logging.error(f"Error getting model response: {e}")
+        return None
+
+
+def _collect(reqs, n):
+    if reqs is None:
+        return [FALLBACK] * n
+    try:
+        return litellm.collect_local(CONFIG['MODEL_NAME'], reqs, timeout=RUN.request_timeout * max(1, n))
+    except Exception as e:
+        logging.error(f"Error getting model response: {e}")
+        return [FALLBACK] * n
+
+
 def _configure_client(device):
     if os.environ.get("OPENAI_API_KEY"):
         litellm.api_key = os.environ["OPENAI_API_KEY"]
@@ -139,30 +162,45 @@ def main():
 
         records = []
         step = 0
+
+        def emit(epoch, prompts, labels, gpu_results, responses):
+            if rank == 0:
+                n = RUN.truncate
+                for prompt, response, label, gpu_result in zip(prompts, responses, labels, gpu_results):
+                    logging.info(f"Prompt: {prompt[:n]}...")
+                    logging.info(f"Response: {response[:n]}...")
+                    logging.info(f"Label: {label}")
+                    logging.info(f"GPU Result: {gpu_result}\n")
+            if RUN.gather_results:
+                n = RUN.truncate
+                records.extend({"rank": rank, "epoch": epoch, "prompt": p[:n], "response": r[:n],
+                                "label": int(lb), "gpu_result": float(g)}
+                               for p, r, lb, g in zip(prompts, responses, labels, gpu_results))
+
+        # lookahead_batches > 0: keep that many DataLoader batches in flight on the
+        # local engine (generated together by continuous batching), results still
+        # logged batch by batch in order; 0 = one batch at a time, as the reference
+        lookahead = RUN.lookahead_batches if _local_engine() else 0
         for epoch in range(RUN.epochs):
             logging.info(f"Starting epoch {epoch}")
             train_sampler.set_epoch(epoch)
+            pending = []  # (prompts, labels, gpu_results, engine requests), oldest first
             for batch in train_dataloader:
                 maybe_inject(RUN, rank, step)
                 prompts = batch["text"]
                 labels = batch["label"]
 
                 gpu_results = gpu_tensor_operations(prompts, device)
-                responses = get_model_responses(prompts)
-
-                if rank == 0:
-                    n = RUN.truncate
-                    for prompt, response, label, gpu_result in zip(prompts, responses, labels, gpu_results):
-                        logging.info(f"Prompt: {prompt[:n]}...")
-                        logging.info(f"Response: {response[:n]}...")
-                        logging.info(f"Label: {label}")
-                        logging.info(f"GPU Result: {gpu_result}\n")
-                if RUN.gather_results:
-                    n = RUN.truncate
-                    records.extend({"rank": rank, "epoch": epoch, "prompt": p[:n], "response": r[:n],
-                                    "label": int(lb), "gpu_result": float(g)}
-                                   for p, r, lb, g in zip(prompts, responses, labels, gpu_results))
+                if lookahead > 0:
+                    pending.append((prompts, labels, gpu_results, _submit(prompts)))
+                    while len(pending) > lookahead:
+                        p_, l_, g_, reqs = pending.pop(0)
+                        emit(epoch, p_, l_, g_, _collect(reqs, len(p_)))
+                else:
+                    emit(epoch, prompts, labels, gpu_results, get_model_responses(prompts))
                 step += 1
+            for p_, l_, g_, reqs in pending:  # drained before the next "Starting epoch" line
+                emit(epoch, p_, l_, g_, _collect(reqs, len(p_)))
         if RUN.gather_results:
             _gather_results(records, rank, world_size)
         if dist.is_initialized():

@@ -123,6 +123,26 @@ def test_inference_plumbing_two_ranks(tmp_path):
     assert sum(1 for x in recs if x["rank"] == 1) == 375
 
 
+def test_inference_lookahead_same_records(tmp_path):
+    """DataLoader batches kept in flight on the local engine (lookahead 8, the
+    default) produce exactly the records, in exactly the order, of the
+    reference's one-batch-at-a-time loop (lookahead 0)."""
+    import json
+
+    recs = {}
+    for la in (0, 8):
+        out = tmp_path / f"r{la}.jsonl"
+        r = subprocess.run([sys.executable, "src/distributed_inference.py"], cwd=ROOT,
+                           env=_env(MXLLM_MAX_NEW_TOKENS=3, MXLLM_MAX_SEQ=256, MXLLM_GATHER_RESULTS=1,
+                                    MXLLM_N_ROWS=40, MXLLM_EPOCHS=2, MXLLM_LOOKAHEAD_BATCHES=la,
+                                    MXLLM_RESULTS_FILE=str(out)), capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        log = r.stdout + r.stderr
+        assert log.count("Prompt: ") == 80 and "An error occurred" not in log
+        recs[la] = [json.loads(x) for x in out.read_text().splitlines()]
+    assert recs[0] == recs[8]
+
+
 def test_two_node_emulation_finetune():
     """BASELINE config 5 (CPU rehearsal): two torchrun agents = two 'nodes'."""
     port = _port()

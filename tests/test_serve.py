@@ -43,6 +43,17 @@ def test_continuous_batching_is_order_independent(tiny_engine):
     assert batched == single
 
 
+def test_batched_prefill_matches_single(tiny_engine):
+    """Prompts of different lengths prefilled together in one pass (and split
+    into several passes by the prefill token budget) generate exactly what
+    each prompt generates alone."""
+    prompts = [[7] * 3, list(range(20, 61)), [1, 2], list(range(100, 117))]
+    single = [tiny_engine.generate([p], max_new_tokens=4)[0] for p in prompts]
+    assert tiny_engine.generate(prompts, max_new_tokens=4) == single
+    eng = Engine(tiny_engine.model, max_batch=4, max_seq=256, prefill_tokens=20)
+    assert eng.generate(prompts, max_new_tokens=4) == single
+
+
 def test_engine_serving_stats(tiny_engine):
     before = tiny_engine.stats()["requests_finished"]
     tiny_engine.generate([[1, 2, 3], [4, 5]], max_new_tokens=4)
