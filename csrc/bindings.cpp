@@ -205,9 +205,10 @@ at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu, int64_t out_pa
 }
 
 // ---------------------------------------------------------------- AdamW
-void adamw_step(at::Tensor master, const at::Tensor& grad, at::Tensor m, at::Tensor v,
+void adamw_step(at::Tensor master, at::Tensor grad, at::Tensor m, at::Tensor v,
                 const c10::optional<at::Tensor>& lowp, double lr, double b1, double b2, double eps, double wd,
-                double bc1, double bc2, const c10::optional<at::Tensor>& scale_t, double scale_f) {
+                double bc1, double bc2, const c10::optional<at::Tensor>& scale_t, double scale_f,
+                bool zero_grad) {
   check_f32(master, "master");
   check_f32(m, "m");
   check_f32(v, "v");
@@ -229,7 +230,7 @@ void adamw_step(at::Tensor master, const at::Tensor& grad, at::Tensor m, at::Ten
   }
   MX_OK(mx_adamw(master.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kBFloat16 ? 1 : 0,
                  m.data_ptr<float>(), v.data_ptr<float>(), lp, n, (float)lr, (float)b1, (float)b2, (float)eps,
-                 (float)wd, (float)bc1, (float)bc2, st, (float)scale_f, cur_stream()));
+                 (float)wd, (float)bc1, (float)bc2, st, (float)scale_f, zero_grad ? 1 : 0, cur_stream()));
 }
 
 // ---------------------------------------------------------------- embedding
@@ -460,7 +461,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
-  m.def("adamw_step(Tensor(a!) master, Tensor grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f) -> ()");
+  m.def("adamw_step(Tensor(a!) master, Tensor(e!) grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f, bool zero_grad=False) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor w) -> Tensor");
   m.def("embedding_bwd(Tensor dy, Tensor ids, int V) -> Tensor");
   m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");

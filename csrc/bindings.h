@@ -25,9 +25,9 @@ extern "C" {
 int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream);
 int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
                   hipStream_t stream);
-int mx_adamw(float* p, const void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
+int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
              float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t, float scale_f,
-             hipStream_t stream);
+             int zero_grad, hipStream_t stream);
 int mx_embedding_fwd(const int64_t* ids, const uint16_t* w, uint16_t* out, int64_t T, int H, int64_t V,
                      hipStream_t stream);
 int mx_embedding_bwd(const int64_t* ids, const uint16_t* dy, float* dw, int64_t T, int H, int64_t V,

@@ -56,9 +56,11 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
   }
 }
 
-// Fused AdamW, 4 elements per lane per iteration (n % 4 == 0).
-template <bool GRAD_BF16, bool LOWP>
-__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const void* __restrict__ gv,
+// Fused AdamW, 4 elements per lane per iteration (n % 4 == 0).  ZERO: the gradient
+// is cleared in the same pass (the next backward accumulates into it with beta=1),
+// so no separate memset re-streams the gradient buffer.
+template <bool GRAD_BF16, bool LOWP, bool ZERO>
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, void* __restrict__ gv,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     uint16_t* __restrict__ lowp, int64_t n, float lr, float b1,
                                                     float b2, float eps, float wd, float inv_bc1, float inv_bc2,
@@ -71,8 +73,10 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     if constexpr (GRAD_BF16) {
       u16x4 gb = *reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(gv) + i);
       g = f32x4{bf2f(gb[0]), bf2f(gb[1]), bf2f(gb[2]), bf2f(gb[3])};
+      if constexpr (ZERO) *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(gv) + i) = u16x4{0, 0, 0, 0};
     } else {
       g = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(gv) + i);
+      if constexpr (ZERO) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(gv) + i) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     f32x4 pp = *reinterpret_cast<f32x4*>(p + i);
     f32x4 mm = *reinterpret_cast<f32x4*>(m + i);
@@ -146,20 +150,23 @@ extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* d
   return (int)hipGetLastError();
 }
 
-extern "C" int mx_adamw(float* p, const void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n,
-                        float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
-                        const float* scale_t, float scale_f, hipStream_t stream) {
+extern "C" int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
+                        float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t,
+                        float scale_f, int zero_grad, hipStream_t stream) {
   if (n % 4) return -1;
   const int grid = grid_for(n / 4);
   const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
-#define ADAM_LAUNCH(GB, LP)                                                                          \
-  adamw_kernel<GB, LP><<<grid, 256, 0, stream>>>(p, g, m, v, lowp, n, lr, b1, b2, eps, wd, ib1, ib2, \
-                                                 scale_t, scale_f)
+#define ADAM_LAUNCH(GB, LP, Z)                                                                          \
+  adamw_kernel<GB, LP, Z><<<grid, 256, 0, stream>>>(p, g, m, v, lowp, n, lr, b1, b2, eps, wd, ib1, ib2, \
+                                                    scale_t, scale_f)
+#define ADAM_Z(GB, LP) \
+  do { if (zero_grad) ADAM_LAUNCH(GB, LP, true); else ADAM_LAUNCH(GB, LP, false); } while (0)
   if (grad_bf16) {
-    if (lowp) ADAM_LAUNCH(true, true); else ADAM_LAUNCH(true, false);
+    if (lowp) ADAM_Z(true, true); else ADAM_Z(true, false);
   } else {
-    if (lowp) ADAM_LAUNCH(false, true); else ADAM_LAUNCH(false, false);
+    if (lowp) ADAM_Z(false, true); else ADAM_Z(false, false);
   }
+#undef ADAM_Z
 #undef ADAM_LAUNCH
   return (int)hipGetLastError();
 }

@@ -16,11 +16,12 @@ from ._ext import native, use_native
 
 def adamw_step_(master: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                 lowp: torch.Tensor | None, *, lr: float, beta1: float, beta2: float, eps: float,
-                weight_decay: float, step: int, grad_scale=1.0) -> None:
+                weight_decay: float, step: int, grad_scale=1.0, zero_grad: bool = False) -> None:
     """In-place AdamW on flat 1-D tensors (``grad`` fp32 or bf16).
 
     ``grad_scale`` is a float or a 1-element f32 device tensor (e.g. the
-    grad-clip coefficient x 1/world computed on device: no host sync)."""
+    grad-clip coefficient x 1/world computed on device: no host sync).
+    ``zero_grad``: clear ``grad`` in the same pass (GPU: fused into the kernel)."""
     if use_native(master):
         bc1 = 1.0 - beta1 ** step
         bc2 = 1.0 - beta2 ** step
@@ -28,10 +29,13 @@ def adamw_step_(master: torch.Tensor, grad: torch.Tensor, m: torch.Tensor, v: to
             st, sf = grad_scale.reshape(1).float().contiguous(), 1.0
         else:
             st, sf = None, float(grad_scale)
-        native().adamw_step(master, grad, m, v, lowp, lr, beta1, beta2, eps, weight_decay, bc1, bc2, st, sf)
+        native().adamw_step(master, grad, m, v, lowp, lr, beta1, beta2, eps, weight_decay, bc1, bc2, st, sf,
+                            bool(zero_grad))
         return
     ref.adamw_(master, grad, m, v, lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
                step=step, grad_scale=grad_scale, p_lowp=lowp)
+    if zero_grad:
+        grad.zero_()
 
 
 def sq_norm(x: torch.Tensor) -> torch.Tensor:

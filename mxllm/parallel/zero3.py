@@ -375,8 +375,7 @@ class Zero3Trainer:
             gscale = scale
         ops.adamw_step_(self.master, self.grads, self.m, self.v, self.shard_params, lr=o.lr_at(self.step_num),
                         beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay, step=self.step_num,
-                        grad_scale=gscale)
-        self.grads.zero_()
+                        grad_scale=gscale, zero_grad=True)  # shard grads cleared in the same pass
         self._refresh_resident()
         return total / n
 

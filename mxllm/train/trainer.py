@@ -101,9 +101,9 @@ class Trainer:
             gscale = scale
         ops.adamw_step_(self.flat.master, self.flat.grads, self.m, self.v, self.lowp, lr=o.lr_at(self.step_num),
                         beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
-                        step=self.step_num, grad_scale=gscale)
+                        step=self.step_num, grad_scale=gscale, zero_grad=True)  # grads cleared in the same pass
         self._sync_adapters()
-        self.flat.zero_grad()
+        self.flat.attach_grads()
 
     def _sync_adapters(self):
         """LoRA adapters -> their copies in the augmented GEMM weight buffers."""

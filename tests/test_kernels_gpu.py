@@ -96,9 +96,18 @@ def test_adamw(gpu, gdt):
     ref.adamw_(pr, g, mr, vr, grad_scale=0.5, **kw)
     from mxllm.ops import adamw_step_
 
+    g0 = g.clone()
     adamw_step_(p, g, m, v, lowp, grad_scale=torch.tensor([0.5], device=gpu), **kw)
     assert rel_err(p, pr) < 1e-6 and rel_err(m, mr) < 1e-6 and rel_err(v, vr) < 1e-6
     assert torch.equal(lowp, p.to(torch.bfloat16))
+    assert torch.equal(g, g0)  # untouched without zero_grad
+    # fused gradient clearing: same update, gradient zeroed in the same pass
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    p3, m3, v3 = p.clone(), m.clone(), v.clone()
+    adamw_step_(p2, g, m2, v2, None, grad_scale=0.5, **kw)
+    adamw_step_(p3, g, m3, v3, None, grad_scale=0.5, zero_grad=True, **kw)
+    assert torch.equal(p2, p3) and torch.equal(m2, m3) and torch.equal(v2, v3)
+    assert g.abs().max().item() == 0.0
 
 
 def test_embedding(gpu):
