@@ -35,6 +35,15 @@ __device__ __forceinline__ u16x4 trd(const char* p) {
   return __builtin_bit_cast(u16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_b*)(p)));
 }
 // (trd_asm / lds_wait / pin: common.h)
+// 16-B chunk swizzle of the 128-B rows of a dS^T image ([key][64 q] bf16).  A
+// half-wave's transposed read touches rows 4a..4a+3, four chunks each: row parity
+// already splits the 64 banks, and bit 2 of the XOR (from row bit 1) moves rows
+// 4a+2/4a+3 to the other half of the chunks -> conflict-free (swzb<8> left rows
+// 4a and 4a+2 on the same banks: 2-way conflicts, a third of the dQ kernel's
+// LDS cycles in SQ_LDS_BANK_CONFLICT).  Depends on row bits 1..3 only, so a
+// 16-row step stays an immediate offset.
+__device__ __forceinline__ int swz8b(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+
 template <int CH>
 __device__ __forceinline__ int swzb(int row) {
   return (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
@@ -301,7 +310,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         if constexpr (DQM == 3)
           dsv[m][gq] = v4;
         else
-          *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swzb<8>(krow)) + 8 * hh) = v4;
+          *reinterpret_cast<u16x4*>(dsi + krow * DSROWB + 16 * (chunk ^ swz8b(krow)) + 8 * hh) = v4;
       }
     }
     if constexpr (DQM == 3) {
@@ -324,8 +333,8 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           const int kbse = 16 * s + 4 * hh;
           const int rA = kbse + tq, rB = kbse + 8 + tq;
           const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
-          const u16x4 a0 = trd(dsi + rA * DSROWB + 16 * (qchunk ^ swzb<8>(rA)) + 8 * (tp & 1));
-          const u16x4 a1 = trd(dsi + rB * DSROWB + 16 * (qchunk ^ swzb<8>(rB)) + 8 * (tp & 1));
+          const u16x4 a0 = trd(dsi + rA * DSROWB + 16 * (qchunk ^ swz8b(rA)) + 8 * (tp & 1));
+          const u16x4 a1 = trd(dsi + rB * DSROWB + 16 * (qchunk ^ swz8b(rB)) + 8 * (tp & 1));
           const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
           const u16x4 b0 = trd(kimg + rA * ROWB + 16 * (dchunk ^ swzb<CH>(rA)) + 8 * (tp & 1));
           const u16x4 b1 = trd(kimg + rB * ROWB + 16 * (dchunk ^ swzb<CH>(rB)) + 8 * (tp & 1));
@@ -453,7 +462,7 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
         const int jt = sg / DSEG, sgl = sg % DSEG;
         const int byte = sgl * 1024 + lane * 16;
         const int row = byte / DSROWB, slot = (byte % DSROWB) / 16;
-        const int ch = slot ^ swzb<8>(row);
+        const int ch = slot ^ swz8b(row);
         const int qt64 = q0 / BQ + jt;  // 64-q tile index; clamp a tail tile past S_pad
         const int qtc = min(qt64, S_pad / BQ - 1);
         __builtin_amdgcn_global_load_lds((gptr_t)(dsp + ((size_t)qtc * Sk_pad + kb0 + row) * BQ + ch * 8),
@@ -479,8 +488,8 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
     const int rA0 = 4 * hh + tq, rB0 = rA0 + 8;
     const int qchunk = (32 * m + 16 * (g & 1) + 4 * tp) >> 3;
     const int dchunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
-    aA[t] = KT + sub * DT + rA0 * DSROWB + 16 * (qchunk ^ swzb<8>(rA0)) + 8 * (tp & 1);
-    aB[t] = KT + sub * DT + rB0 * DSROWB + 16 * (qchunk ^ swzb<8>(rB0)) + 8 * (tp & 1);
+    aA[t] = KT + sub * DT + rA0 * DSROWB + 16 * (qchunk ^ swz8b(rA0)) + 8 * (tp & 1);
+    aB[t] = KT + sub * DT + rB0 * DSROWB + 16 * (qchunk ^ swz8b(rB0)) + 8 * (tp & 1);
     bA[t] = rA0 * ROWB + 16 * (dchunk ^ swzb<CH>(rA0)) + 8 * (tp & 1);
     bB[t] = rB0 * ROWB + 16 * (dchunk ^ swzb<CH>(rB0)) + 8 * (tp & 1);
   }
