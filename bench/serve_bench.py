@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--requests", type=int, default=64)
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--e2e-prompt-len", type=int, default=256)
+    ap.add_argument("--fp8", action="store_true", help="e4m3 projection weights (serving quantisation)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
 
@@ -50,9 +51,14 @@ def main():
     t0 = time.perf_counter()
     model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     model.requires_grad_(False)
+    if a.fp8:
+        from mxllm.serve.quant import quantize_model_fp8_
+
+        quantize_model_fp8_(model)
     torch.cuda.synchronize()
     init_s = time.perf_counter() - t0
-    wbytes = sum(p.numel() for p in model.parameters()) * 2
+    wbytes = sum(p.numel() * p.element_size() for p in model.parameters()) + \
+        sum(b.numel() * b.element_size() for n, b in model.named_buffers() if n.endswith((".q", ".scale")))
     bmax = max(int(b) for b in a.batches.split(","))
     max_seq = max(a.prompt_len, a.ctx + a.decode_steps, a.e2e_prompt_len + a.new_tokens) + 8
     eng = Engine(model, max_batch=max(bmax, 1), max_seq=max_seq)
@@ -72,7 +78,8 @@ def main():
         times.append(time.perf_counter() - t)
     del nxt
     pre_s = min(times)
-    out = {"model": a.model, "weights_gb": round(wbytes / 1e9, 1), "init_s": round(init_s, 1),
+    out = {"model": a.model, "weights": "fp8-e4m3 projections" if a.fp8 else "bf16",
+           "weights_gb": round(wbytes / 1e9, 1), "init_s": round(init_s, 1),
            "prefill": {"prompt_len": a.prompt_len, "ttft_ms": round(1e3 * pre_s, 2),
                        "tokens_per_s": round(a.prompt_len / pre_s, 1)},
            "decode": []}

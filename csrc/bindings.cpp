@@ -453,6 +453,51 @@ at::Tensor sample(const at::Tensor& logits, double temperature, int64_t seed, in
 
 }  // namespace
 
+
+// ---------------------------------------------------------------- fp8 weights (serving)
+// y[M, N] = x[M, K] . (scale[:, None] * q[N, K])^T ; q: e4m3 codes (uint8), scale f32 [N].
+// M <= 32: the fused weight-streaming kernel; otherwise dequantise to bf16 and run the
+// hipBLASLt GEMM (mxllm/serve/quant.py routes large calls to the fp8 x fp8 GEMM instead).
+at::Tensor w8_linear(const at::Tensor& x, const at::Tensor& q, const at::Tensor& scale) {
+  MX_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "x: bf16 [M, K] rows");
+  MX_CHECK(q.is_cuda() && q.scalar_type() == at::kByte && q.dim() == 2 && q.is_contiguous(), "q: uint8 [N, K]");
+  check_f32(scale, "scale");
+  const int64_t M = x.size(0), K = x.size(1), N = q.size(0);
+  MX_CHECK(q.size(1) == K && scale.numel() == N, "w8_linear shapes");
+  DevGuard g(x.device());
+  if (M <= 32 && N % 16 == 0 && K % 512 == 0 && x.stride(0) % 8 == 0) {
+    auto y = at::empty({M, N}, x.options());
+    MX_OK(mx_w8a16_gemm(bf(x), x.stride(0), q.data_ptr<uint8_t>(), scale.data_ptr<float>(), bfm(y), N, (int)M,
+                        (int)N, (int)K, cur_stream()));
+    return y;
+  }
+  auto w = at::empty({N, K}, x.options());
+  MX_OK(mx_w8_dequant(q.data_ptr<uint8_t>(), scale.data_ptr<float>(), bfm(w), N, (int)K, cur_stream()));
+  return at::mm(x, w.t());
+}
+
+// per-token e4m3 quantisation of bf16 rows: (codes uint8 [M, K], scale f32 [M, 1])
+std::tuple<at::Tensor, at::Tensor> quant_rows_e4m3(const at::Tensor& x) {
+  MX_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "x: bf16 [M, K] rows");
+  DevGuard g(x.device());
+  const int64_t M = x.size(0), K = x.size(1);
+  auto q = at::empty({M, K}, x.options().dtype(at::kByte));
+  auto s = at::empty({M, 1}, x.options().dtype(at::kFloat));
+  MX_OK(mx_quant_rows_e4m3(bf(x), x.stride(0), q.data_ptr<uint8_t>(), s.data_ptr<float>(), M, (int)K,
+                           cur_stream()));
+  return {q, s};
+}
+
+at::Tensor w8_dequant(const at::Tensor& q, const at::Tensor& scale) {
+  MX_CHECK(q.is_cuda() && q.scalar_type() == at::kByte && q.dim() == 2 && q.is_contiguous(), "q: uint8 [N, K]");
+  check_f32(scale, "scale");
+  DevGuard g(q.device());
+  auto w = at::empty({q.size(0), q.size(1)}, q.options().dtype(at::kBFloat16));
+  MX_OK(mx_w8_dequant(q.data_ptr<uint8_t>(), scale.data_ptr<float>(), bfm(w), q.size(0), (int)q.size(1),
+                      cur_stream()));
+  return w;
+}
+
 TORCH_LIBRARY(mxllm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? res, Tensor w, float eps, int out_pad=0) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw, int out_pad=0) -> (Tensor, Tensor)");
@@ -471,6 +516,9 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D) -> Tensor");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
+  m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
+  m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
+  m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3) -> (Tensor, Tensor, Tensor)");
 }
@@ -495,4 +543,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rope_append", &rope_append);
   m.impl("decode_attn", &decode_attn);
   m.impl("sample", &sample);
+  m.impl("w8_linear", &w8_linear);
+  m.impl("w8_dequant", &w8_dequant);
+  m.impl("quant_rows_e4m3", &quant_rows_e4m3);
 }

@@ -60,3 +60,11 @@ int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, co
 int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature, uint32_t seed,
               uint32_t step, hipStream_t stream);
 }
+
+extern "C" {
+// fp8_gemm.hip
+int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, const float* scale, uint16_t* y, int64_t ldy,
+                  int M, int N, int K, hipStream_t stream);
+int mx_w8_dequant(const uint8_t* q, const float* scale, uint16_t* w, int64_t N, int K, hipStream_t stream);
+int mx_quant_rows_e4m3(const uint16_t* x, int64_t ldx, uint8_t* q, float* s, int64_t M, int K, hipStream_t stream);
+}

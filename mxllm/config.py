@@ -35,7 +35,8 @@ class RunConfig:
     backend: str = ""  # "" = auto: nccl (RCCL) with GPUs, gloo on CPU
     seed: int = 0
     # local inference engine
-    engine_model: str = ""  # "" = tiny on CPU, llama3.1-8b on GPU
+    engine_model: str = ""  # "" = preset from MODEL_NAME on GPU (tiny stub on CPU)
+    engine_weights: str = "bf16"  # bf16 | fp8 (e4m3 projection weights for serving, mxllm/serve/quant.py)
     max_new_tokens: int = 32
     temperature: float = 0.0
     max_batch: int = 32

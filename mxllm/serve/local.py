@@ -26,7 +26,7 @@ def preset_for(model_name: str, device: torch.device) -> str:
 
 
 def ensure_local_engine(model_name: str, device, engine_model: str = "", max_batch: int = 8, max_seq: int = 2048,
-                        tokenizer_path: str = "", checkpoint: str = "", seed: int = 0):
+                        tokenizer_path: str = "", checkpoint: str = "", seed: int = 0, weights: str = "bf16"):
     from ..data.tokenizer import get_tokenizer
     from ..models import Llama, get_config
 
@@ -42,6 +42,10 @@ def ensure_local_engine(model_name: str, device, engine_model: str = "", max_bat
 
         load_model_weights(model, checkpoint)
     model.eval()
+    if weights == "fp8":
+        from .quant import quantize_model_fp8_
+
+        quantize_model_fp8_(model)
     tok = get_tokenizer(cfg.vocab_size, tokenizer_path or None, cfg.bos_id, cfg.eos_id)
     if cfg.vocab_size > 512 and not tokenizer_path:
         max_seq = max_seq

@@ -170,7 +170,8 @@ def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = 
 
 
 def build_default(model: str = "tiny", device: str | None = None, max_batch: int = 8, max_seq: int = 2048,
-                  checkpoint: str | None = None, tokenizer_path: str | None = None, seed: int = 0):
+                  checkpoint: str | None = None, tokenizer_path: str | None = None, seed: int = 0,
+                  weights: str = "bf16"):
     from ..data.tokenizer import get_tokenizer
     from ..models import Llama, get_config
 
@@ -183,6 +184,10 @@ def build_default(model: str = "tiny", device: str | None = None, max_batch: int
 
         load_model_weights(m, checkpoint)
     m.eval()
+    if weights == "fp8":
+        from .quant import quantize_model_fp8_
+
+        quantize_model_fp8_(m)
     tok = get_tokenizer(cfg.vocab_size, tokenizer_path, cfg.bos_id, cfg.eos_id)
     eng = Engine(m, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id, getattr(tok, "eos_id", cfg.eos_id)))
     return eng, tok
@@ -199,9 +204,11 @@ def main(argv=None):
     ap.add_argument("--tokenizer", default=None)
     ap.add_argument("--api-key", default=os.environ.get("MXLLM_API_KEY"))
     ap.add_argument("--served-name", default=None)
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default=os.environ.get("MXLLM_ENGINE_WEIGHTS", "bf16"),
+                    help="fp8: e4m3 projection weights (serving quantisation, mxllm/serve/quant.py)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
-    eng, tok = build_default(a.model, None, a.max_batch, a.max_seq, a.checkpoint, a.tokenizer)
+    eng, tok = build_default(a.model, None, a.max_batch, a.max_seq, a.checkpoint, a.tokenizer, weights=a.weights)
     app = build_app(eng, tok, a.served_name or a.model, a.api_key)
     import uvicorn
 

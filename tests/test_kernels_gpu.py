@@ -287,3 +287,36 @@ def test_sq_norm_deterministic(gpu, dtype, n):
     assert torch.equal(a, b)
     ref = x.double().pow(2).sum().item()
     assert abs(a.item() - ref) / ref < 1e-5
+
+
+@pytest.mark.parametrize("M,K", [(1, 1024), (5, 1024), (16, 1536), (17, 1024), (32, 2048), (33, 1024),
+                                 (64, 1024), (100, 1024), (5, 768)])
+def test_w8_linear(gpu, M, K):
+    """FP8-weight GEMM (decode kernel for M <= 32 and K % 512 == 0, dequantise +
+    hipBLASLt otherwise) vs an fp32 matmul with the reference-decoded weights."""
+    from mxllm.serve.quant import dequantize_e4m3, quantize_e4m3
+
+    torch.manual_seed(11)
+    N = 96
+    w = torch.randn(N, K, device=gpu) * 0.02
+    q, s = quantize_e4m3(w)
+    x = torch.randn(M, K + 64, device=gpu, dtype=torch.bfloat16)[:, :K]  # strided rows (padded producer buffers)
+    y = _ops().w8_linear(x, q, s)
+    yr = x.float() @ dequantize_e4m3(q, s).t()
+    assert y.shape == (M, N) and rel_err(y, yr) < 1e-2
+    assert rel_err(_ops().w8_dequant(q, s), dequantize_e4m3(q, s)) < 5e-3
+
+
+def test_quant_rows_e4m3(gpu):
+    """Per-token activation quantisation kernel == torch's e4m3fn conversion of
+    x / (amax / 448), and its decode reproduces x to e4m3 precision."""
+    torch.manual_seed(12)
+    x = (torch.randn(37, 1024 + 64, device=gpu) * 3).to(torch.bfloat16)[:, :1024]
+    q, s = _ops().quant_rows_e4m3(x)
+    xf = x.float()
+    s_ref = xf.abs().amax(1, keepdim=True) / 448.0
+    assert torch.allclose(s, s_ref, rtol=1e-6)
+    ref = (xf / s).to(torch.float8_e4m3fn)
+    mism = (q.view(torch.float8_e4m3fn).float() != ref.float()).float().mean().item()
+    assert mism < 1e-3, mism  # RNE on both sides; only 1/s rounding can flip a tie
+    assert rel_err(q.view(torch.float8_e4m3fn).float() * s, xf) < 0.04

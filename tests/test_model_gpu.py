@@ -267,3 +267,31 @@ def test_lora_producers_pad_in_place(gpu, monkeypatch):
     m(ids, ids).backward()
     n_lin = 4 * len(m.layers)
     assert calls == {"padded": 2 * n_lin, "copied": 0}, calls
+
+
+def test_engine_fp8_weights_close_to_bf16(gpu):
+    """Serving with e4m3 projection weights: prefill logits stay close to the
+    bf16 engine's, and graphed decode runs through the fp8 decode GEMM."""
+    from mxllm.models import Llama, get_config
+    from mxllm.serve.engine import Engine
+    from mxllm.serve.quant import W8Linear, quantize_model_fp8_
+
+    cfg = get_config("tiny-d128")
+    prompt = list(range(3, 60))
+    ref = Engine(Llama(cfg, device=gpu, seed=9).eval(), max_batch=2, max_seq=256)
+    l_ref = ref.prefill(0, prompt)
+    m8 = Llama(cfg, device=gpu, seed=9).eval()
+    assert quantize_model_fp8_(m8) > 0 and isinstance(m8.layers[0].wgu, W8Linear)
+    eng = Engine(m8, max_batch=2, max_seq=256)
+    l8 = eng.prefill(0, prompt)
+    cos = torch.nn.functional.cosine_similarity(l8.float(), l_ref.float(), dim=0).item()
+    assert cos > 0.99, cos
+    out = eng.generate([prompt, [1, 2, 3]], max_new_tokens=8)
+    assert all(len(o) == 8 for o in out)
+    # the fp8 x fp8 path (> SMALL_M tokens per call) against the bf16 reference layer
+    from mxllm.serve.quant import dequantize_e4m3
+
+    lin = m8.layers[0].wgu
+    x = torch.randn(40, lin.in_features, device=gpu, dtype=torch.bfloat16)
+    yr = x.float() @ dequantize_e4m3(lin.q, lin.scale).t()
+    assert _rel(lin(x), yr) < 3e-2

@@ -126,3 +126,23 @@ def test_lora_augmented_gemm_matches_two_gemm_form():
         torch.testing.assert_close(g, w, rtol=1e-5, atol=1e-5)
     # off-diagonal blocks of B get exactly zero gradient
     assert float(lin.lora_b.grad[:40, 4:].abs().max()) == 0.0
+
+
+def test_fp8_weight_quantization_roundtrip():
+    """Serving-time e4m3 weight quantisation (mxllm/serve/quant.py): per-channel
+    scales, no zero / subnormal codes (the HIP decoder relies on it), the
+    reference decoder agrees with torch's float8_e4m3fn, and the round-trip
+    error is what 3 mantissa bits give."""
+    from mxllm.serve.quant import dequantize_e4m3, quantize_e4m3
+
+    torch.manual_seed(0)
+    w = torch.randn(96, 512) * 0.02
+    w[3, :5] = 0.0  # exact zeros -> smallest normal code
+    q, s = quantize_e4m3(w)
+    assert q.dtype == torch.uint8 and s.shape == (96,)
+    assert int(((q & 0x78) == 0).sum()) == 0
+    ref = q.view(torch.float8_e4m3fn).float() * s[:, None]
+    assert torch.equal(dequantize_e4m3(q, s), ref)
+    err = (dequantize_e4m3(q, s) - w).norm() / w.norm()
+    assert err < 0.04, err
+    assert (dequantize_e4m3(q, s)[3, :5].abs() <= s[3] * 2 ** -6 + 1e-12).all()

@@ -155,3 +155,20 @@ def test_local_inproc_route(tiny_engine):
         assert isinstance(r.choices[0].message.content, str)
     finally:
         client.unregister_local("tiny-local")
+
+
+def test_fp8_weight_engine_cpu():
+    """Serving with e4m3 projection weights (CPU reference path): the model keeps
+    generating and its prefill logits stay close to the bf16 model's."""
+    from mxllm.serve.quant import W8Linear, quantize_model_fp8_
+
+    cfg = get_config("tiny")
+    prompt = [5, 9, 77, 1, 300, 12, 44]
+    ref = Engine(Llama(cfg, seed=4).eval(), max_batch=2, max_seq=128)
+    m8 = Llama(cfg, seed=4).eval()
+    quantize_model_fp8_(m8)
+    assert isinstance(m8.layers[0].wqkv, W8Linear)
+    eng = Engine(m8, max_batch=2, max_seq=128)
+    cos = torch.nn.functional.cosine_similarity(eng.prefill(0, prompt), ref.prefill(0, prompt), dim=0).item()
+    assert cos > 0.99, cos
+    assert len(eng.generate([prompt], max_new_tokens=5)[0]) == 5
