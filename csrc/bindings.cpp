@@ -10,6 +10,8 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 #include "bindings.h"
+#include <algorithm>
+#include <vector>
 
 namespace {
 
@@ -137,10 +139,10 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
 }
 
 // ---------------------------------------------------------------- misc
-// desc: int64 [n, 7] on the device (see misc.hip); total_blocks = sum of per-descriptor blocks
+// desc: int64 [n, 9] on the device (see misc.hip); total_blocks = sum of per-descriptor blocks
 void copy2d_batched(const at::Tensor& desc, int64_t total_blocks) {
-  MX_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 7 &&
-               desc.is_contiguous(), "desc must be int64 [n, 7] on the GPU");
+  MX_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 9 &&
+               desc.is_contiguous(), "desc must be int64 [n, 9] on the GPU");
   DevGuard g(desc.device());
   MX_OK(mx_copy2d_batched(desc.data_ptr<int64_t>(), (int)desc.size(0), total_blocks, cur_stream()));
 }
@@ -498,6 +500,64 @@ at::Tensor w8_dequant(const at::Tensor& q, const at::Tensor& scale) {
   return w;
 }
 
+// ---------------------------------------------------------------- LoRA rank-r GEMMs
+// out[:, 0:Vrows] = alpha * x . v^T (x [M, K], v [Vrows, K] row views, Vrows % 64 == 0):
+// the forward s x A^T / backward s dy B products written into the augmented-GEMM tails.
+void lora_xwt(const at::Tensor& x, const at::Tensor& v, at::Tensor& out, double alpha) {
+  const int64_t ldx = check_rows_bf16(x, "x"), ldv = check_rows_bf16(v, "v"), ldo = check_rows_bf16(out, "out");
+  const int64_t M = x.size(0), K = x.size(1), Vr = v.size(0);
+  MX_CHECK(v.size(1) == K && out.size(0) == M && out.size(1) >= Vr, "lora_xwt shapes");
+  MX_CHECK(M % 64 == 0 && K % 64 == 0 && Vr % 64 == 0 && ldo % 4 == 0, "lora_xwt: M, K, rows(v) must be multiples of 64");
+  DevGuard g(x.device());
+  const int64_t nws = mx_lora_xwt_ws((int)M, (int)K);
+  auto ws = at::empty({nws > 0 ? nws : 1}, x.options().dtype(at::kFloat));
+  MX_OK(mx_lora_xwt(bf(x), ldx, bf(v), ldv, (int)Vr, bfm(out), ldo, ws.data_ptr<float>(), (int)M, (int)K, (float)alpha,
+                    cur_stream()));
+}
+
+// LoRA adapter gradients in ONE launch: ga [R, K] (+)= g^T x and the diagonal blocks
+// gb[off_i : off_i + n_i, i r : (i + 1) r] (+)= dy_i^T st_i.  x [T, K], dy [T, N], and the
+// tails g [T, >= 64], st [T, >= 64] (row views); r % 16 == 0.
+void lora_grads(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& g, const at::Tensor& st, at::Tensor& ga,
+                at::Tensor& gb, at::IntArrayRef splits, int64_t r, bool accumulate) {
+  const int64_t ldx = check_rows_bf16(x, "x"), ldd = check_rows_bf16(dy, "dy");
+  const int64_t ldg = check_rows_bf16(g, "g"), lds = check_rows_bf16(st, "st");
+  check_bf16(ga, "ga");
+  check_bf16(gb, "gb");
+  const int64_t T = x.size(0), K = x.size(1), N = dy.size(1), n = (int64_t)splits.size(), R = n * r;
+  MX_CHECK(dy.size(0) == T && g.size(0) == T && st.size(0) == T, "lora_grads: token counts differ");
+  MX_CHECK(ga.size(0) == R && ga.size(1) == K && gb.size(0) == N && gb.size(1) == R, "lora_grads: grad shapes");
+  MX_CHECK(T % 64 == 0 && K % 64 == 0 && r % 16 == 0 && r <= 64, "lora_grads: T, K multiples of 64, r of 16");
+  std::vector<int64_t> desc;
+  auto add = [&](const uint16_t* X, int64_t lx, const uint16_t* G, int64_t lg, int64_t gw, uint16_t* out, int64_t os_n,
+                 int64_t os_j, int64_t Nx, int64_t jb0, int64_t JB) {
+    // JB > 1 reads a 64-column G window starting at column 16 jb0
+    MX_CHECK(JB == 1 || 16 * jb0 + 64 <= gw, "lora_grads: operand tail too narrow");
+    MX_CHECK(Nx % 64 == 0, "lora_grads: split sizes must be multiples of 64");
+    desc.insert(desc.end(), {(int64_t)X, (int64_t)G, (int64_t)out, lx, lg, os_n, os_j, Nx, jb0, JB});
+  };
+  // dA: R columns of g in chunks of <= 4 blocks
+  for (int64_t j0 = 0; j0 < R; j0 += 64) {
+    const int64_t jb = std::min<int64_t>(4, (R - j0) / 16);
+    add(bf(x), ldx, bf(g), ldg, g.size(1), bfm(ga) + j0 * K, 1, K, K, j0 / 16, jb);
+  }
+  int64_t off = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t ni = splits[i];
+    add(bf(dy) + off, ldd, bf(st), lds, st.size(1), bfm(gb) + off * R + i * r, R, 1, ni, i * r / 16, r / 16);
+    off += ni;
+  }
+  MX_CHECK(off == N, "lora_grads: splits do not sum to dy's width");
+  const int np = (int)(desc.size() / 10);
+  MX_CHECK(np <= 8, "lora_grads: too many problems");
+  int64_t ntiles = 0;
+  for (int i = 0; i < np; ++i) ntiles += desc[i * 10 + 7] / 64;
+  DevGuard gd(x.device());
+  const int64_t nws = mx_lora_xtg_ws((int)ntiles, (int)T);
+  auto ws = at::empty({nws > 0 ? nws : 1}, x.options().dtype(at::kFloat));
+  MX_OK(mx_lora_xtg(desc.data(), np, (int)T, 1.0f, accumulate ? 1 : 0, ws.data_ptr<float>(), cur_stream()));
+}
+
 TORCH_LIBRARY(mxllm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? res, Tensor w, float eps, int out_pad=0) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw, int out_pad=0) -> (Tensor, Tensor)");
@@ -519,6 +579,8 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
+  m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha) -> ()");
+  m.def("lora_grads(Tensor x, Tensor dy, Tensor g, Tensor st, Tensor(a!) ga, Tensor(b!) gb, int[] splits, int r, bool accumulate) -> ()");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3) -> (Tensor, Tensor, Tensor)");
 }
@@ -546,4 +608,6 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("w8_linear", &w8_linear);
   m.impl("w8_dequant", &w8_dequant);
   m.impl("quant_rows_e4m3", &quant_rows_e4m3);
+  m.impl("lora_xwt", &lora_xwt);
+  m.impl("lora_grads", &lora_grads);
 }

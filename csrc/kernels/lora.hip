@@ -1,0 +1,480 @@
+// mxllm — LoRA rank-r GEMMs for gfx950 (MI355X): the skinny products around a
+// frozen projection that hipBLASLt tiles poorly (measured at the Llama-3.1-70B
+// shapes, T = 4096 tokens: 28-141 us per call, 1.5-4x off the HBM roofline).
+//
+//   lora_xwt : out[M, 64c] = alpha * X[M, K] . V[64c, K]^T        (c = 1, 2, ...)
+//              forward  s x A^T  (V = A, zero-padded rows)  -> x_aug tail
+//              backward s dy B   (V = B^T, a transposed copy kept by FusedLinear)
+//   lora_xtg : out[n, j] (+)= alpha * sum_t X[t, n] . G[t, j]     (batched problems)
+//              dA   = g^T x      (X = x,    G = the dy_aug tail, all R columns)
+//              dB_i = dy_i^T st_i (X = dy_i, G = 16-column block i of the x_aug tail)
+//
+// Both are HBM-streaming reductions (arithmetic intensity <= 64 FLOP/B): the
+// design goal is one pass over the big operand at full bandwidth with enough
+// workgroups to fill 256 CUs, so both split their reduction across the 4 waves
+// of a workgroup AND across workgroups (grid.y), and finish with an ORDERED
+// reduction: the last workgroup of a tile to arrive (agent-scope counter, no
+// spinning) sums the fp32 partials in split order -> bit-reproducible results.
+//
+// lora_xwt: the reduction index k is contiguous in both operands, so MFMA
+// fragments come straight from HBM/L2 into registers (v_mfma_f32_16x16x32_bf16,
+// lane (c, g) holds row c and k = 16 g + 8 p .. +7 of each 64-k block, p = k-step);
+// a wave owns a 64 x 64 output tile (16 accumulators) and double-buffers its
+// 64-k blocks in registers.
+// lora_xtg: the reduction index t is the ROW index of both operands, so each
+// wave streams 64-row blocks of X (64 columns = 128 B per row) and G through
+// LDS-DMA (global_load_lds, source-swizzled 16-B chunks, double-buffered per
+// wave, no workgroup barrier in the loop) and reads both MFMA operands with
+// ds_read_b64_tr_b16 (the attention-V recipe: t permuted inside each 32-row
+// k-step identically for both operands).  Reference: the reference has no LoRA
+// path at all (fine-tuning is a planned-but-missing module,
+// reference src/distributed_inference.py:61-76); the math follows PEFT's LoRA.
+#include "common.h"
+#include <stdlib.h>
+
+namespace mx {
+
+namespace {
+
+typedef __bf16 lbf16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(1))) const void* lgptr_t;
+typedef __attribute__((address_space(3))) void* llptr_t;
+
+__device__ __forceinline__ f32x4 lmfma(const u16x8& a, const u16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(lbf16x8_t, a), __builtin_bit_cast(lbf16x8_t, b),
+                                                 c, 0, 0, 0);
+}
+
+constexpr int kRS = 68;  // fp32 row stride of the 64 x 64 reduction images (16-B aligned, g-rows 16 banks apart)
+constexpr int kMaxTiles = 16384;
+
+// per-tile arrival counters of the ordered split reduction; zero at load, reset
+// to zero by the last workgroup of every tile (all LoRA kernels of a process run
+// on one stream, so calls never interleave on a counter)
+__device__ unsigned int g_xwt_cnt[kMaxTiles];
+__device__ unsigned int g_xtg_cnt[kMaxTiles];
+
+// true in exactly one workgroup of the tile: the last of `S` to arrive.  Every
+// thread's partial stores are made visible at agent scope before the arrival.
+__device__ __forceinline__ bool arrive_last(unsigned int* cnt, int S, int* s_flag) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(cnt, 1u);
+    *s_flag = prev == (unsigned)(S - 1);
+    if (*s_flag) *cnt = 0u;
+  }
+  __syncthreads();
+  const bool last = *s_flag;
+  if (last) __threadfence();  // acquire: the other workgroups' partials
+  return last;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ lora_xwt
+// grid (M/64, S), 256 threads; M % 64 == 0, K % 64 == 0; writes out[:, 0:64].
+__global__ void __launch_bounds__(256, 1) lora_xwt_kernel(const uint16_t* __restrict__ X, int64_t ldx,
+                                                          const uint16_t* __restrict__ V, int64_t ldv,
+                                                          uint16_t* __restrict__ out, int64_t ldo,
+                                                          float* __restrict__ ws, int M, int K, int S, float alpha,
+                                                          int fused_red) {
+  __shared__ __attribute__((aligned(16))) float red[4][64 * kRS];
+  __shared__ int s_last;
+  const int mtiles = M >> 6, mt = blockIdx.x, split = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps the block loop scalar
+  const int nb = K >> 6, nw = S * 4, gw = split * 4 + w;
+  const int b0 = (int)((int64_t)gw * nb / nw), b1 = (int)((int64_t)(gw + 1) * nb / nw);
+  const uint16_t* xp = X + (int64_t)(mt * 64 + c) * ldx + 16 * g;
+  const uint16_t* vp = V + (int64_t)c * ldv + 16 * g;
+  const int64_t xrb = 16 * ldx, vcb = 16 * ldv;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load = [&](int b, u16x8(&xr)[4][2], u16x8(&vr)[4][2]) {
+    const int k0 = b * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        xr[i][p] = *reinterpret_cast<const u16x8*>(xp + i * xrb + k0 + 8 * p);
+        vr[i][p] = *reinterpret_cast<const u16x8*>(vp + i * vcb + k0 + 8 * p);
+      }
+  };
+  auto comp = [&](const u16x8(&xr)[4][2], const u16x8(&vr)[4][2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = lmfma(xr[i][p], vr[j][p], acc[i][j]);
+  };
+  u16x8 xA[4][2], vA[4][2], xB[4][2], vB[4][2];
+  int b = b0;
+  if (b < b1) load(b, xA, vA);
+  // two blocks per trip, the next block's loads issued before this block's MFMAs
+  // (sched_barrier: the scheduler would otherwise sink them below the MFMAs and
+  // leave one block in flight)
+  for (; b + 1 < b1; b += 2) {
+    load(b + 1, xB, vB);
+    __builtin_amdgcn_sched_barrier(0);
+    comp(xA, vA);
+    __builtin_amdgcn_sched_barrier(0);
+    load(min(b + 2, b1 - 1), xA, vA);  // unconditional (a redundant reload at the end): no branch in the loop
+    __builtin_amdgcn_sched_barrier(0);
+    comp(xB, vB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (b < b1) comp(xA, vA);
+  // 4 waves -> one 64 x 64 tile (fixed wave order)
+  float* rw = red[w];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rw[(16 * i + 4 * g + e) * kRS + 16 * j + c] = acc[i][j][e];
+  __syncthreads();
+  float4 v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
+    float4 s = *reinterpret_cast<const float4*>(&red[0][row * kRS + col]);
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const float4 t = *reinterpret_cast<const float4*>(&red[ww][row * kRS + col]);
+      s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
+    }
+    v[q] = s;
+  }
+  if (S > 1) {
+    float* wp = ws + ((int64_t)split * mtiles + mt) * 4096;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) reinterpret_cast<float4*>(wp)[tid + 256 * q] = v[q];
+    if (!fused_red) return;  // lora_xwt_reduce_kernel finishes
+    if (!arrive_last(&g_xwt_cnt[mt], S, &s_last)) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[tid + 256 * q];
+      for (int sp = 1; sp < S; ++sp) {
+        const float4 t = reinterpret_cast<const float4*>(ws + ((int64_t)sp * mtiles + mt) * 4096)[tid + 256 * q];
+        s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
+      }
+      v[q] = s;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
+    uint2 o;
+    o.x = pack_bf16x2(alpha * v[q].x, alpha * v[q].y);
+    o.y = pack_bf16x2(alpha * v[q].z, alpha * v[q].w);
+    *reinterpret_cast<uint2*>(out + (int64_t)(mt * 64 + row) * ldo + col) = o;
+  }
+}
+
+// split partials ws[S][M/64][64][64] -> out (fixed split order); grid M/64
+__global__ void __launch_bounds__(256) lora_xwt_reduce_kernel(const float* __restrict__ ws, int S, int mtiles,
+                                                              uint16_t* __restrict__ out, int64_t ldo, float alpha) {
+  const int mt = blockIdx.x, tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[tid + 256 * q];
+    for (int sp = 1; sp < S; ++sp) {
+      const float4 t = reinterpret_cast<const float4*>(ws + ((int64_t)sp * mtiles + mt) * 4096)[tid + 256 * q];
+      s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
+    }
+    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
+    uint2 o;
+    o.x = pack_bf16x2(alpha * s.x, alpha * s.y);
+    o.y = pack_bf16x2(alpha * s.z, alpha * s.w);
+    *reinterpret_cast<uint2*>(out + (int64_t)(mt * 64 + row) * ldo + col) = o;
+  }
+}
+
+// ------------------------------------------------------------------ lora_xtg
+struct XtgProb {
+  const uint16_t* X;  // [T, >= n0 + Nx] row stride ldx (column 0 of this problem)
+  const uint16_t* G;  // [T, >= 64] row stride ldg (column 0 of the 64-wide operand tail)
+  uint16_t* out;      // element (n, j) at out[n * os_n + j * os_j]
+  int64_t ldx, ldg, os_n, os_j;
+  int Nx, jb0, JB, tile0;  // jb0: first 16-col block of G; JB blocks (<= 4); narrow when JB == 1
+};
+constexpr int kMaxProb = 8;
+struct XtgArgs {
+  XtgProb p[kMaxProb];
+  int np, T, S, ntiles;
+  float alpha;
+  int accumulate;
+  int fused_red;  // 1: last-arriving workgroup reduces; 0: lora_xtg_reduce_kernel does
+};
+
+// 16-B chunk swizzle of a 128-B LDS row: conflict-free ds_read_b64_tr_b16 of
+// rows 4 g + qq (each 32-lane half reads 8 rows x 32 B onto 8 distinct 32-B bank groups)
+__device__ __forceinline__ int xsw(int row) { return (((row >> 1) & 1) << 2) | (((row >> 2) & 1) << 1); }
+
+// grid (ntiles, S), 256 threads; T % 64 == 0, every Nx % 64 == 0.
+__global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float* __restrict__ ws) {
+  constexpr int XB = 8192, STG = 16384, WREG = 2 * STG;  // per wave: 2 stages x (X 8 KiB + G <= 8 KiB)
+  __shared__ __attribute__((aligned(16))) char smem[4 * WREG];
+  __shared__ int s_last;
+  const int tile = blockIdx.x, split = blockIdx.y;
+  // this tile's problem, selected with uniform conditional copies (a dynamic index
+  // into the kernel-argument array would be lowered through scratch)
+  XtgProb P = a.p[0];
+#pragma unroll
+  for (int i = 1; i < kMaxProb; ++i)
+    if (i < a.np && tile >= a.p[i].tile0) P = a.p[i];
+  const int n0 = (tile - P.tile0) * 64;
+  const bool wide = P.JB > 1;
+  const int JB = P.JB;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps the block loop scalar
+  const int qq = c >> 2, pp = c & 3;
+  const int nblk = a.T >> 6, nw = a.S * 4, gw = split * 4 + w;
+  const int b0 = (int)((int64_t)gw * nblk / nw), b1 = (int)((int64_t)(gw + 1) * nblk / nw);
+  char* wreg = smem + w * WREG;
+  const uint32_t wbase = lds_addr(wreg);
+
+  // LDS-DMA sources (lane-linear 1-KiB destinations): X rows 8 q + (lane >> 3)
+  const int xrow = lane >> 3, xch = (lane & 7) ^ xsw(lane >> 3);
+  const uint16_t* xsrc = P.X + (int64_t)xrow * P.ldx + n0 + 8 * xch;
+  const uint16_t* gsrc = wide ? P.G + (int64_t)xrow * P.ldg + 16 * P.jb0 + 8 * xch
+                              : P.G + (int64_t)(lane >> 1) * P.ldg + 16 * P.jb0 + 8 * (lane & 1);
+  auto issue = [&](int b, int s) {
+    const int64_t t0 = (int64_t)b * 64;
+    char* xs = wreg + s * STG;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_global_load_lds((lgptr_t)(xsrc + (t0 + 8 * q) * P.ldx), (llptr_t)(xs + q * 1024), 16, 0, 0);
+    if (wide) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        __builtin_amdgcn_global_load_lds((lgptr_t)(gsrc + (t0 + 8 * q) * P.ldg), (llptr_t)(xs + XB + q * 1024), 16, 0,
+                                         0);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_global_load_lds((lgptr_t)(gsrc + (t0 + 32 * q) * P.ldg), (llptr_t)(xs + XB + q * 1024), 16,
+                                         0, 0);
+    }
+  };
+  // transposed-read lane bases: row 4 g + qq of each 16-row group, logical cols 16 blk + 4 pp
+  const int fl = xsw(4 * g + qq);
+  uint32_t xb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xb[i] = wbase + (4 * g + qq) * 128 + 16 * ((2 * i + (pp >> 1)) ^ fl) + 8 * (pp & 1);
+  const uint32_t gnb = wbase + XB + (4 * g + qq) * 32 + 8 * pp;  // narrow G image: 32-B rows
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto block = [&](auto SC, int b) {
+    constexpr int s = decltype(SC)::value;
+    // this block's DMA has landed (the next block's may still be in flight)
+    if (b + 1 < b1) {
+      if (wide) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    u16x4 xr[2][2][4], gr[2][2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[ks][h][i] = trd_off(xb[i], s * STG + (32 * ks + 16 * h) * 128);
+        if (wide) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < JB) gr[ks][h][j] = trd_off(xb[j], s * STG + XB + (32 * ks + 16 * h) * 128);
+        } else {
+          gr[ks][h][0] = trd_off(gnb, s * STG + (32 * ks + 16 * h) * 32);
+        }
+      }
+    lds_wait();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pin(xr[ks][h][i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < JB) pin(gr[ks][h][j]);
+      }
+    if (b + 2 < b1) issue(b + 2, s);  // refill this stage (its reads have retired)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= JB) continue;
+        const u16x8 bf = u16x8{gr[ks][0][j][0], gr[ks][0][j][1], gr[ks][0][j][2], gr[ks][0][j][3],
+                               gr[ks][1][j][0], gr[ks][1][j][1], gr[ks][1][j][2], gr[ks][1][j][3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const u16x8 af = u16x8{xr[ks][0][i][0], xr[ks][0][i][1], xr[ks][0][i][2], xr[ks][0][i][3],
+                                 xr[ks][1][i][0], xr[ks][1][i][1], xr[ks][1][i][2], xr[ks][1][i][3]};
+          acc[i][j] = lmfma(af, bf, acc[i][j]);
+        }
+      }
+    }
+  };
+  if (b0 < b1) issue(b0, 0);
+  if (b0 + 1 < b1) issue(b0 + 1, 1);
+  for (int b = b0; b < b1; b += 2) {
+    block(std::integral_constant<int, 0>{}, b);
+    if (b + 1 < b1) block(std::integral_constant<int, 1>{}, b + 1);
+  }
+  // 4 waves -> one 64 x 16 JB tile in LDS (each wave's own region; its DMA has drained)
+  float* rw = reinterpret_cast<float*>(wreg);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j >= JB) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rw[(16 * i + 4 * g + e) * kRS + 16 * j + c] = acc[i][j][e];
+    }
+  __syncthreads();
+  const int J = 16 * JB, nel = 64 * J;
+  const bool jfast = P.os_j == 1;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q;
+    v[q] = 0.f;
+    if (e < nel) {
+      const int n = jfast ? e / J : (e & 63), j = jfast ? e % J : (e >> 6);
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) s += reinterpret_cast<const float*>(smem + ww * WREG)[n * kRS + j];
+      v[q] = s;
+    }
+  }
+  if (a.S > 1) {
+    float* wp = ws + ((int64_t)split * a.ntiles + tile) * 4096;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (tid + 256 * q < nel) wp[tid + 256 * q] = v[q];
+    if (!a.fused_red) return;
+    if (!arrive_last(&g_xtg_cnt[tile], a.S, &s_last)) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 256 * q;
+      if (e < nel) {
+        float s = ws[(int64_t)tile * 4096 + e];
+        for (int sp = 1; sp < a.S; ++sp) s += ws[((int64_t)sp * a.ntiles + tile) * 4096 + e];
+        v[q] = s;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q;
+    if (e < nel) {
+      const int n = jfast ? e / J : (e & 63), j = jfast ? e % J : (e >> 6);
+      uint16_t* o = P.out + (int64_t)(n0 + n) * P.os_n + (int64_t)j * P.os_j;
+      const float r = a.alpha * v[q] + (a.accumulate ? bf2f(*o) : 0.f);
+      *o = f2bf(r);
+    }
+  }
+}
+
+// split partials -> outputs (fixed split order); grid ntiles
+__global__ void __launch_bounds__(256) lora_xtg_reduce_kernel(const XtgArgs a, const float* __restrict__ ws) {
+  const int tile = blockIdx.x, tid = threadIdx.x;
+  XtgProb P = a.p[0];
+#pragma unroll
+  for (int i = 1; i < kMaxProb; ++i)
+    if (i < a.np && tile >= a.p[i].tile0) P = a.p[i];
+  const int n0 = (tile - P.tile0) * 64, J = 16 * P.JB, nel = 64 * J;
+  const bool jfast = P.os_j == 1;
+  for (int e = tid; e < nel; e += 256) {
+    float s = ws[(int64_t)tile * 4096 + e];
+    for (int sp = 1; sp < a.S; ++sp) s += ws[((int64_t)sp * a.ntiles + tile) * 4096 + e];
+    const int n = jfast ? e / J : (e & 63), j = jfast ? e % J : (e >> 6);
+    uint16_t* o = P.out + (int64_t)(n0 + n) * P.os_n + (int64_t)j * P.os_j;
+    *o = f2bf(a.alpha * s + (a.accumulate ? bf2f(*o) : 0.f));
+  }
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+// split count of the ordered split reduction: ~512 workgroups, >= 2 blocks per wave
+static int lora_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+static int lora_splits(int tiles, int blocks, int smax) {
+  const int target = lora_env("MXLLM_LORA_WGS", 256);  // tuning knob: workgroups to aim for
+  int S = (target + tiles - 1) / tiles;
+  S = S < 1 ? 1 : (S > smax ? smax : S);
+  while (S > 1 && blocks / (4 * S) < 2) --S;
+  return S;
+}
+
+// fp32 workspace floats needed by mx_lora_xwt (M, K) / mx_lora_xtg (total 64-col tiles, T)
+extern "C" int64_t mx_lora_xwt_ws(int M, int K) {
+  const int S = lora_splits(M / 64, K / 64, 16);
+  return S > 1 ? (int64_t)S * (M / 64) * 4096 : 0;
+}
+extern "C" int64_t mx_lora_xtg_ws(int ntiles, int T) {
+  const int S = lora_splits(ntiles, T / 64, 8);
+  return S > 1 ? (int64_t)S * ntiles * 4096 : 0;
+}
+
+// out[:, 0:Vrows] = alpha X V^T, one launch per 64 output columns.
+extern "C" int mx_lora_xwt(const uint16_t* X, int64_t ldx, const uint16_t* V, int64_t ldv, int Vrows, uint16_t* out,
+                           int64_t ldo, float* ws, int M, int K, float alpha, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M % 64 || K % 64 || Vrows % 64 || M / 64 > kMaxTiles) return (int)hipErrorInvalidValue;
+  const int mtiles = M / 64, S = lora_splits(mtiles, K / 64, 16);
+  const int fused = lora_env("MXLLM_LORA_FUSED_RED", 0);
+  for (int c0 = 0; c0 < Vrows; c0 += 64) {
+    lora_xwt_kernel<<<dim3(mtiles, S), 256, 0, stream>>>(X, ldx, V + (int64_t)c0 * ldv, ldv, out + c0, ldo, ws, M, K,
+                                                         S, alpha, fused);
+    if (S > 1 && !fused) lora_xwt_reduce_kernel<<<mtiles, 256, 0, stream>>>(ws, S, mtiles, out + c0, ldo, alpha);
+  }
+  return (int)hipGetLastError();
+}
+
+// Batched sum_t X[t, n] G[t, j] problems (see XtgProb).  desc: np rows of
+// {X, G, out, ldx, ldg, os_n, os_j, Nx, jb0, JB} as int64; ws: mx_lora_xtg_ws floats.
+extern "C" int mx_lora_xtg(const int64_t* desc, int np, int T, float alpha, int accumulate, float* ws,
+                           hipStream_t stream) {
+  if (np <= 0 || np > kMaxProb || T % 64) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  XtgArgs a{};
+  int ntiles = 0;
+  for (int i = 0; i < np; ++i) {
+    const int64_t* d = desc + i * 10;
+    XtgProb& p = a.p[i];
+    p.X = reinterpret_cast<const uint16_t*>(d[0]);
+    p.G = reinterpret_cast<const uint16_t*>(d[1]);
+    p.out = reinterpret_cast<uint16_t*>(d[2]);
+    p.ldx = d[3], p.ldg = d[4], p.os_n = d[5], p.os_j = d[6];
+    p.Nx = (int)d[7], p.jb0 = (int)d[8], p.JB = (int)d[9];
+    if (p.Nx <= 0 || p.Nx % 64 || p.JB < 1 || p.JB > 4) return (int)hipErrorInvalidValue;
+    p.tile0 = ntiles;
+    ntiles += p.Nx / 64;
+  }
+  if (ntiles > kMaxTiles) return (int)hipErrorInvalidValue;
+  a.np = np, a.T = T, a.S = lora_splits(ntiles, T / 64, 8), a.ntiles = ntiles, a.alpha = alpha;
+  a.accumulate = accumulate;
+  a.fused_red = lora_env("MXLLM_LORA_FUSED_RED", 0);
+  lora_xtg_kernel<<<dim3(ntiles, a.S), 256, 0, stream>>>(a, ws);
+  if (a.S > 1 && !a.fused_red) lora_xtg_reduce_kernel<<<ntiles, 256, 0, stream>>>(a, ws);
+  return (int)hipGetLastError();
+}

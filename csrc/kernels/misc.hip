@@ -72,7 +72,8 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
 // Batched strided 2-D copy of 16-bit elements: one launch refreshes every LoRA
 // adapter's copy inside the augmented GEMM weight buffers after an optimizer
 // step (mxllm/models/llama.py, FusedLinear).  desc[i] = {src, dst, rows, cols,
-// src_ld, dst_ld, first_block}; block b belongs to the descriptor with the
+// src_ld, dst_ld, first_block, src_col_stride, dst_col_stride} (column strides != 1
+// give transposed copies, e.g. B -> the B^T image of the LoRA backward kernel); block b belongs to the descriptor with the
 // largest first_block <= b (binary search), each block copies 4096 elements.
 constexpr int kCopyBlockElems = 4096;
 
@@ -81,18 +82,18 @@ __global__ void __launch_bounds__(256) copy2d_batched_kernel(const int64_t* __re
   const int64_t b = blockIdx.x;
   while (lo < hi) {
     const int mid = (lo + hi + 1) / 2;
-    if (desc[mid * 7 + 6] <= b) lo = mid;
+    if (desc[mid * 9 + 6] <= b) lo = mid;
     else hi = mid - 1;
   }
-  const int64_t* d = desc + lo * 7;
+  const int64_t* d = desc + lo * 9;
   const uint16_t* src = reinterpret_cast<const uint16_t*>(d[0]);
   uint16_t* dst = reinterpret_cast<uint16_t*>(d[1]);
-  const int64_t rows = d[2], cols = d[3], sld = d[4], dld = d[5];
+  const int64_t rows = d[2], cols = d[3], sld = d[4], dld = d[5], scs = d[7], dcs = d[8];
   const int64_t e0 = (b - d[6]) * kCopyBlockElems;
   const int64_t total = rows * cols;
   for (int64_t e = e0 + threadIdx.x; e < min(total, e0 + kCopyBlockElems); e += 256) {
     const int64_t r = e / cols, c = e - r * cols;
-    dst[r * dld + c] = src[r * sld + c];
+    dst[r * dld + c * dcs] = src[r * sld + c * scs];
   }
 }
 

@@ -55,6 +55,9 @@ class FusedLinear(nn.Module):
             self.pad = (n * lora_r + 63) // 64 * 64
             self.register_buffer("wbuf", torch.zeros(N + self.pad, in_features + self.pad, dtype=dtype,
                                                      device=device), persistent=False)
+            # B^T [pad, N] (zero rows past n*r): the k-contiguous operand of the
+            # backward s dy B kernel (csrc/kernels/lora.hip), refreshed with wbuf
+            self.register_buffer("wbt", torch.zeros(self.pad, N, dtype=dtype, device=device), persistent=False)
             self.weight = nn.Parameter(self.wbuf[:N, :in_features], requires_grad=train_base)
             # A: all splits' down-projections stacked; B: block-diagonal up-projection
             self.lora_a = nn.Parameter(torch.empty(n * lora_r, in_features, dtype=dtype, device=device))
@@ -79,7 +82,8 @@ class FusedLinear(nn.Module):
     def adapter_copies(self):
         """(src, dst) pairs: adapter parameters -> their slots in ``wbuf``."""
         N, K, R = sum(self.splits), self.in_features, self.lora_a.shape[0]
-        return [(self.lora_a.data, self.wbuf[N:N + R, :K]), (self.lora_b.data, self.wbuf[:N, K:K + R])]
+        return [(self.lora_a.data, self.wbuf[N:N + R, :K]), (self.lora_b.data, self.wbuf[:N, K:K + R]),
+                (self.lora_b.data, self.wbt[:R, :N].t())]
 
     @torch.no_grad()
     def sync_adapter_(self):
@@ -100,7 +104,7 @@ class FusedLinear(nn.Module):
         if self.lora_r > 0:
             if self.augmented():
                 return ops.lora_linear_aug(x, self.lora_a, self.lora_b, self.wbuf, self.splits, self.scaling,
-                                           self.pad)
+                                           self.pad, self.wbt)
             return ops.lora_linear(x, self.weight, self.lora_a, self.lora_b, self.splits, self.scaling)
         return ops.linear(x, self.weight)
 
@@ -231,9 +235,10 @@ class Llama(nn.Module):
         if getattr(self, "_adapter_desc_key", None) != key:
             rows, total = [], 0
             for s, d in pairs:
-                assert s.is_contiguous() and d.stride(1) == 1 and s.element_size() == 2
+                assert s.shape == d.shape and s.element_size() == 2 and d.element_size() == 2
                 n = s.shape[0] * s.shape[1]
-                rows.append([s.data_ptr(), d.data_ptr(), s.shape[0], s.shape[1], s.stride(0), d.stride(0), total])
+                rows.append([s.data_ptr(), d.data_ptr(), s.shape[0], s.shape[1], s.stride(0), d.stride(0), total,
+                             s.stride(1), d.stride(1)])
                 total += (n + 4095) // 4096
             self._adapter_desc = torch.tensor(rows, dtype=torch.int64, device=pairs[0][0].device)
             self._adapter_blocks = total

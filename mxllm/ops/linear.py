@@ -25,12 +25,14 @@ cast or accumulate kernels — and DDP is told via ``mark_ready``.
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence
 
 import torch
 import torch.nn.functional as F
 
 from ..parallel.grad_ready import direct_grad, mark_ready
+from ._ext import native, use_native
 
 
 class _LoRALinearFn(torch.autograd.Function):
@@ -102,6 +104,16 @@ def _augment(t: torch.Tensor, pad: int) -> torch.Tensor:
     return full
 
 
+_LORA_KERNELS = os.environ.get("MXLLM_LORA_KERNELS", "1") != "0"  # A/B switch (benchmarks)
+
+
+def _lora_native(x2: torch.Tensor, N: int, K: int, splits, r: int, wbt) -> bool:
+    """Shapes the hand-written LoRA kernels (csrc/kernels/lora.hip) take; others
+    (tiny test models) use hipBLASLt for the rank-r products."""
+    return (_LORA_KERNELS and wbt is not None and use_native(x2) and x2.shape[0] % 64 == 0 and K % 64 == 0 and r % 16 == 0
+            and r <= 64 and all(n % 64 == 0 for n in splits) and x2.dtype == torch.bfloat16)
+
+
 class _LoRAAugFn(torch.autograd.Function):
     """LoRA projection as ONE augmented GEMM per direction (FusedLinear, models/llama.py).
 
@@ -118,59 +130,83 @@ class _LoRAAugFn(torch.autograd.Function):
     extra traffic is the rank-Rp tail — no read-modify-write of the [T, N]
     output or the [T, K] input gradient (measured at the 70B shapes: qkv fwd
     0.79 -> 0.68 ms, gu fwd 2.66 -> 2.47 ms, down bwd 1.56 -> 1.47 ms).
+    The rank-r products (the two tails, dA and every dB_i) run on the HIP
+    kernels of csrc/kernels/lora.hip — one streaming pass over x or dy each,
+    dA and all dB_i in ONE launch — with ``wbt`` = B^T as the k-contiguous
+    operand of s dy B; hipBLASLt handles them for shapes those kernels do not take.
     """
 
     @staticmethod
-    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad):
+    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt):
         N, K = wbuf.shape[0] - pad, wbuf.shape[1] - pad
         x2 = x.reshape(-1, K)
         xa = _augment(x2, pad)
-        xa[:, K:].addmm_(x2, wbuf[N:, :K].t(), beta=0.0, alpha=scaling)  # s t, zero in the pad columns
+        nat = _lora_native(x2, N, K, splits, r, wbt)
+        if nat:
+            native().lora_xwt(x2, wbuf[N:, :K], xa[:, K:], scaling)  # s t, zero in the pad columns
+        else:
+            xa[:, K:].addmm_(x2, wbuf[N:, :K].t(), beta=0.0, alpha=scaling)
         y = torch.mm(xa, wbuf[:N, :].t())
         ctx.save_for_backward(xa, wbuf)
-        ctx.lora_a, ctx.lora_b = a, b
-        ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape)
+        ctx.lora_a, ctx.lora_b, ctx.wbt = a, b, wbt
+        ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat)
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
         xa, wbuf = ctx.saved_tensors
-        N, K, s, splits, r, pad, xshape = ctx.dims
+        N, K, s, splits, r, pad, xshape, nat = ctx.dims
         R = r * len(splits)
         dy2 = dy.reshape(-1, N)
         dya = _augment(dy2, pad)
-        dya[:, N:].addmm_(dy2, wbuf[:N, K:], beta=0.0, alpha=s)  # g = s dy B, zero in the pad columns
+        if nat:
+            native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s)  # g = s dy B, zero in the pad columns
+        else:
+            dya[:, N:].addmm_(dy2, wbuf[:N, K:], beta=0.0, alpha=s)
         g = dya[:, N:N + R]
         x2, st = xa[:, :K], xa[:, K:K + R]
         da = db = None
-        if ctx.needs_input_grad[1]:
-            ga = direct_grad(ctx.lora_a)
-            if ga is not None:
-                ga.addmm_(g.t(), x2)
+        need_a, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        ga = direct_grad(ctx.lora_a) if need_a else None
+        gb = direct_grad(ctx.lora_b) if need_b else None
+        if nat and need_a and need_b:
+            # dA and every diagonal dB_i in one launch, straight into the flat grads when present
+            acc = ga is not None and gb is not None
+            tga = ga if acc else torch.empty(R, K, dtype=dy2.dtype, device=dy2.device)
+            tgb = gb if acc else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
+            native().lora_grads(x2, dy2, dya[:, N:], xa[:, K:], tga, tgb, list(splits), r, acc)
+            if acc:
                 mark_ready(ctx.lora_a)
-            else:
-                da = torch.mm(g.t(), x2)
-        if ctx.needs_input_grad[2]:
-            gb = direct_grad(ctx.lora_b)
-            tgt = gb if gb is not None else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
-            off = 0
-            for i, n_i in enumerate(splits):
-                tgt[off:off + n_i, i * r:(i + 1) * r].addmm_(dy2[:, off:off + n_i].t(), st[:, i * r:(i + 1) * r],
-                                                            beta=1.0 if gb is not None else 0.0)
-                off += n_i
-            if gb is not None:
                 mark_ready(ctx.lora_b)
             else:
-                db = tgt
+                da, db = tga, tgb
+        else:
+            if need_a:
+                if ga is not None:
+                    ga.addmm_(g.t(), x2)
+                    mark_ready(ctx.lora_a)
+                else:
+                    da = torch.mm(g.t(), x2)
+            if need_b:
+                tgt = gb if gb is not None else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
+                off = 0
+                for i, n_i in enumerate(splits):
+                    tgt[off:off + n_i, i * r:(i + 1) * r].addmm_(dy2[:, off:off + n_i].t(), st[:, i * r:(i + 1) * r],
+                                                                beta=1.0 if gb is not None else 0.0)
+                    off += n_i
+                if gb is not None:
+                    mark_ready(ctx.lora_b)
+                else:
+                    db = tgt
         dx = torch.mm(dya, wbuf[:, :K])
-        return dx.view(xshape), da, db, None, None, None, None, None
+        return dx.view(xshape), da, db, None, None, None, None, None, None
 
 
 def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: torch.Tensor, splits: Sequence[int],
-                    scaling: float, pad: int) -> torch.Tensor:
+                    scaling: float, pad: int, wbt: torch.Tensor | None = None) -> torch.Tensor:
     """LoRA projection through the augmented weight buffer (see _LoRAAugFn)."""
     r = a.shape[0] // len(splits)
-    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad)
+    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt)
 
 
 class _LinearFn(torch.autograd.Function):

@@ -70,7 +70,7 @@ class Engine:
     def __init__(self, model, max_batch: int = 8, max_seq: int = 4096, device=None, eos_ids=(),
                  use_graphs: bool | None = None, prefill_tokens: int = 16384):
         self.model = model
-        self.prefill_tokens = max(1, prefill_tokens)
+        self.prefill_budget = max(1, prefill_tokens)  # tokens per prefill pass
         self.cfg = model.cfg
         self.device = device or model.tok_emb.device
         self.max_batch = max_batch
@@ -308,7 +308,7 @@ class Engine:
         # prefill_tokens tokens (bounds the activation memory of one pass)
         groups, cur, ntok = [], [], 0
         for r in admit:
-            if cur and ntok + len(r.prompt) > self.prefill_tokens:
+            if cur and ntok + len(r.prompt) > self.prefill_budget:
                 groups.append(cur)
                 cur, ntok = [], 0
             cur.append(r)
@@ -414,3 +414,5 @@ def merge_lora_(model) -> None:
             mod.lora_r = 0
             del mod.lora_a
             del mod.lora_b
+            if hasattr(mod, "wbt"):
+                del mod.wbt

@@ -320,3 +320,63 @@ def test_quant_rows_e4m3(gpu):
     mism = (q.view(torch.float8_e4m3fn).float() != ref.float()).float().mean().item()
     assert mism < 1e-3, mism  # RNE on both sides; only 1/s rounding can flip a tie
     assert rel_err(q.view(torch.float8_e4m3fn).float() * s, xf) < 0.04
+
+
+@pytest.mark.parametrize("T,K,vrows", [(256, 512, 64), (256, 4096, 64), (4096, 1024, 128), (64, 192, 64)])
+def test_lora_xwt(gpu, T, K, vrows):
+    """out[:, :vrows] = alpha x V^T into the tail of a padded buffer (S = 1 and the
+    ordered split reduction), columns past the tail untouched."""
+    torch.manual_seed(3)
+    buf = torch.randn(T, K + vrows + 8, device=gpu, dtype=torch.bfloat16)
+    x = buf[:, :K]
+    vb = torch.randn(vrows, K + 8, device=gpu, dtype=torch.bfloat16)
+    v = vb[:, :K]
+    sentinel = buf[:, K + vrows:].clone()
+    _ops().lora_xwt(x, v, buf[:, K:K + vrows], 2.0)
+    want = 2.0 * x.float() @ v.float().t()
+    assert rel_err(buf[:, K:K + vrows], want) < 1e-2
+    assert torch.equal(buf[:, K + vrows:], sentinel)
+    first = buf[:, K:K + vrows].clone()
+    _ops().lora_xwt(x, v, buf[:, K:K + vrows], 2.0)
+    assert torch.equal(buf[:, K:K + vrows], first)  # bit-reproducible
+
+
+@pytest.mark.parametrize("T,K,splits,r,acc", [(256, 512, [512, 128, 128], 16, False),
+                                              (4096, 1024, [1024, 256, 256], 16, True),
+                                              (512, 256, [1024, 1024], 16, True),
+                                              (256, 320, [192], 16, False),
+                                              (256, 512, [512, 256, 256], 32, True)])
+def test_lora_grads(gpu, T, K, splits, r, acc):
+    """dA = g^T x and the diagonal blocks dB_i = dy_i^T st_i in one launch,
+    accumulated into bf16 grads or written fresh; off-diagonal blocks untouched."""
+    torch.manual_seed(4)
+    n, N = len(splits), sum(splits)
+    R = n * r
+    pad = (R + 63) // 64 * 64
+    xa = torch.randn(T, K + pad, device=gpu, dtype=torch.bfloat16)
+    dya = torch.randn(T, N + pad, device=gpu, dtype=torch.bfloat16)
+    ga = torch.randn(R, K, device=gpu, dtype=torch.bfloat16) if acc else torch.zeros(R, K, device=gpu,
+                                                                                       dtype=torch.bfloat16)
+    gb = torch.randn(N, R, device=gpu, dtype=torch.bfloat16) if acc else torch.zeros(N, R, device=gpu,
+                                                                                       dtype=torch.bfloat16)
+    ga0, gb0 = ga.clone(), gb.clone()
+    x2, dy2, g, st = xa[:, :K], dya[:, :N], dya[:, N:], xa[:, K:]
+    _ops().lora_grads(x2, dy2, g, st, ga, gb, splits, r, acc)
+    want_a = g[:, :R].float().t() @ x2.float() + (ga0.float() if acc else 0)
+    assert rel_err(ga, want_a) < 1e-2
+    want_b = gb0.float().clone()
+    off = 0
+    for i, ni in enumerate(splits):
+        blk = dy2[:, off:off + ni].float().t() @ st[:, i * r:(i + 1) * r].float()
+        want_b[off:off + ni, i * r:(i + 1) * r] = blk + (want_b[off:off + ni, i * r:(i + 1) * r] if acc else 0)
+        off += ni
+    assert rel_err(gb, want_b) < 1e-2
+    mask = torch.ones_like(gb, dtype=torch.bool)
+    off = 0
+    for i, ni in enumerate(splits):
+        mask[off:off + ni, i * r:(i + 1) * r] = False
+        off += ni
+    assert torch.equal(gb[mask], gb0[mask])  # off-diagonal blocks untouched
+    ga1, gb1 = ga0.clone(), gb0.clone()
+    _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
+    assert torch.equal(ga1, ga) and torch.equal(gb1, gb)  # bit-reproducible

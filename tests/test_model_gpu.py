@@ -17,7 +17,7 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("preset,lora", [("tiny-d128", 0), ("tiny-d128", 8), ("tiny", 0)])
+@pytest.mark.parametrize("preset,lora", [("tiny-d128", 0), ("tiny-d128", 8), ("tiny-d128", 16), ("tiny", 0)])
 def test_train_step_matches_reference_path(gpu, preset, lora, monkeypatch):
     from mxllm.models import Llama, get_config
 
