@@ -147,6 +147,17 @@ void copy2d_batched(const at::Tensor& desc, int64_t total_blocks) {
   MX_OK(mx_copy2d_batched(desc.data_ptr<int64_t>(), (int)desc.size(0), total_blocks, cur_stream()));
 }
 
+// out[C, R] = in[R, C]^T for a row-major (row-strided) 16-bit 2-D GPU tensor
+at::Tensor transpose2d(const at::Tensor& in) {
+  MX_CHECK(in.is_cuda() && in.dim() == 2 && in.element_size() == 2, "in must be a 2-D 16-bit GPU tensor");
+  MX_CHECK(in.stride(1) == 1 && in.stride(0) >= in.size(1), "in must be a row-major (row-strided) view");
+  DevGuard g(in.device());
+  const int64_t R = in.size(0), C = in.size(1);
+  auto out = at::empty({C, R}, in.options());
+  MX_OK(mx_transpose16(in.data_ptr(), out.data_ptr(), R, C, in.stride(0), R, cur_stream()));
+  return out;
+}
+
 at::Tensor segmented_mean(const at::Tensor& codes, const at::Tensor& offsets) {
   MX_CHECK(codes.is_cuda() && codes.scalar_type() == at::kInt, "codes must be int32 GPU");
   MX_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kLong, "offsets must be int64 GPU");
@@ -563,6 +574,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw, int out_pad=0) -> (Tensor, Tensor)");
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
+  m.def("transpose2d(Tensor x) -> Tensor");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
@@ -590,6 +602,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("segmented_mean", &segmented_mean);
   m.impl("copy2d_batched", &copy2d_batched);
+  m.impl("transpose2d", &transpose2d);
   m.impl("sqnorm", &sqnorm);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);

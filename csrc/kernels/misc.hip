@@ -131,3 +131,63 @@ extern "C" int mx_sqnorm(const void* x, int bf16, int64_t n, float* out, float* 
   sum_partials_kernel<<<1, 256, 0, stream>>>(work, (int)blocks, out);
   return (int)hipGetLastError();
 }
+
+// 16-bit 2-D transpose out[c, r] = in[r, c] through a 64x64 LDS tile (full
+// fine-tuning dW GEMMs: token-major activations -> token-contiguous images so
+// hipBLASLt runs its reduction-contiguous kernel family, mxllm/ops/linear.py).
+// 256 threads: 16-B row loads (8 threads per 64-element row, 32 rows per pass),
+// 16-B row stores of the transposed tile; row stride 66 halves keeps the
+// column reads at <= 2-way bank sharing.  Edge tiles fall back to scalar
+// accesses.  Row strides are in elements.
+namespace mx {
+constexpr int kTrTile = 64;
+
+__global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                          int64_t R, int64_t C, int64_t ld_in, int64_t ld_out) {
+  __shared__ uint16_t tile[kTrTile][kTrTile + 2];
+  const int64_t r0 = (int64_t)blockIdx.y * kTrTile, c0 = (int64_t)blockIdx.x * kTrTile;
+  const int t = threadIdx.x, sub = t & 7, row = t >> 3;  // 8 threads x 8 elements per row
+  const bool full = (r0 + kTrTile <= R) && (c0 + kTrTile <= C) && (ld_in % 8 == 0) && (ld_out % 8 == 0);
+  if (full) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int r = row + 32 * p;
+      const u16x8 v = *reinterpret_cast<const u16x8*>(in + (r0 + r) * ld_in + c0 + sub * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[r][sub * 8 + j] = v[j];
+    }
+  } else {
+    for (int e = t; e < kTrTile * kTrTile; e += 256) {
+      const int r = e / kTrTile, c = e % kTrTile;
+      if (r0 + r < R && c0 + c < C) tile[r][c] = in[(r0 + r) * ld_in + c0 + c];
+    }
+  }
+  __syncthreads();
+  if (full) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int c = row + 32 * p;  // output row (input column)
+      u16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = tile[sub * 8 + j][c];
+      *reinterpret_cast<u16x8*>(out + (c0 + c) * ld_out + r0 + sub * 8) = v;
+    }
+  } else {
+    for (int e = t; e < kTrTile * kTrTile; e += 256) {
+      const int c = e / kTrTile, r = e % kTrTile;
+      if (r0 + r < R && c0 + c < C) out[(c0 + c) * ld_out + r0 + r] = tile[r][c];
+    }
+  }
+}
+}  // namespace mx
+
+extern "C" int mx_transpose16(const void* in, void* out, int64_t R, int64_t C, int64_t ld_in, int64_t ld_out,
+                              hipStream_t stream) {
+  if (R <= 0 || C <= 0) return 0;
+  if (ld_in < C || ld_out < R) return -1;
+  const int64_t gx = (C + kTrTile - 1) / kTrTile, gy = (R + kTrTile - 1) / kTrTile;
+  if (gy > 65535 || gx > 0x7fffffff) return -1;
+  transpose16_kernel<<<dim3((unsigned)gx, (unsigned)gy), 256, 0, stream>>>(
+      reinterpret_cast<const uint16_t*>(in), reinterpret_cast<uint16_t*>(out), R, C, ld_in, ld_out);
+  return (int)hipGetLastError();
+}

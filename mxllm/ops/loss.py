@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._ext import native, use_native
+from .linear import weight_grad_
 
 
 class _LinearCEFn(torch.autograd.Function):
@@ -35,7 +36,7 @@ class _LinearCEFn(torch.autograd.Function):
             if not (isinstance(gl, torch.Tensor) and gl.numel() == 1 and float(gl) == 1.0):
                 dh = dh * gl.to(dh.dtype)
         if ctx.needs_input_grad[1]:
-            dw = torch.matmul(dlogits.t(), h)
+            dw = weight_grad_(None, dlogits, h)
             if not (isinstance(gl, torch.Tensor) and gl.numel() == 1 and float(gl) == 1.0):
                 dw = dw * gl.to(dw.dtype)
         return dh, dw, None, None

@@ -380,3 +380,33 @@ def test_lora_grads(gpu, T, K, splits, r, acc):
     ga1, gb1 = ga0.clone(), gb0.clone()
     _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
     assert torch.equal(ga1, ga) and torch.equal(gb1, gb)  # bit-reproducible
+
+
+@pytest.mark.parametrize("R,C,ld", [(4096, 8192, None), (64, 64, None), (37, 130, None), (130, 4096, 4160),
+                                    (4096, 1, None)])
+def test_transpose2d(gpu, R, C, ld):
+    """LDS-tiled 16-bit transpose (full fine-tuning dW operand images): exact,
+    row-strided inputs and ragged edge tiles included."""
+    torch.manual_seed(0)
+    base = torch.randn(R, ld or C, device=gpu, dtype=torch.bfloat16)
+    x = base[:, :C]
+    y = _ops().transpose2d(x)
+    assert y.shape == (C, R) and y.is_contiguous()
+    assert torch.equal(y, x.t())
+
+
+@pytest.mark.parametrize("T,N,K", [(4096, 1024, 512), (300, 130, 72)])
+def test_weight_grad_tn(gpu, T, N, K):
+    """Full fine-tuning dW through transposed token-contiguous images equals
+    dy^T x (fp32 reference), with and without beta=1 accumulation."""
+    from mxllm.ops.linear import weight_grad_
+
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device=gpu, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=gpu, dtype=torch.bfloat16)
+    want = dy.float().t() @ x.float()
+    assert rel_err(weight_grad_(None, dy, x), want) < 1e-2
+    acc = torch.randn(N, K, device=gpu, dtype=torch.float32)
+    want2 = acc + want
+    weight_grad_(acc, dy, x)
+    assert rel_err(acc, want2) < 1e-3
