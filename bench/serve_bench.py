@@ -11,6 +11,13 @@ Measures on one GPU, random-init bf16 weights, synthetic prompts:
   * end-to-end: Engine.generate over --requests prompts (continuous batching),
     output tokens/s and mean TTFT.
 Prints one JSON line (and writes it to --json-out).
+
+Tensor parallelism (mxllm/parallel/tensor.py):
+  * ``torchrun --nproc-per-node=N bench/serve_bench.py --model llama3.1-70b``:
+    every rank serves its TP shard, two RCCL all-reduces per layer and a
+    vocab-parallel head inside the graphed decode step; rank 0 reports;
+  * ``--tp-shard-proxy N`` (one GPU): rank 0's shard of a TP-N deployment with
+    the collectives left out — the per-GPU compute floor of a TP-N decode step.
 """
 from __future__ import annotations
 
@@ -38,6 +45,8 @@ def main():
     ap.add_argument("--e2e-prompt-len", type=int, default=256)
     ap.add_argument("--fp8", action="store_true", help="e4m3 projection weights (serving quantisation)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--tp-shard-proxy", type=int, default=0,
+                    help="one GPU: run rank 0's TP-N shard without the collectives (per-GPU compute floor)")
     a = ap.parse_args()
 
     from mxllm.models import Llama, get_config
@@ -45,12 +54,29 @@ def main():
     from mxllm.utils import gemm_tuning
 
     gemm_tuning.enable()
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    tp_group, rank = None, 0
+    if world > 1:
+        import torch.distributed as dist
+
+        from mxllm.parallel import runtime
+
+        env = runtime.init()
+        dev, rank, tp_group = env.device, env.rank, dist.group.WORLD
+    else:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
     cfg = get_config(a.model)
     t0 = time.perf_counter()
-    model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    tp = world if world > 1 else a.tp_shard_proxy
+    if tp > 1:
+        from mxllm.parallel.tensor import random_shard
+
+        model = random_shard(cfg, rank, tp, dev, seed=0)
+    else:
+        model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     model.requires_grad_(False)
+    full_cfg, cfg = cfg, model.cfg  # per-rank shapes from here on (KV bytes, prompts use the vocab below)
     if a.fp8:
         from mxllm.serve.quant import quantize_model_fp8_
 
@@ -61,11 +87,11 @@ def main():
         sum(b.numel() * b.element_size() for n, b in model.named_buffers() if n.endswith((".q", ".scale")))
     bmax = max(int(b) for b in a.batches.split(","))
     max_seq = max(a.prompt_len, a.ctx + a.decode_steps, a.e2e_prompt_len + a.new_tokens) + 8
-    eng = Engine(model, max_batch=max(bmax, 1), max_seq=max_seq)
+    eng = Engine(model, max_batch=max(bmax, 1), max_seq=max_seq, tp_group=tp_group)
     g = torch.Generator().manual_seed(0)
 
     def prompt(n):
-        return torch.randint(0, cfg.vocab_size, (n,), generator=g).tolist()
+        return torch.randint(0, full_cfg.vocab_size, (n,), generator=g).tolist()
 
     # ---- prefill / TTFT
     eng.prefill(0, prompt(a.prompt_len))  # warm-up (library handles)
@@ -79,6 +105,10 @@ def main():
     del nxt
     pre_s = min(times)
     out = {"model": a.model, "weights": "fp8-e4m3 projections" if a.fp8 else "bf16",
+           "tensor_parallel": ({"tp": world, "collectives": "RCCL all-reduce x2/layer + logits all-gather"}
+                               if world > 1 else
+                               {"tp": a.tp_shard_proxy, "collectives": "omitted (one-GPU shard proxy)"}
+                               if a.tp_shard_proxy > 1 else None),
            "weights_gb": round(wbytes / 1e9, 1), "init_s": round(init_s, 1),
            "prefill": {"prompt_len": a.prompt_len, "ttft_ms": round(1e3 * pre_s, 2),
                        "tokens_per_s": round(a.prompt_len / pre_s, 1)},
@@ -89,7 +119,7 @@ def main():
         slots = list(range(bs))
         for s in slots:
             eng.lens[s] = a.ctx
-        tok = torch.randint(0, cfg.vocab_size, (bs,), generator=g)
+        tok = torch.randint(0, full_cfg.vocab_size, (bs,), generator=g)
         for _ in range(3):  # capture + warm
             eng.decode(slots, tok)
         for s in slots:
@@ -125,11 +155,14 @@ def main():
                       "output_tokens_per_s": round(ntok / dt, 1),
                       "total_tokens_per_s": round((ntok + a.requests * a.e2e_prompt_len) / dt, 1),
                       "mean_ttft_ms": round(1e3 * (eng2.ttft_sum - ttft0) / max(1, eng2.finished - f0), 1)}
-    line = json.dumps(out)
-    print(line, flush=True)
-    if a.json_out:
-        with open(a.json_out, "w") as f:
-            f.write(line + "\n")
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        runtime.cleanup()
 
 
 if __name__ == "__main__":

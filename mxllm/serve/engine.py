@@ -68,8 +68,19 @@ class Request:
 
 class Engine:
     def __init__(self, model, max_batch: int = 8, max_seq: int = 4096, device=None, eos_ids=(),
-                 use_graphs: bool | None = None, prefill_tokens: int = 16384):
+                 use_graphs: bool | None = None, prefill_tokens: int = 16384, tp_group=None):
+        """``tp_group``: serve a tensor-parallel shard (mxllm/parallel/tensor.py
+        ``shard_llama`` / ``random_shard``) with the other ranks of the group;
+        every rank of the group runs the same schedule (same submissions in the
+        same order, e.g. SPMD ``generate`` or ``serve_follower``)."""
         self.model = model
+        self.tp = None
+        if tp_group is not None:
+            from ..parallel.tensor import TPComm
+
+            self.tp = TPComm(tp_group, getattr(model, "tp_vocab", model.cfg.vocab_size))
+            if self.tp.world == 1:
+                self.tp = None
         self.prefill_budget = max(1, prefill_tokens)  # tokens per prefill pass
         self.cfg = model.cfg
         self.device = device or model.tok_emb.device
@@ -77,6 +88,10 @@ class Engine:
         self.max_seq = min(max_seq, self.cfg.max_seq_len)
         if use_graphs is None:
             use_graphs = self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_GRAPHS", "1") != "0"
+            if self.tp is not None:  # RCCL collectives are graph-capturable, gloo's are not
+                import torch.distributed as dist
+
+                use_graphs = use_graphs and dist.get_backend(self.tp.group) == "nccl"
         self.use_graphs = bool(use_graphs)
         self._graphs: dict = {}
         self._pool = None
@@ -119,8 +134,12 @@ class Engine:
             qkv = layer.wqkv(xn)
             o = attn_fn(i, qkv)
             a = layer.wo(o)
+            if self.tp is not None:  # row-parallel Wo: sum the heads' partial outputs
+                self.tp.all_reduce_(a)
             xn, h = ops.add_rms_norm(a, h, layer.mlp_norm, c.norm_eps)
             d = layer.wd(ops.swiglu(layer.wgu(xn)))
+            if self.tp is not None:  # row-parallel Wdown
+                self.tp.all_reduce_(d)
             nxt = m.layers[i + 1].attn_norm if i + 1 < len(m.layers) else m.final_norm
             xn, h = ops.add_rms_norm(d, h, nxt, c.norm_eps)
         return xn
@@ -142,7 +161,13 @@ class Engine:
 
         xn = self._layers(x, attn)
         self.lens[slot] = S
-        return torch.matmul(xn[-1:], m.head_weight.t()).float()[0]
+        return self._logits(xn[-1:]).float()[0]
+
+    def _logits(self, xn: torch.Tensor) -> torch.Tensor:
+        out = torch.matmul(xn, self.model.head_weight.t())
+        if self.tp is not None:  # vocab-parallel head
+            out = self.tp.gather_logits(out)
+        return out
 
     @torch.no_grad()
     def prefill_batch(self, slots: list[int], prompts: list[list[int]]) -> torch.Tensor:
@@ -170,7 +195,7 @@ class Engine:
         for s_, S in zip(slots, lens):
             self.lens[s_] = S
         last = torch.tensor([o - 1 for o in offs[1:]], device=self.device)
-        return torch.matmul(xn.index_select(0, last), m.head_weight.t()).float()
+        return self._logits(xn.index_select(0, last)).float()
 
     @torch.no_grad()
     def decode(self, slots: list[int], tokens: torch.Tensor) -> torch.Tensor:
@@ -200,7 +225,7 @@ class Engine:
                                          c.n_heads, c.n_kv_heads, c.head_dim, max_len)
 
         xn = self._layers(x, attn)
-        return torch.matmul(xn, m.head_weight.t())
+        return self._logits(xn)
 
     def _buckets(self, B: int, max_len: int) -> tuple[int, int]:
         bb = 1
@@ -295,6 +320,45 @@ class Engine:
         elif self.lens[r.slot] + 1 >= self.max_seq:
             self._finish(r, "length")
 
+    def enable_tp_sync(self) -> None:
+        """Server mode of a tensor-parallel group: requests arrive on group rank 0
+        only; every ``step`` rank 0 broadcasts the requests it admits (prompt +
+        sampling params, usually an empty list) and the other ranks, running
+        ``follow()``, admit the same requests into the same slots.  The schedule
+        is deterministic from there on (identical logits on every rank)."""
+        if self.tp is None:
+            return
+        self.tp_sync = True
+        self._tp_stop = False
+
+    def _sync_admit(self, admit: list) -> list:
+        import torch.distributed as dist
+
+        src = dist.get_global_rank(self.tp.group, 0)
+        dev = self.device if dist.get_backend(self.tp.group) == "nccl" else torch.device("cpu")
+        if self.tp.rank == 0:
+            payload = [None if self._stop else [(r.prompt, r.params) for r in admit]]
+            dist.broadcast_object_list(payload, src=src, group=self.tp.group, device=dev)
+            return admit
+        payload = [None]
+        dist.broadcast_object_list(payload, src=src, group=self.tp.group, device=dev)
+        if payload[0] is None:
+            self._tp_stop = True
+            return []
+        mirrored = []
+        for prompt, params in payload[0]:
+            r = Request(next(self._ids), list(prompt), params)
+            r.slot = self.free_slots.pop(0)
+            mirrored.append(r)
+        return mirrored
+
+    def follow(self) -> None:
+        """Non-zero ranks of a TP serving group: mirror rank 0's schedule until it
+        stops (``enable_tp_sync`` first)."""
+        self.enable_tp_sync()
+        while not self._tp_stop:
+            self.step()
+
     def step(self) -> bool:
         """Admit + prefill waiting requests into free slots, then one decode step
         for the running batch.  Returns False when there is nothing to do."""
@@ -304,6 +368,8 @@ class Engine:
                 r = self.waiting.pop(0)
                 r.slot = self.free_slots.pop(0)
                 admit.append(r)
+        if getattr(self, "tp_sync", False):
+            admit = self._sync_admit(admit)
         # admitted prompts are prefilled together, in groups of at most
         # prefill_tokens tokens (bounds the activation memory of one pass)
         groups, cur, ntok = [], [], 0
@@ -378,11 +444,16 @@ class Engine:
         def loop():
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
+            sync = getattr(self, "tp_sync", False)
             while not self._stop:
                 with self._cv:
                     while not self._stop and not self.waiting and not self.active:
                         self._cv.wait(timeout=0.5)
+                        if sync:  # idle heartbeat: followers wait inside a broadcast
+                            break
                 if self._stop:
+                    if sync:
+                        self._sync_admit([])  # tells the followers to stop
                     break
                 try:
                     self.step()

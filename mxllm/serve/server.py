@@ -171,7 +171,10 @@ def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = 
 
 def build_default(model: str = "tiny", device: str | None = None, max_batch: int = 8, max_seq: int = 2048,
                   checkpoint: str | None = None, tokenizer_path: str | None = None, seed: int = 0,
-                  weights: str = "bf16"):
+                  weights: str = "bf16", tp_group=None):
+    """Engine + tokenizer.  ``tp_group``: this rank serves its tensor-parallel
+    shard (mxllm/parallel/tensor.py) of the model; the full model is built (or
+    loaded) on the rank's GPU, sliced and freed."""
     from ..data.tokenizer import get_tokenizer
     from ..models import Llama, get_config
 
@@ -184,12 +187,21 @@ def build_default(model: str = "tiny", device: str | None = None, max_batch: int
 
         load_model_weights(m, checkpoint)
     m.eval()
+    if tp_group is not None:
+        import torch.distributed as dist
+
+        from ..parallel.tensor import shard_llama
+
+        m = shard_llama(m, dist.get_rank(tp_group), dist.get_world_size(tp_group))
+        if str(device).startswith("cuda"):
+            torch.cuda.empty_cache()
     if weights == "fp8":
         from .quant import quantize_model_fp8_
 
         quantize_model_fp8_(m)
     tok = get_tokenizer(cfg.vocab_size, tokenizer_path, cfg.bos_id, cfg.eos_id)
-    eng = Engine(m, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id, getattr(tok, "eos_id", cfg.eos_id)))
+    eng = Engine(m, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id, getattr(tok, "eos_id", cfg.eos_id)),
+                 tp_group=tp_group)
     return eng, tok
 
 
@@ -206,13 +218,40 @@ def main(argv=None):
     ap.add_argument("--served-name", default=None)
     ap.add_argument("--weights", choices=["bf16", "fp8"], default=os.environ.get("MXLLM_ENGINE_WEIGHTS", "bf16"),
                     help="fp8: e4m3 projection weights (serving quantisation, mxllm/serve/quant.py)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree: launch with torchrun --nproc-per-node=TP; rank 0 serves HTTP, "
+                         "the other ranks follow its schedule")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
-    eng, tok = build_default(a.model, None, a.max_batch, a.max_seq, a.checkpoint, a.tokenizer, weights=a.weights)
+    group, env = None, None
+    if a.tp > 1:
+        import torch.distributed as dist
+
+        from ..parallel import runtime
+
+        env = runtime.init()
+        if env.world_size != a.tp:
+            raise SystemExit(f"--tp {a.tp} needs exactly {a.tp} ranks (torchrun --nproc-per-node={a.tp})")
+        group = dist.group.WORLD
+    eng, tok = build_default(a.model, None, a.max_batch, a.max_seq, a.checkpoint, a.tokenizer, weights=a.weights,
+                             tp_group=group)
+    if group is not None:
+        eng.enable_tp_sync()
+        if env.rank != 0:
+            try:
+                eng.follow()
+            finally:
+                runtime.cleanup()
+            return
     app = build_app(eng, tok, a.served_name or a.model, a.api_key)
     import uvicorn
 
-    uvicorn.run(app, host=a.host, port=a.port, log_level="warning")
+    try:
+        uvicorn.run(app, host=a.host, port=a.port, log_level="warning")
+    finally:
+        if group is not None:
+            eng.stop()
+            runtime.cleanup()
 
 
 if __name__ == "__main__":
