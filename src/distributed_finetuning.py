@@ -18,9 +18,10 @@ import sys
 import time
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-for _p in (_HERE, os.path.dirname(_HERE)):
-    if _p not in sys.path:
-        sys.path.insert(0, _p)
+# the repo root (for mxllm); src/ itself is on the path only when run as a script
+# (adding it on import would shadow the top-level ``tests`` package with src/tests)
+if os.path.dirname(_HERE) not in sys.path:
+    sys.path.insert(0, os.path.dirname(_HERE))
 
 import torch  # noqa: E402
 
