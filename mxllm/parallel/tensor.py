@@ -22,15 +22,19 @@ GPU).  Tensor parallelism splits that stream over the node's GPUs:
     [hidden] vector).
 
 Per token and layer this is two all-reduces of ``tokens x hidden`` bf16 — at
-decode that is 16 KB per sequence for 70B, a latency-bound message: on one
-8-GPU node the communicator is RCCL over the fully connected xGMI mesh
-(``torch.distributed`` "nccl" backend), and the collectives are captured into
-the engine's decode hipGraph with the rest of the step.  Divisibility: tp must
+decode that is 16 KB per sequence for 70B, a latency-bound message.  On one
+8-GPU node those go through a graph-safe one-shot xGMI kernel
+(``XgmiGraphComm``: every rank pushes its partial straight into all 7 peers'
+buffers over the direct links and reduces locally in rank order; epochs live
+in device memory so the launch is captured into the engine's decode hipGraph
+with the rest of the step); prefill-sized reductions and the logits gather
+use RCCL (``torch.distributed`` "nccl" backend, also graph-captured).  Divisibility: tp must
 divide n_kv_heads (8 for Llama-3.1 8B/70B -> tp in {1, 2, 4, 8}) and ffn.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -116,17 +120,39 @@ def _head_shard(w: torch.Tensor, rank: int, tp: int) -> torch.Tensor:
 
 
 class TPComm:
-    """The two collectives of a tensor-parallel forward over ``group``."""
+    """The two collectives of a tensor-parallel forward over ``group``.
 
-    def __init__(self, group, vocab: int):
+    Partial-sum all-reduces up to ``max_xgmi_elems`` bf16 elements (decode
+    batches: B x hidden) go through the graph-safe xGMI one-shot kernel when
+    every rank of the group is on this node (``mxllm/parallel/xgmi.py``
+    ``XgmiGraphComm``: each rank pushes its partial into all peers' buffers
+    over the direct links, one hop, no RCCL channel setup); larger ones
+    (prefill) and non-GPU groups use ``torch.distributed`` (RCCL / gloo).
+    The choice depends only on the tensor size, so every rank takes the same
+    path for the same call."""
+
+    def __init__(self, group, vocab: int, device=None, max_xgmi_elems: int = 1 << 19):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.vocab = vocab
+        self.xgmi = None
+        if (device is not None and device.type == "cuda" and self.world > 1
+                and os.environ.get("MXLLM_TP_XGMI", "1") != "0"):
+            from . import xgmi
+
+            self.xgmi = xgmi.create(device, group, cls=xgmi.XgmiGraphComm, max_elems=max_xgmi_elems)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.xgmi is not None and self.xgmi.fits(t):
+            return self.xgmi.all_reduce_(t)
         dist.all_reduce(t, group=self.group)
         return t
+
+    def close(self):
+        if self.xgmi is not None:
+            self.xgmi.close()
+            self.xgmi = None
 
     def gather_logits(self, local: torch.Tensor) -> torch.Tensor:
         """[B, V_shard] per rank -> [B, vocab] (identical on every rank)."""

@@ -91,6 +91,60 @@ class XgmiComm:
         self._c.close()
 
 
+class XgmiGraphComm:
+    """Graph-safe bf16 sum all-reduce over peer memory (tensor-parallel decode):
+    device-resident epochs, so the launch can be captured into a hipGraph and
+    replayed.  ``csrc/kernels/xgmi.hip`` ``mx_xgmi_allreduce_bf16``."""
+
+    def __init__(self, rank: int, world: int, device: torch.device, *, max_elems: int = 1 << 19,
+                 timeout_s: float | None = None):
+        from ..ops._ext import native
+
+        native()
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("MXLLM_XGMI_TIMEOUT_S", "300"))
+        self.rank, self.world, self.device, self.timeout_s = rank, world, device, float(timeout_s)
+        self.max_elems = max_elems
+        self._c = torch.classes.mxllm.XgmiGraphComm(rank, world, device.index, max_elems, float(timeout_s))
+
+    def handle(self) -> list[int]:
+        return self._c.handle().tolist()
+
+    def open(self, handles: list[list[int]]):
+        self._c.open(torch.tensor(handles, dtype=torch.uint8))
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return (t.dtype == torch.bfloat16 and t.is_contiguous() and t.device == self.device
+                and 0 < t.numel() <= self.max_elems and t.numel() % 8 == 0)
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        self._c.all_reduce_(t)
+        return t
+
+    def self_test(self, timeout_s: float = 20.0) -> bool:
+        self._c.set_timeout(timeout_s)
+        try:
+            n = 4096 + 8
+            t = (torch.arange(n, device=self.device) % 7 + self.rank).to(torch.bfloat16)
+            self.all_reduce_(t)
+            want = ((torch.arange(n, device=self.device) % 7) * self.world
+                    + self.world * (self.world - 1) / 2).to(torch.bfloat16)
+            ok = bool(torch.equal(t, want)) and not self._c.error()
+            if not ok:
+                log.warning("xGMI bf16 self-test mismatch on rank %d", self.rank)
+            return ok
+        finally:
+            self._c.clear_error()
+            self._c.set_timeout(self.timeout_s)
+
+    def check(self):
+        if self._c.error():
+            raise RuntimeError("xGMI bf16 all-reduce timed out waiting for a peer (MXLLM_XGMI_TIMEOUT_S)")
+
+    def close(self):
+        self._c.close()
+
+
 def eligible(group=None) -> bool:
     if os.environ.get("MXLLM_XGMI", "1") == "0" or not dist.is_initialized():
         return False
@@ -101,16 +155,17 @@ def eligible(group=None) -> bool:
     return 1 < world <= 16 and local_world == world
 
 
-def create(device: torch.device, group=None, **kw) -> XgmiComm | None:
+def create(device: torch.device, group=None, cls=XgmiComm, **kw):
     """Collective over ``group``: every rank must call it.  Returns a
-    communicator on every rank, or ``None`` on every rank (never a mix, so all
-    ranks keep issuing the same collectives) when peer memory is not usable."""
+    communicator (``cls``: XgmiComm or XgmiGraphComm) on every rank, or
+    ``None`` on every rank (never a mix, so all ranks keep issuing the same
+    collectives) when peer memory is not usable."""
     if not eligible(group):
         return None
     world = dist.get_world_size(group)
     comm, handle = None, None
     try:
-        comm = XgmiComm(dist.get_rank(group), world, device, **kw)
+        comm = cls(dist.get_rank(group), world, device, **kw)
         handle = comm.handle()
     except Exception as e:  # noqa: BLE001
         log.warning("xGMI communicator: local setup failed (%s)", e)

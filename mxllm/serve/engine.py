@@ -78,7 +78,8 @@ class Engine:
         if tp_group is not None:
             from ..parallel.tensor import TPComm
 
-            self.tp = TPComm(tp_group, getattr(model, "tp_vocab", model.cfg.vocab_size))
+            self.tp = TPComm(tp_group, getattr(model, "tp_vocab", model.cfg.vocab_size),
+                             device=device or model.tok_emb.device)
             if self.tp.world == 1:
                 self.tp = None
         self.prefill_budget = max(1, prefill_tokens)  # tokens per prefill pass

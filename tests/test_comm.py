@@ -171,3 +171,87 @@ def test_xgmi_world1_and_roctx(gpu):
     assert torch.ops.mxllm.roctx_available()
     with profiling.range_("test-range"):
         profiling.mark("inside")
+
+
+def _xgmi_graph_worker(rank, world, port, q):
+    """Graph-safe bf16 all-reduce: eager calls of several sizes (multi-workgroup
+    chunks), then the same calls captured once into a hipGraph and replayed
+    with fresh inputs — exact vs the rank-ordered f32 sum, identical on ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from mxllm.parallel import xgmi
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    out = {"rank": rank}
+
+    def vals(n, seed):
+        return [torch.randn(n, generator=torch.Generator().manual_seed(seed * 31 + r)).to(torch.bfloat16)
+                for r in range(world)]
+
+    def want(vs):
+        acc = vs[0].float()
+        for v in vs[1:]:
+            acc = acc + v.float()
+        return acc.to(torch.bfloat16)
+
+    try:
+        comm = xgmi.create(dev, cls=xgmi.XgmiGraphComm, max_elems=1 << 17, timeout_s=30.0)
+        out["created"] = comm is not None
+        if comm is None:
+            return
+        ok = True
+        for it, n in enumerate([8, 8192, 8200, 65536, 131072]):
+            vs = vals(n, it)
+            t = vs[rank].to(dev)
+            comm.all_reduce_(t)
+            ok &= bool(torch.equal(t.cpu(), want(vs)))
+        out["eager_ok"] = ok
+        # capture two reductions (decode-sized) into one graph, replay with new data
+        a = torch.zeros(8192, dtype=torch.bfloat16, device=dev)
+        b = torch.zeros(4 * 8192, dtype=torch.bfloat16, device=dev)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            comm.all_reduce_(a)
+            comm.all_reduce_(b)
+        ok = True
+        for it in range(5):
+            va, vb = vals(a.numel(), 100 + it), vals(b.numel(), 200 + it)
+            a.copy_(va[rank])
+            b.copy_(vb[rank])
+            g.replay()
+            torch.cuda.synchronize()
+            ok &= bool(torch.equal(a.cpu(), want(va))) and bool(torch.equal(b.cpu(), want(vb)))
+        comm.check()
+        out["graph_ok"] = ok
+        dist.barrier()
+        comm.close()
+    except Exception as e:  # noqa: BLE001
+        out["exc"] = repr(e)
+    finally:
+        q.put(out)
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_xgmi_graph_allreduce_bf16_two_procs_one_gpu(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_xgmi_graph_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in ps:
+        o = q.get(timeout=240)
+        res[o["rank"]] = o
+    for p in ps:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert "exc" not in res[r], res[r]
+        assert res[r]["created"] and res[r]["eager_ok"] and res[r]["graph_ok"], res[r]
