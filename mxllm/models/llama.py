@@ -19,6 +19,7 @@ Reference parity: the reference repo advertises "fine-tuning of Meta Llama 3.1
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -42,7 +43,7 @@ class FusedLinear(nn.Module):
     """
 
     def __init__(self, in_features: int, splits: list[int], *, dtype, device, lora_r: int = 0,
-                 lora_alpha: float = 16.0, train_base: bool = True):
+                 lora_alpha: float = 16.0, train_base: bool = True, dx_image: bool = False):
         super().__init__()
         self.in_features = in_features
         self.splits = list(splits)
@@ -58,6 +59,13 @@ class FusedLinear(nn.Module):
             # B^T [pad, N] (zero rows past n*r): the k-contiguous operand of the
             # backward s dy B kernel (csrc/kernels/lora.hip), refreshed with wbuf
             self.register_buffer("wbt", torch.zeros(self.pad, N, dtype=dtype, device=device), persistent=False)
+            # optional [W; A]^T image [in, N + pad]: the input-gradient GEMM then runs in
+            # hipBLASLt's reduction-contiguous form (dx = dy_aug @ wxt^T) instead of the
+            # ~15-30 % slower NN form; frozen W part refreshed by refresh_images_(), the A^T
+            # columns by every adapter sync.  Costs one more copy of W (qkv/o only by default)
+            if dx_image and not train_base:
+                self.register_buffer("wxt", torch.zeros(in_features, N + self.pad, dtype=dtype, device=device),
+                                     persistent=False)
             self.weight = nn.Parameter(self.wbuf[:N, :in_features], requires_grad=train_base)
             # A: all splits' down-projections stacked; B: block-diagonal up-projection
             self.lora_a = nn.Parameter(torch.empty(n * lora_r, in_features, dtype=dtype, device=device))
@@ -82,8 +90,19 @@ class FusedLinear(nn.Module):
     def adapter_copies(self):
         """(src, dst) pairs: adapter parameters -> their slots in ``wbuf``."""
         N, K, R = sum(self.splits), self.in_features, self.lora_a.shape[0]
-        return [(self.lora_a.data, self.wbuf[N:N + R, :K]), (self.lora_b.data, self.wbuf[:N, K:K + R]),
-                (self.lora_b.data, self.wbt[:R, :N].t())]
+        out = [(self.lora_a.data, self.wbuf[N:N + R, :K]), (self.lora_b.data, self.wbuf[:N, K:K + R]),
+               (self.lora_b.data, self.wbt[:R, :N].t())]
+        if getattr(self, "wxt", None) is not None:
+            out.append((self.lora_a.data, self.wxt[:, N:N + R].t()))
+        return out
+
+    @torch.no_grad()
+    def refresh_images_(self):
+        """Rebuild the transposed [W; A] image after the frozen weight changed
+        (init, checkpoint load)."""
+        if getattr(self, "wxt", None) is not None and self.augmented():
+            K = self.in_features
+            self.wxt.copy_(ops.transpose2d(self.wbuf[:, :K]))
 
     @torch.no_grad()
     def sync_adapter_(self):
@@ -99,14 +118,22 @@ class FusedLinear(nn.Module):
             self.lora_b.zero_()
             if self.augmented():
                 self.sync_adapter_()
+                self.refresh_images_()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.lora_r > 0:
             if self.augmented():
                 return ops.lora_linear_aug(x, self.lora_a, self.lora_b, self.wbuf, self.splits, self.scaling,
-                                           self.pad, self.wbt)
+                                           self.pad, self.wbt, getattr(self, "wxt", None))
             return ops.lora_linear(x, self.weight, self.lora_a, self.lora_b, self.splits, self.scaling)
         return ops.linear(x, self.weight)
+
+
+# LoRA projections that keep a transposed [W; A] image for the input-gradient GEMM
+# (FusedLinear.wxt).  Default qkv + o: measured at the 70B shapes, dX 0.625 -> 0.427 ms
+# (qkv) and 0.395 -> 0.333 ms (o) for +24 GB of HBM; gate/up and down would need
+# +113 GB, which a 70B LoRA step (240 GB peak) cannot spare.
+DX_IMAGE = tuple(x for x in os.environ.get("MXLLM_DX_IMAGE", "qkv,o").split(",") if x)
 
 
 class LlamaLayer(nn.Module):
@@ -116,8 +143,8 @@ class LlamaLayer(nn.Module):
         h = cfg.hidden
         self.attn_norm = nn.Parameter(torch.ones(h, dtype=dtype, device=device), requires_grad=train_base)
         self.mlp_norm = nn.Parameter(torch.ones(h, dtype=dtype, device=device), requires_grad=train_base)
-        self.wqkv = FusedLinear(h, [cfg.q_dim, cfg.kv_dim, cfg.kv_dim], **kw)
-        self.wo = FusedLinear(cfg.q_dim, [h], **kw)
+        self.wqkv = FusedLinear(h, [cfg.q_dim, cfg.kv_dim, cfg.kv_dim], dx_image="qkv" in DX_IMAGE, **kw)
+        self.wo = FusedLinear(cfg.q_dim, [h], dx_image="o" in DX_IMAGE, **kw)
         self.wgu = FusedLinear(h, [cfg.ffn, cfg.ffn], **kw)
         self.wd = FusedLinear(cfg.ffn, [h], **kw)
 
@@ -244,6 +271,14 @@ class Llama(nn.Module):
             self._adapter_blocks = total
             self._adapter_desc_key = key
         ops.native().copy2d_batched(self._adapter_desc, self._adapter_blocks)
+
+    @torch.no_grad()
+    def refresh_images_(self) -> None:
+        """Rebuild derived weight images (transposed [W; A] of the LoRA
+        projections) after the frozen base weights were written."""
+        for m in self.modules():
+            if isinstance(m, FusedLinear):
+                m.refresh_images_()
 
     def set_sequence_parallel(self, group) -> None:
         """Shard sequences over ``group`` (Ulysses all-to-all around attention,

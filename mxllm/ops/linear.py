@@ -137,7 +137,7 @@ class _LoRAAugFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt):
+    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt, wxt=None):
         N, K = wbuf.shape[0] - pad, wbuf.shape[1] - pad
         x2 = x.reshape(-1, K)
         xa = _augment(x2, pad)
@@ -148,7 +148,7 @@ class _LoRAAugFn(torch.autograd.Function):
             xa[:, K:].addmm_(x2, wbuf[N:, :K].t(), beta=0.0, alpha=scaling)
         y = torch.mm(xa, wbuf[:N, :].t())
         ctx.save_for_backward(xa, wbuf)
-        ctx.lora_a, ctx.lora_b, ctx.wbt = a, b, wbt
+        ctx.lora_a, ctx.lora_b, ctx.wbt, ctx.wxt = a, b, wbt, wxt
         ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat)
         return y.view(*x.shape[:-1], N)
 
@@ -198,15 +198,20 @@ class _LoRAAugFn(torch.autograd.Function):
                     mark_ready(ctx.lora_b)
                 else:
                     db = tgt
-        dx = torch.mm(dya, wbuf[:, :K])
-        return dx.view(xshape), da, db, None, None, None, None, None, None
+        if ctx.wxt is not None:  # reduction-contiguous image of [W; A]: hipBLASLt "TN"
+            dx = torch.mm(dya, ctx.wxt.t())
+        else:
+            dx = torch.mm(dya, wbuf[:, :K])
+        return dx.view(xshape), da, db, None, None, None, None, None, None, None
 
 
 def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: torch.Tensor, splits: Sequence[int],
-                    scaling: float, pad: int, wbt: torch.Tensor | None = None) -> torch.Tensor:
-    """LoRA projection through the augmented weight buffer (see _LoRAAugFn)."""
+                    scaling: float, pad: int, wbt: torch.Tensor | None = None,
+                    wxt: torch.Tensor | None = None) -> torch.Tensor:
+    """LoRA projection through the augmented weight buffer (see _LoRAAugFn);
+    ``wxt``: optional [K, N+pad] transposed image of wbuf[:, :K] for dX."""
     r = a.shape[0] // len(splits)
-    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt)
+    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt)
 
 
 def transpose2d(t: torch.Tensor) -> torch.Tensor:

@@ -488,3 +488,5 @@ def merge_lora_(model) -> None:
             del mod.lora_b
             if hasattr(mod, "wbt"):
                 del mod.wbt
+            if hasattr(mod, "wxt"):
+                del mod.wxt

@@ -112,3 +112,5 @@ def load_model_weights(model, path: str) -> None:
                     named[k].copy_(v.to(named[k].device, named[k].dtype))
         if hasattr(model, "sync_adapters_"):
             model.sync_adapters_()
+        if hasattr(model, "refresh_images_"):
+            model.refresh_images_()

@@ -146,3 +146,37 @@ def test_fp8_weight_quantization_roundtrip():
     err = (dequantize_e4m3(q, s) - w).norm() / w.norm()
     assert err < 0.04, err
     assert (dequantize_e4m3(q, s)[3, :5].abs() <= s[3] * 2 ** -6 + 1e-12).all()
+
+
+def test_lora_dx_image_matches_augmented_buffer():
+    """FusedLinear's transposed [W; A] image (dX in the reduction-contiguous
+    GEMM form) gives the same input gradient as the augmented buffer, also
+    after an adapter update is synced."""
+    import torch
+
+    from mxllm.models.llama import FusedLinear
+
+    torch.manual_seed(0)
+    kw = dict(dtype=torch.float32, device="cpu", lora_r=4, lora_alpha=8.0, train_base=False)
+    a = FusedLinear(64, [32, 16, 16], dx_image=True, **kw)
+    b = FusedLinear(64, [32, 16, 16], dx_image=False, **kw)
+    gen = torch.Generator().manual_seed(1)
+    a.reset_parameters(0.02, gen)
+    b.load_state_dict(a.state_dict(), strict=False)
+    with torch.no_grad():
+        b.wbuf.copy_(a.wbuf)
+        for m in (a, b):
+            m.lora_b.normal_(0, 0.1, generator=torch.Generator().manual_seed(2))
+            m.sync_adapter_()
+    assert a.wxt is not None and not hasattr(b, "wxt")
+    for step in range(2):
+        x = torch.randn(8, 64, generator=torch.Generator().manual_seed(3 + step))
+        xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        dy = torch.randn(8, 64, generator=torch.Generator().manual_seed(9))
+        a(xa).backward(dy)
+        b(xb).backward(dy)
+        assert torch.allclose(xa.grad, xb.grad, atol=1e-5)
+        with torch.no_grad():  # adapter update, then the owner's sync
+            for m in (a, b):
+                m.lora_a.add_(0.05)
+                m.sync_adapter_()
