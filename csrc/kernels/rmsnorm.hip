@@ -23,6 +23,15 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
   const size_t base = (size_t)row * H;
   float v[ITERS][8];
   float ss = 0.f;
+  // gamma is loaded up front with the row, so its HBM latency overlaps the
+  // row's instead of following the reduction (small-T decode calls are
+  // latency-bound: one workgroup per row)
+  u16x8 gw[ITERS];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int c = (it * 256 + threadIdx.x) * 8;
+    if (c < H) gw[it] = *reinterpret_cast<const u16x8*>(w + c);
+  }
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
     const int c = (it * 256 + threadIdx.x) * 8;
@@ -56,7 +65,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(
   for (int it = 0; it < ITERS; ++it) {
     const int c = (it * 256 + threadIdx.x) * 8;
     if (c < H) {
-      u16x8 g = *reinterpret_cast<const u16x8*>(w + c);
+      const u16x8 g = gw[it];
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(v[it][j] * rs * bf2f(g[j]));
