@@ -144,6 +144,8 @@ def main(argv=None):
     tps = tokens_per_step * a.steps / elapsed if a.steps else 0.0
     ms = 1e3 * elapsed / max(1, a.steps)
     peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else 0.0
+    reserved_gb = torch.cuda.max_memory_reserved(dev) / 1e9 if dev.type == "cuda" else 0.0
+    total_gb = torch.cuda.mem_get_info(dev)[1] / 1e9 if dev.type == "cuda" else 0.0
     flops_tok = cfg.train_flops_per_token(a.seq_len, lora=(a.finetune == "lora"))
     mfu = tps * flops_tok / (env.world_size * 2.5e15) if dev.type == "cuda" else 0.0
     out = {
@@ -177,6 +179,8 @@ def main(argv=None):
         "model_tflops_per_gpu": round(tps * flops_tok / env.world_size / 1e12, 1),
         "mfu_vs_2.5PF_dense": round(mfu, 4),
         "peak_hbm_gb": round(peak_gb, 1),
+        "peak_hbm_reserved_gb": round(reserved_gb, 1),
+        "hbm_total_gb": round(total_gb, 1),
         "init_s": round(init_s, 1),
         "final_loss": round(loss_v, 4),
         "allreduce_mb_per_step": (round(trainer.ddp.bytes_per_step / 2 ** 20, 1)
