@@ -4,6 +4,7 @@ uses (row strides K+64 / N+64), and append them to the selection table.
 
   fwd: y  = x_aug[T, K+64] @ wbuf[:N, :]^T        (wbuf row stride K+64)
   bwd: dx = dy_aug[T, N+64] @ wbuf[:, :K]         (row stride K+64)
+  bwd_tn: dx = dy_aug @ wxt^T  (wxt = [W; A]^T image, qkv/o projections)
 
 The table is written after every shape, so a time limit loses at most one.
 """
@@ -41,7 +42,9 @@ def ops_for(N, K):
     xa = torch.randn(T, K + PAD, device="cuda", dtype=bf)
     dya = torch.randn(T, N + PAD, device="cuda", dtype=bf)
     wf, wb = wbuf[:N, :], wbuf[:, :K]
-    return {"fwd": lambda: torch.mm(xa, wf.t()), "bwd": lambda: torch.mm(dya, wb)}
+    wxt = wb.t().contiguous()  # FusedLinear.wxt: transposed [W; A] image (TN dX)
+    return {"fwd": lambda: torch.mm(xa, wf.t()), "bwd": lambda: torch.mm(dya, wb),
+            "bwd_tn": lambda: torch.mm(dya, wxt.t())}
 
 
 def main():

@@ -20,10 +20,11 @@ TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _ON = False
 
 
-def enable(path: str = TABLE) -> bool:
-    """Use the tuned GEMM table (read-only).  No-op without a GPU / table or
-    when MXLLM_GEMM_TUNING=0."""
+def enable(path: str | None = None) -> bool:
+    """Use the tuned GEMM table (read-only; ``MXLLM_GEMM_TABLE`` overrides the
+    path).  No-op without a GPU / table or when MXLLM_GEMM_TUNING=0."""
     global _ON
+    path = path or os.environ.get("MXLLM_GEMM_TABLE") or TABLE
     if _ON:
         return True
     if os.environ.get("MXLLM_GEMM_TUNING", "1") == "0" or not torch.cuda.is_available() or not os.path.exists(path):
