@@ -19,6 +19,8 @@
 //    bf16 = sign<<15 | ((e4m3 & 0x7F) << 4) + (120 << 7)   (exponent rebias 7 -> 127),
 //    two bytes at a time with 32-bit ALU ops (byte permute, and, shift-add, and-or);
 //  * the per-channel scale is applied once in the epilogue.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mx {
@@ -47,37 +49,50 @@ __device__ __forceinline__ u16x8 dequant8(uint32_t lo, uint32_t hi) {
 // MB: 16-token blocks (1 or 2); X rows >= M are clamped to M-1 and discarded.
 // NW waves per workgroup split K into NW contiguous parts (more loads in flight for
 // the projections with few output channels: o / down have only N/16 = 512 workgroups).
-template <int MB, int NW>
+// NC: 16-channel groups per wave (1 or 2).  Every workgroup reads its waves' K parts of
+// X once; with M distinct tokens that is M*2 bytes per k against 16*NC weight bytes, so
+// for 6..16 tokens NC = 2 halves the X traffic per streamed weight byte (the X
+// fragments of a chunk feed both channel groups' MFMAs).
+template <int MB, int NW, int NC>
 __global__ void __launch_bounds__(64 * NW) w8a16_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx,
                                                              const uint8_t* __restrict__ Q,
                                                              const float* __restrict__ scale, uint16_t* __restrict__ Y,
                                                              int64_t ldy, int M, int N, int K) {
-  __shared__ f32x4 red[NW][MB][64];
+  __shared__ f32x4 red[NW][NC][MB][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16;
+  const int n0 = blockIdx.x * 16 * NC;
   const int kq = K / NW;  // this wave's K part
-  const uint8_t* qrow = Q + (int64_t)(n0 + c) * K + (int64_t)w * kq + 16 * g;
+  const uint8_t* qrow[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) qrow[j] = Q + (int64_t)(n0 + 16 * j + c) * K + (int64_t)w * kq + 16 * g;
   const uint16_t* xr[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) xr[mb] = X + (int64_t)min(mb * 16 + c, M - 1) * ldx + (int64_t)w * kq + 16 * g;
 
-  f32x4 acc[MB];
+  f32x4 acc[NC][MB];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // one 64-k chunk: 16 fp8 weights and 2 x 8 activations per lane, two MFMA k-steps
-  auto step = [&](const u32x4& q, const u16x8 (&b)[MB][2]) {
-    const u16x8 a0 = dequant8(q[0], q[1]);  // k = 16g + 0..7   (MFMA step 0)
-    const u16x8 a1 = dequant8(q[2], q[3]);  // k = 16g + 8..15  (MFMA step 1)
+  for (int j = 0; j < NC; ++j)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      acc[mb] = mfma16_f8(a0, b[mb][0], acc[mb]);
-      acc[mb] = mfma16_f8(a1, b[mb][1], acc[mb]);
+    for (int mb = 0; mb < MB; ++mb) acc[j][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // one 64-k chunk: 16 fp8 weights per channel group and 2 x 8 activations per lane,
+  // two MFMA k-steps per (group, token block)
+  auto step = [&](const u32x4 (&q)[NC], const u16x8 (&b)[MB][2]) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const u16x8 a0 = dequant8(q[j][0], q[j][1]);  // k = 16g + 0..7   (MFMA step 0)
+      const u16x8 a1 = dequant8(q[j][2], q[j][3]);  // k = 16g + 8..15  (MFMA step 1)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        acc[j][mb] = mfma16_f8(a0, b[mb][0], acc[j][mb]);
+        acc[j][mb] = mfma16_f8(a1, b[mb][1], acc[j][mb]);
+      }
     }
   };
-  auto load = [&](int k, u32x4& q, u16x8 (&b)[MB][2]) {
-    q = *reinterpret_cast<const u32x4*>(qrow + k);
+  auto load = [&](int k, u32x4 (&q)[NC], u16x8 (&b)[MB][2]) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) q[j] = *reinterpret_cast<const u32x4*>(qrow[j] + k);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       b[mb][0] = *reinterpret_cast<const u16x8*>(xr[mb] + k);
@@ -85,12 +100,12 @@ __global__ void __launch_bounds__(64 * NW) w8a16_gemm_kernel(const uint16_t* __r
     }
   };
   // batches of UNR chunks: all of a batch's loads are issued before its first use, so
-  // UNR 16-B weight loads per lane are in flight (a plain loop waits on each one)
+  // UNR 16-B weight loads per lane and group are in flight (a plain loop waits on each)
   constexpr int UNR = 8;
   const int nit = kq / 64;
   int it = 0;
   for (; it + UNR <= nit; it += UNR) {
-    u32x4 q[UNR];
+    u32x4 q[UNR][NC];
     u16x8 b[UNR][MB][2];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) load((it + u) * 64, q[u], b[u]);
@@ -98,29 +113,34 @@ __global__ void __launch_bounds__(64 * NW) w8a16_gemm_kernel(const uint16_t* __r
     for (int u = 0; u < UNR; ++u) step(q[u], b[u]);
   }
   for (; it < nit; ++it) {
-    u32x4 q;
+    u32x4 q[NC];
     u16x8 b[MB][2];
     load(it * 64, q, b);
     step(q, b);
   }
-  // C[row = channel 4g + i][col = token c] per m-block: sum the NW K parts
+  // C[row = channel 4g + i][col = token c] per (group, m-block): sum the NW K parts
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) red[w][mb][lane] = acc[mb];
+  for (int j = 0; j < NC; ++j)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) red[w][j][mb][lane] = acc[j][mb];
   __syncthreads();
   if (w == 0) {
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      f32x4 s = red[0][mb][lane];
+    for (int j = 0; j < NC; ++j) {
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) s += red[ww][mb][lane];
-      const int m = mb * 16 + c;
-      if (m < M) {
-        const int n = n0 + 4 * g;
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + n);
-        u16x4 o;
+      for (int mb = 0; mb < MB; ++mb) {
+        f32x4 s = red[0][j][mb][lane];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = f2bf(s[i] * sc[i]);
-        *reinterpret_cast<u16x4*>(Y + (int64_t)m * ldy + n) = o;
+        for (int ww = 1; ww < NW; ++ww) s += red[ww][j][mb][lane];
+        const int m = mb * 16 + c;
+        if (m < M) {
+          const int n = n0 + 16 * j + 4 * g;
+          const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + n);
+          u16x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = f2bf(s[i] * sc[i]);
+          *reinterpret_cast<u16x4*>(Y + (int64_t)m * ldy + n) = o;
+        }
       }
     }
   }
@@ -171,9 +191,17 @@ extern "C" int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, c
                              int64_t ldy, int M, int N, int K, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 32 || N % 16 || K % 512 || ldx % 8 || ldy % 4 || ldx < K || ldy < N) return -1;
-  const int grid = N / 16;
-  if (M <= 16) w8a16_gemm_kernel<1, 8><<<grid, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
-  else w8a16_gemm_kernel<2, 8><<<grid, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
+  // two channel groups per wave for 6..16 tokens when that still leaves >= 256 workgroups
+  // (70B fp8 decode step, one group -> two: 22.0 -> 21.1 ms at 8 tokens, but 18.5 -> 19.3 ms
+  // at 4; profiles/r1g_fp8_decode_ab.md).  MXLLM_W8_NC=1 forces one group (A/B switch).
+  static const bool nc1 = [] {
+    const char* e = getenv("MXLLM_W8_NC");
+    return e && e[0] == '1';
+  }();
+  if (!nc1 && M >= 6 && M <= 16 && N % 32 == 0 && N / 32 >= 256)
+    w8a16_gemm_kernel<1, 8, 2><<<N / 32, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
+  else if (M <= 16) w8a16_gemm_kernel<1, 8, 1><<<N / 16, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
+  else w8a16_gemm_kernel<2, 8, 1><<<N / 16, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
   return (int)hipGetLastError();
 }
 

@@ -22,6 +22,8 @@ end).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -30,9 +32,10 @@ from ..ops._ext import native, use_native
 E4M3_MAX = 448.0
 # decode batches up to this many tokens use the weight-only HIP kernel (it streams the
 # fp8 weights once per call); above it the activations are quantised per token too and
-# hipBLASLt's fp8 MFMA GEMM runs.  Measured (70B decode step): the HIP kernel 16.6 ms at
-# 1 token and 18.7 ms at 4, hipBLASLt's fp8 GEMM 27.8 ms at 8 tokens but 21.7 ms at 32.
-SMALL_M = 16
+# hipBLASLt's fp8 MFMA GEMM runs.  Measured (70B decode step, profiles/r1g_fp8_decode_ab.md):
+# HIP kernel 16.4 / 18.5 / 21.1 / 24.6 ms at 1 / 4 / 8 / 12 tokens, hipBLASLt's fp8 GEMM
+# 27.7 ms at 8 but 24.0 ms at 12 and 21.7 ms at 32, so the crossover is near 10 tokens.
+SMALL_M = int(os.environ.get("MXLLM_W8_SMALL_M", "10"))
 
 
 def quantize_e4m3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:

@@ -307,6 +307,22 @@ def test_w8_linear(gpu, M, K):
     assert rel_err(_ops().w8_dequant(q, s), dequantize_e4m3(q, s)) < 5e-3
 
 
+@pytest.mark.parametrize("M", [1, 4, 8, 16])
+def test_w8_linear_wide(gpu, M):
+    """FP8-weight decode GEMM at a projection-sized N (>= 8192: the two-channel-group
+    variant for 6..16 tokens) vs an fp32 matmul with the reference-decoded weights."""
+    from mxllm.serve.quant import dequantize_e4m3, quantize_e4m3
+
+    torch.manual_seed(12)
+    N, K = 8192, 1536
+    w = torch.randn(N, K, device=gpu) * 0.02
+    q, s = quantize_e4m3(w)
+    x = torch.randn(M, K + 64, device=gpu, dtype=torch.bfloat16)[:, :K]
+    y = _ops().w8_linear(x, q, s)
+    yr = x.float() @ dequantize_e4m3(q, s).t()
+    assert y.shape == (M, N) and rel_err(y, yr) < 1e-2
+
+
 def test_quant_rows_e4m3(gpu):
     """Per-token activation quantisation kernel == torch's e4m3fn conversion of
     x / (amax / 448), and its decode reproduces x to e4m3 precision."""
