@@ -19,6 +19,17 @@ of the adapter gradients, grad-norm clip and fused AdamW.
 
 ``--finetune full`` (e.g. with ``--model llama3.1-8b``) trains every weight
 (bf16 params/grads, fp32 master + Adam moments) — BASELINE config 2/3.
+
+BASELINE config 4 (Llama-3.1-70B FULL-parameter fine-tune, sharded over 8
+GPUs): ``--finetune full --parallel zero3 --act-ckpt``.  When the headline run
+is on 8 GPUs (``--config4 auto``) it is ALSO measured after the headline steps,
+in a fresh 8-rank child job, and reported under ``config4_full_zero3`` in the
+same JSON line.  ``--emulate-world N`` runs ZeRO-3 in one process with world-N
+shard sizes (per-rank memory/compute proxy without link traffic).
+
+``--gpus N`` without a torchrun environment spawns the N ranks itself (child
+``torch.distributed.run``, rendezvous on 127.0.0.1); under torchrun a
+WORLD_SIZE different from N is an error (exit 1).
 """
 from __future__ import annotations
 
@@ -60,22 +71,164 @@ def parse(argv=None):
     ap.add_argument("--layers", type=int, default=None, help="override n_layers (NOT valid for the headline)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-gemm-table", action="store_true", help="ignore the tuned hipBLASLt solution table")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="zero3 only: one process holding world-N shard sizes (gathers tile the local shard)")
+    ap.add_argument("--config4", choices=["auto", "on", "off"], default="auto",
+                    help="also measure BASELINE config 4 (70B full fine-tune, ZeRO-3) after the headline; "
+                         "auto = when the headline runs on 8 GPUs")
+    ap.add_argument("--config4-micro-batch", type=int, default=4)
+    ap.add_argument("--config4-model", default="llama3.1-70b", help=argparse.SUPPRESS)  # tests: tiny models
+    ap.add_argument("--config4-steps", type=int, default=4)
+    ap.add_argument("--config4-warmup", type=int, default=2)
+    ap.add_argument("--config4-timeout", type=float, default=900.0)
     return ap.parse_args(argv)
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc: int, argv: list[str], script: str | None = None, timeout_s: float | None = None,
+                 env: dict | None = None) -> int:
+    """Run ``script argv`` as ``nproc`` torchrun ranks in a CHILD process group
+    (one rank per GPU, rendezvous on 127.0.0.1) and relay its stdout.
+
+    The parent never touches the GPU (``import torch`` does not initialise HIP)
+    and never re-execs itself: it waits for the child and returns its exit code.
+    Reference contract: /root/reference/scripts/run_node0.sh:10-16 (torchrun,
+    one process per device)."""
+    import signal
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script or os.path.abspath(__file__)]
+    p = subprocess.Popen(cmd + list(argv), stdout=subprocess.PIPE, text=True, start_new_session=True,
+                         env=env if env is not None else os.environ.copy())
+    t_end = None if timeout_s is None else time.time() + timeout_s
+    try:
+        for line in p.stdout:
+            print(line, end="", flush=True)
+            if t_end is not None and time.time() > t_end:
+                raise TimeoutError
+        return p.wait(timeout=None if t_end is None else max(1.0, t_end - time.time()))
+    except (KeyboardInterrupt, TimeoutError, subprocess.TimeoutExpired):
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+        return 124
+
+
+def check_world(gpus: int) -> str:
+    """'launch' (no torchrun env and N > 1: spawn N ranks), 'run' (env matches
+    or single process) or 'mismatch' (torchrun WORLD_SIZE != --gpus)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws in (None, ""):
+        return "launch" if gpus > 1 else "run"
+    return "run" if int(ws) == gpus else "mismatch"
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    mode = check_world(a.gpus)
+    if mode == "mismatch":
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks",
+              file=sys.stderr, flush=True)
+        return 1
+    if mode == "launch":
+        return launch_ranks(a.gpus, argv)
     if a.device == "cpu":
         os.environ["MXLLM_FORCE_CPU"] = "1"
-    from mxllm.models import Llama, get_config
     from mxllm.parallel import runtime
-    from mxllm.train.trainer import OptimConfig, Trainer
-    from mxllm.data import SyntheticTokens
 
     # the timed step issues no small collectives, so the bench keeps RCCL for its
     # two bookkeeping reductions (MXLLM_XGMI=1 opts into the peer-memory path)
     os.environ.setdefault("MXLLM_XGMI", "0")
     env = runtime.init()
+    out = run(a, env)
+    c4 = a.config4 == "on" or (a.config4 == "auto" and env.world_size == 8 and a.model == "llama3.1-70b"
+                               and a.finetune == "lora" and a.parallel == "ddp" and env.device.type == "cuda")
+    if not c4:
+        if env.is_main:
+            emit(out, a.json_out)
+        runtime.cleanup()
+        return 0
+    # BASELINE config 4 in a fresh job: this job's ranks free the GPUs (non-zero
+    # ranks exit; the launcher waits for rank 0), local rank 0 runs the child
+    runtime.cleanup()
+    import gc
+
+    gc.collect()
+    if env.device.type == "cuda":
+        torch.cuda.empty_cache()
+    if env.is_main:
+        out["config4_full_zero3"] = run_config4(a, env.world_size)
+        emit(out, a.json_out)
+    return 0
+
+
+def emit(out: dict, json_out: str | None):
+    line = json.dumps(out)
+    print(line, flush=True)
+    if json_out:
+        with open(json_out, "w") as f:
+            f.write(line + "\n")
+
+
+def run_config4(a, world: int) -> dict:
+    """70B full-parameter ZeRO-3 fine-tune (activation checkpointing) on ``world``
+    GPUs as a child torchrun job; returns its parsed JSON (or the error)."""
+    import tempfile
+
+    fd, path = tempfile.mkstemp(suffix=".json", prefix="mxllm_c4_")
+    os.close(fd)
+    argv = ["--gpus", str(world), "--model", a.config4_model, "--finetune", "full", "--parallel", "zero3",
+            "--act-ckpt", "--micro-batch", str(a.config4_micro_batch), "--seq-len", str(a.seq_len),
+            "--steps", str(a.config4_steps), "--warmup", str(a.config4_warmup), "--config4", "off",
+            "--json-out", path] + (["--device", a.device] if a.device else [])
+    keep = {k: v for k, v in os.environ.items()
+            if not (k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                          "ROLE_WORLD_SIZE", "ROLE_NAME", "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+                    or k.startswith("TORCHELASTIC_") or k.startswith("TORCH_ELASTIC"))}
+    t0 = time.time()
+    import contextlib
+    import io
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):  # the child's own JSON line must not become a second output line
+        rc = launch_ranks(world, argv, timeout_s=a.config4_timeout, env=keep)
+    res = {"error": f"child job exit code {rc}", "wall_s": round(time.time() - t0, 1)}
+    try:
+        with open(path) as f:
+            txt = f.read().strip()
+        if txt:
+            res = json.loads(txt)
+            res["wall_s"] = round(time.time() - t0, 1)
+    except (OSError, ValueError) as e:
+        res["error"] = f"{res.get('error')}; no result ({e})"
+    finally:
+        with contextlib.suppress(OSError):
+            os.remove(path)
+    res.pop("vs_baseline", None)
+    res["label"] = ("BASELINE config 4: Llama-3.1-70B FULL-parameter fine-tune, ZeRO-3 sharded over "
+                    f"{world} GPUs, activation checkpointing, measured after the headline in a separate job")
+    return res
+
+
+def run(a, env) -> dict:
+    """Build the trainer, run W warm-up + K timed steps, return the JSON dict."""
+    from mxllm.models import Llama, get_config
+    from mxllm.parallel import runtime
+    from mxllm.train.trainer import OptimConfig, Trainer
+    from mxllm.data import SyntheticTokens
+
     dev = env.device
     from mxllm.utils import gemm_tuning
 
@@ -87,12 +240,18 @@ def main(argv=None):
     lora_r = a.lora_r if a.finetune == "lora" else 0
     t0 = time.perf_counter()
     opt = OptimConfig(lr=1e-4, weight_decay=0.0, grad_clip=1.0)
+    emulated = 0
     if a.parallel == "zero3":
         if a.finetune != "full":
             raise SystemExit("--parallel zero3 requires --finetune full")
         from mxllm.parallel.zero3 import Zero3Trainer
 
-        trainer = Zero3Trainer(cfg, env, opt, seed=1234)
+        if a.emulate_world > 1:
+            if env.world_size > 1:
+                raise SystemExit("--emulate-world is a single-process proxy")
+            emulated = a.emulate_world
+        trainer = Zero3Trainer(cfg, env, opt, seed=1234, activation_checkpointing=a.act_ckpt,
+                               emulate_world=emulated)
         model = trainer.model
     else:
         model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
@@ -121,6 +280,7 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    loss = None
     for _ in range(a.warmup):
         loss = step()
     sync()
@@ -139,7 +299,8 @@ def main(argv=None):
 
         gpu_sample = sample_device(dev.index)  # clocks / power right after the timed steps
     elapsed = runtime.all_reduce_scalars([elapsed], op="max")[0]
-    loss_v = float(loss.float().item()) if a.steps or a.warmup else float("nan")
+    loss_v = float(loss.float().item()) if loss is not None else float("nan")
+    world = emulated or env.world_size  # emulation: tokens of ONE rank of that world
     tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size // a.sp
     tps = tokens_per_step * a.steps / elapsed if a.steps else 0.0
     ms = 1e3 * elapsed / max(1, a.steps)
@@ -148,6 +309,11 @@ def main(argv=None):
     total_gb = torch.cuda.mem_get_info(dev)[1] / 1e9 if dev.type == "cuda" else 0.0
     flops_tok = cfg.train_flops_per_token(a.seq_len, lora=(a.finetune == "lora"))
     mfu = tps * flops_tok / (env.world_size * 2.5e15) if dev.type == "cuda" else 0.0
+    if a.parallel == "zero3":
+        par = f"zero3-dp{world}" + (" (EMULATED on 1 GPU: world-%d shard sizes, no link traffic)" % world
+                                    if emulated else "")
+    else:
+        par = f"dp{env.world_size // a.sp}-sp{a.sp}" if a.sp > 1 else f"dp{env.world_size}"
     out = {
         "metric": METRIC,
         "value": round(tps, 2),
@@ -165,8 +331,7 @@ def main(argv=None):
             "model": PRETTY.get(cfg.name, cfg.name) + (f" ({cfg.n_layers} layers)" if a.layers else ""),
             "global_batch": a.micro_batch * a.grad_accum * env.world_size // a.sp,
             "seq_len": a.seq_len,
-            "parallelism": (f"zero3-dp{env.world_size}" if a.parallel == "zero3" else
-                            (f"dp{env.world_size // a.sp}-sp{a.sp}" if a.sp > 1 else f"dp{env.world_size}")),
+            "parallelism": par,
             "finetune": (f"lora r={lora_r} alpha={a.lora_alpha} on q,k,v,o,gate,up,down; frozen bf16 base"
                          if a.finetune == "lora" else "full (bf16 params+grads, fp32 master/Adam)"),
             "micro_batch": a.micro_batch,
@@ -192,14 +357,12 @@ def main(argv=None):
                                   if k in gpu_sample},
         "trainable_params": (cfg.n_params() if a.parallel == "zero3" else model.num_params(trainable_only=True)),
     }
-    if env.is_main:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
-    runtime.cleanup()
+    if emulated:
+        out["emulated_world"] = emulated
+        out["note"] = ("PROXY: one GPU holding one rank's world-%d shards; value/ms exclude all collective "
+                       "time and are per emulated rank" % emulated)
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

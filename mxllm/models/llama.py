@@ -167,6 +167,7 @@ class Llama(nn.Module):
         self.final_norm = nn.Parameter(torch.ones(cfg.hidden, dtype=dtype, device=device), requires_grad=train_base)
         if cfg.tie_embeddings:
             self.lm_head = None
+            self.tok_emb._mx_no_direct = True  # two uses (embedding + head): gradient via autograd
         else:
             self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, dtype=dtype, device=device),
                                         requires_grad=train_base)

@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..parallel.grad_ready import deliver_grad
 from ._ext import native, use_native
 
 
@@ -20,18 +21,28 @@ class _EmbeddingFn(torch.autograd.Function):
         ctx.save_for_backward(ids)
         ctx.vocab = weight.shape[0]
         ctx.wdtype = weight.dtype
-        return native().embedding_fwd(ids, weight)
+        ctx.wp = weight if weight.is_leaf else None  # for an owner-side gradient sink (ZeRO-3)
+        ctx.nat = use_native(weight)
+        return native().embedding_fwd(ids, weight) if ctx.nat else F.embedding(ids, weight)
 
     @staticmethod
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
         if not ctx.needs_input_grad[1]:
             return None, None
-        dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab)
-        return None, dw.to(ctx.wdtype)
+        if ctx.nat:
+            dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab).to(ctx.wdtype)
+        else:
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            dw = torch.zeros(ctx.vocab, dy2.shape[1], dtype=torch.float32, device=dy.device)
+            dw.index_add_(0, ids.reshape(-1), dy2.float())
+            dw = dw.to(ctx.wdtype)
+        if deliver_grad(ctx.wp, dw):
+            return None, None
+        return None, dw
 
 
 def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    if use_native(weight):
+    if use_native(weight) or getattr(weight, "_mx_grad_sink", None) is not None:
         return _EmbeddingFn.apply(ids.contiguous(), weight)
     return F.embedding(ids, weight)

@@ -227,9 +227,10 @@ def transpose2d(t: torch.Tensor) -> torch.Tensor:
 _DW_TN = os.environ.get("MXLLM_DW_TN", "1") != "0"
 
 
-def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
     """dW = dy^T x (reduction over the token dimension), accumulated into
-    ``out`` (beta = 1) when given.
+    ``out`` (``out = beta * out + dW``; beta 0 ignores whatever ``out`` held)
+    when given.
 
     Both activations are token-major, so the direct GEMM is hipBLASLt's
     reduction-strided "NT" kernel family (~0.93-1.15 PF on the Llama-3.1
@@ -243,10 +244,30 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor) ->
         dyt = transpose2d(dy)
         if out is None:
             return torch.mm(dyt, xt.t())
-        return out.addmm_(dyt, xt.t())
+        return out.addmm_(dyt, xt.t(), beta=beta)
     if out is None:
         return torch.mm(dy.t(), x)
-    return out.addmm_(dy.t(), x)
+    return out.addmm_(dy.t(), x, beta=beta)
+
+
+def param_weight_grad(wp: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor | None:
+    """Weight gradient of parameter ``wp`` for a backward pass.
+
+    When an owner pre-attached ``wp.grad`` (the trainer's flat grad buffer, or a
+    ZeRO-3 unit's gathered-gradient buffer) the dW GEMM writes straight into it —
+    accumulating (beta 1), or overwriting (beta 0) when the owner flagged the
+    buffer ``_mx_grad_fresh`` so it need not be zero-filled first — the owner is
+    notified via ``mark_ready`` and None is returned.  Otherwise the dW tensor
+    is returned for autograd to accumulate."""
+    g = direct_grad(wp) if wp is not None else None
+    if g is None:
+        return weight_grad_(None, dy, x)
+    fresh = getattr(wp, "_mx_grad_fresh", False)
+    weight_grad_(g, dy, x, beta=0.0 if fresh else 1.0)
+    if fresh:
+        wp._mx_grad_fresh = False
+    mark_ready(wp)
+    return None
 
 
 class _LinearFn(torch.autograd.Function):
@@ -259,6 +280,9 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.save_for_backward(x2, w)
+        # the Parameter itself (its .grad is the direct-accumulation target): under
+        # ZeRO-3 the saved ``w`` unpacks as a view of the re-gathered unit, not the leaf
+        ctx.wp = w if w.is_leaf else None
         ctx.xshape = x.shape
         return torch.mm(x2, w.t()).view(*x.shape[:-1], w.shape[0])
 
@@ -267,14 +291,7 @@ class _LinearFn(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
         dx = torch.mm(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = None
-        if ctx.needs_input_grad[1]:
-            g = direct_grad(w)
-            if g is not None:
-                weight_grad_(g, dy2, x2)
-                mark_ready(w)
-            else:
-                dw = weight_grad_(None, dy2, x2)
+        dw = param_weight_grad(ctx.wp, dy2, x2) if ctx.needs_input_grad[1] else None
         return dx, dw
 
 

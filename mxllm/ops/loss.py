@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._ext import native, use_native
-from .linear import weight_grad_
+from .linear import param_weight_grad
 
 
 class _LinearCEFn(torch.autograd.Function):
@@ -25,20 +25,25 @@ class _LinearCEFn(torch.autograd.Function):
         logits = torch.matmul(h, w.t())  # [T, V] bf16, hipBLASLt
         loss, _ = native().ce_fwd_bwd(logits, labels, ignore_index)  # logits <- dlogits
         ctx.save_for_backward(h, w, logits)
+        ctx.wp = w if w.is_leaf else None
         return loss
 
     @staticmethod
     def backward(ctx, gl):
+        # the upstream scalar gradient ``gl`` stays on device (no host read to
+        # test for 1.0): it scales dlogits once when the head's weight gradient
+        # is formed too (both GEMMs then read the scaled logits), else only the
+        # small [T, H] dh
         h, w, dlogits = ctx.saved_tensors
         dh = dw = None
+        if ctx.needs_input_grad[1]:
+            dlogits.mul_(gl.to(dlogits.dtype))
         if ctx.needs_input_grad[0]:
             dh = torch.matmul(dlogits, w)
-            if not (isinstance(gl, torch.Tensor) and gl.numel() == 1 and float(gl) == 1.0):
-                dh = dh * gl.to(dh.dtype)
+            if not ctx.needs_input_grad[1]:
+                dh.mul_(gl.to(dh.dtype))
         if ctx.needs_input_grad[1]:
-            dw = weight_grad_(None, dlogits, h)
-            if not (isinstance(gl, torch.Tensor) and gl.numel() == 1 and float(gl) == 1.0):
-                dw = dw * gl.to(dw.dtype)
+            dw = param_weight_grad(ctx.wp, dlogits, h)
         return dh, dw, None, None
 
 

@@ -11,8 +11,24 @@ def mark_ready(p) -> None:
 
 
 def direct_grad(p):
-    """The preallocated .grad of ``p`` if it can be accumulated into in place."""
+    """The preallocated .grad of ``p`` if it can be accumulated into in place
+    (never for a parameter used twice in the graph, e.g. a tied embedding/head:
+    its gradient is complete only after autograd summed both uses)."""
+    if getattr(p, "_mx_no_direct", False):
+        return None
     g = p.grad
     if g is not None and g.shape == p.shape and g.dtype == p.dtype and g.is_contiguous():
         return g
     return None
+
+
+def deliver_grad(p, g) -> bool:
+    """Hand a freshly computed full gradient ``g`` of ``p`` to its owner instead
+    of autograd (ZeRO-3 sets ``p._mx_grad_sink`` on parameters whose storage is
+    released between uses, where AccumulateGrad would need the full-shape
+    parameter).  True when the owner took it (return None to autograd then)."""
+    sink = getattr(p, "_mx_grad_sink", None) if p is not None else None
+    if sink is None:
+        return False
+    sink(p, g)
+    return True

@@ -1,7 +1,7 @@
 """ZeRO-3 / fully-sharded data parallel for full fine-tuning.
 
 Llama-3.1-70B full fine-tuning needs 16 B/param = 1,129 GB of state: it only
-fits an 8 x 288 GB MI355X node sharded.  Design:
+fits an 8 x 288 GB MI355X node sharded (141 GB of state per GPU).  Design:
 
   * units: the model is cut into flat parameter units — the embedding, each
     transformer layer's four projection matrices, the LM head — plus one small
@@ -12,16 +12,30 @@ fits an 8 x 288 GB MI355X node sharded.  Design:
     AdamW launch per step.
   * forward: a unit is all-gathered (``all_gather_into_tensor`` over RCCL /
     xGMI: each rank receives 7/8 of a 1.7 GB layer) just before use, with the
-    NEXT unit's gather already in flight (async), and released after use;
+    NEXT unit's gather already in flight, and released after use.
   * autograd never keeps a gathered weight alive: a ``saved_tensors_hooks``
     pair saves a (unit, offset, shape, stride) handle instead of any tensor
-    that lives in a gathered buffer, and re-gathers the unit on unpack during
-    backward (prefetching the unit below it);
-  * gradients: when the last parameter of a unit has accumulated its gradient
-    (post-accumulate-grad hooks), the unit's full gradient is reduce-scattered
-    into the rank's fp32 grad shard and the gathered weights are freed.
+    that lives in a gathered buffer.  An identity autograd node at every
+    unit's output (``_PreBackward``) runs first in backward: it re-gathers the
+    unit (waiting on the prefetch issued one unit earlier), prefetches the unit
+    below and attaches the unit's gradient buffer.
+  * gradients: the projection backward writes dW straight into a per-unit
+    flat bf16 gradient buffer (``param_weight_grad``, beta 0: no zero fill,
+    no concatenation copy).  When the unit's last gradient lands, the buffer is
+    reduce-scattered ASYNCHRONOUSLY on a second communicator (so gathers and
+    reduce-scatters of neighbouring units use both directions of the xGMI
+    links concurrently); at most ``max_inflight`` reduce-scatters are
+    outstanding, and each finished one is folded into the fp32 grad shard on
+    the compute stream (a dependency, never a host wait).
+  * activation checkpointing: a layer's forward runs under no_grad keeping
+    only its (x, h) inputs; its backward re-gathers the unit, recomputes the
+    layer and back-propagates through it (one gather serves both).
   * the model is built on the meta device and materialised unit by unit with
     a per-unit seed, so no rank ever holds the full 141 GB model.
+  * ``emulate_world=W`` (one process): the rank holds world-W shard sizes and
+    a gather tiles the local shard W times, a reduce-scatter sums the W
+    slices — the per-rank memory footprint and local traffic of a W-GPU run
+    without its link traffic (the 80-layer config-4 sizing proxy).
 Reference parity: none — the reference advertises 70B fine-tuning
 (README.md:1-3) with no training code.
 """
@@ -29,6 +43,8 @@ from __future__ import annotations
 
 import logging
 import math
+import os
+from collections import deque
 
 import torch
 import torch.distributed as dist
@@ -64,6 +80,8 @@ def _realize_on(model, device):
             model._meta_shapes[full] = tuple(p.shape)
             mod._parameters[pname] = nn.Parameter(torch.empty(0, dtype=torch.bfloat16, device=device))
     cfg = model.cfg
+    if cfg.tie_embeddings:
+        model.tok_emb._mx_no_direct = True
     cos, sin = ref.rope_tables(min(cfg.max_seq_len, 131072), cfg.head_dim, cfg.rope_theta, cfg.rope_scaling, device)
     model.rope_cos, model.rope_sin = cos, sin
 
@@ -117,9 +135,45 @@ def init_full_state(cfg, seed, device) -> dict:
     return out
 
 
+class Comm:
+    """The two collectives ZeRO-3 issues, over real ranks or emulated.
+
+    ``ag_pg`` carries the all-gathers and ``rs_pg`` the reduce-scatters: two
+    communicators = two RCCL streams, so a prefetch gather and the previous
+    unit's reduce-scatter run concurrently (xGMI links are full duplex).
+    ``emulate`` > 1: single process standing in for rank 0 of that many."""
+
+    def __init__(self, world: int, rank: int, ag_pg=None, rs_pg=None, emulate: int = 0):
+        self.world, self.rank, self.ag_pg, self.rs_pg = world, rank, ag_pg, rs_pg
+        self.emulate = emulate > 1
+
+    @property
+    def real(self) -> bool:
+        return self.world > 1 and not self.emulate
+
+    def all_gather(self, full: torch.Tensor, shard: torch.Tensor, async_op: bool):
+        if self.real:
+            return dist.all_gather_into_tensor(full, shard, group=self.ag_pg, async_op=async_op)
+        full.view(self.world, -1).copy_(shard.unsqueeze(0).expand(self.world, -1))
+        return None
+
+    def reduce_scatter(self, out: torch.Tensor, full: torch.Tensor, async_op: bool):
+        if self.real:
+            return dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.rs_pg, async_op=async_op)
+        if self.world == 1:
+            out.copy_(full)
+        else:
+            torch.sum(full.view(self.world, -1), dim=0, out=out)
+        return None
+
+    def all_reduce(self, t: torch.Tensor):
+        if self.real:
+            dist.all_reduce(t, group=self.rs_pg)
+
+
 class Unit:
-    def __init__(self, uid: int, named, world: int, rank: int, pg, resident: bool = False):
-        self.uid, self.world, self.rank, self.pg, self.resident = uid, world, rank, pg, resident
+    def __init__(self, uid: int, named, world: int, rank: int, comm: Comm, resident: bool = False):
+        self.uid, self.world, self.rank, self.comm, self.resident = uid, world, rank, comm, resident
         self.names = [e[0] for e in named]
         self.params = [e[1] for e in named]
         self.shapes = [tuple(e[2]) for e in named]
@@ -137,7 +191,10 @@ class Unit:
         self.work = None
         self.shard = None  # bf16 view (set by the trainer)
         self.grad_shard = None  # fp32 view
-        self.pending = 0
+        self.gbuf: torch.Tensor | None = None  # gathered-size bf16 gradient buffer (backward only)
+        self.seen: set[int] = set()
+        self.reduced = False  # this micro-batch's gradient already handed to the reduce-scatter
+        self.n_trainable = len(self.params)
         self.device = None
         self.dtype = None
 
@@ -146,16 +203,13 @@ class Unit:
         if self.full is not None:
             return
         self.full = torch.empty(self.full_numel, dtype=self.dtype, device=self.device)
-        if self.world > 1:
-            self.work = dist.all_gather_into_tensor(self.full, self.shard, group=self.pg, async_op=async_op)
-        else:
-            self.full.copy_(self.shard)
+        self.work = self.comm.all_gather(self.full, self.shard, async_op)
 
     def materialize(self):
         if self.full is None:
             self.gather(async_op=False)
         if self.work is not None:
-            self.work.wait()
+            self.work.wait()  # stream dependency on the RCCL stream, no host wait
             self.work = None
         for p, o, n, s in zip(self.params, self.offsets, self.numels, self.shapes):
             p.data = self.full[o:o + n].view(s)
@@ -171,49 +225,138 @@ class Unit:
         self.full = None
 
     # -------------------------------------------------------------- gradients
-    def reduce_grads(self, accumulate: bool):
-        parts = []
-        for p, n in zip(self.params, self.numels):
+    def attach_grads(self):
+        """Point every parameter's .grad at its slice of a fresh gathered-size
+        gradient buffer; the dW GEMMs overwrite it (``_mx_grad_fresh``), so only
+        the alignment pad is zeroed.  Parameters whose gradient comes from
+        autograd (embedding, tied weights) are copied in at reduce time."""
+        if self.gbuf is not None:
+            return
+        # GPU: every projection/head gradient comes from param_weight_grad, which
+        # honours the fresh flag; the CPU reference ops accumulate through autograd
+        fresh = ops.use_native(self.shard)
+        if fresh:
+            self.gbuf = torch.empty(self.full_numel, dtype=self.dtype, device=self.device)
+            if self.full_numel > self.numel:
+                self.gbuf[self.numel:].zero_()
+        else:
+            self.gbuf = torch.zeros(self.full_numel, dtype=self.dtype, device=self.device)
+        for p, o, n, s in zip(self.params, self.offsets, self.numels, self.shapes):
+            if getattr(p, "_mx_no_direct", False) or p.shape != s:
+                continue
+            p.grad = self.gbuf[o:o + n].view(s)
+            p._mx_grad_fresh = fresh
+
+    def reduce_async(self):
+        """Launch the reduce-scatter of the unit's gradient buffer; returns
+        (work | None, bf16 shard) to be folded into ``grad_shard`` later."""
+        if self.gbuf is None:
+            g0 = self.params[0].grad if len(self.params) == 1 else None
+            if (g0 is not None and g0.is_contiguous() and g0.numel() == self.full_numel
+                    and g0.dtype == self.dtype):
+                self.gbuf = g0.view(-1)  # autograd's own gradient tensor, no copy (e.g. the embedding)
+            else:
+                self.gbuf = torch.zeros(self.full_numel, dtype=self.dtype, device=self.device)
+        for p, o, n in zip(self.params, self.offsets, self.numels):
             g = p.grad
-            parts.append(g.reshape(-1).to(self.dtype) if g is not None else torch.zeros(n, dtype=self.dtype,
-                                                                                         device=self.device))
+            dst = self.gbuf[o:o + n]
+            if g is None:
+                if getattr(p, "_mx_grad_fresh", False):
+                    dst.zero_()  # attached but never written (parameter unused this step)
+            elif g.data_ptr() != dst.data_ptr():
+                dst.copy_(g.reshape(-1))
+            elif getattr(p, "_mx_grad_fresh", False):
+                dst.zero_()
             p.grad = None
-        pad = self.full_numel - self.numel
-        if pad:
-            parts.append(torch.zeros(pad, dtype=self.dtype, device=self.device))
-        gfull = torch.cat(parts)
+            p._mx_grad_fresh = False
         out = torch.empty(self.shard_numel, dtype=self.dtype, device=self.device)
-        if self.world > 1:
-            dist.reduce_scatter_tensor(out, gfull, op=dist.ReduceOp.SUM, group=self.pg)
-        else:
-            out.copy_(gfull)
-        if accumulate:
-            self.grad_shard.add_(out.float())
-        else:
-            self.grad_shard.copy_(out)
+        work = self.comm.reduce_scatter(out, self.gbuf, async_op=True)
+        self.gbuf = None  # RCCL keeps the buffer alive until the collective is done
+        self.seen.clear()
+        self.reduced = True
+        return work, out
+
+
+class _PreBackward(torch.autograd.Function):
+    """Identity on a unit's outputs whose backward runs before any of the unit's
+    own backward ops: re-gather the unit, prefetch the next one, attach grads."""
+
+    @staticmethod
+    def forward(ctx, trainer, uid, *xs):
+        ctx.trainer, ctx.uid = trainer, uid
+        out = tuple(x.view_as(x) for x in xs)
+        return out if len(out) > 1 else out[0]
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ctx.trainer._pre_backward(ctx.uid)
+        return (None, None) + gs
+
+
+class _CkptLayer(torch.autograd.Function):
+    """Activation-checkpointed transformer layer under ZeRO-3: forward keeps only
+    (x, h); backward re-gathers the unit, recomputes and back-propagates."""
+
+    @staticmethod
+    def forward(ctx, trainer, i, x, h):
+        ctx.trainer, ctx.i = trainer, i
+        ctx.save_for_backward(x, h)
+        with torch.no_grad():
+            xo, ho = trainer.model._layer(i, x, h, trainer._B, trainer._S)
+        ctx.BS = (trainer._B, trainer._S)
+        return xo, ho
+
+    @staticmethod
+    def backward(ctx, dxo, dho):
+        tr = ctx.trainer
+        x, h = ctx.saved_tensors
+        uid = tr._units_by_layer[ctx.i].uid
+        tr._pre_backward(uid)
+        xd = x.detach().requires_grad_(True)
+        hd = h.detach().requires_grad_(True)
+        with torch.enable_grad():
+            xo, ho = tr.model._layer(ctx.i, xd, hd, *ctx.BS)
+        outs, grads = [], []
+        for o, g in ((xo, dxo), (ho, dho)):
+            if g is not None and o.requires_grad:
+                outs.append(o)
+                grads.append(g)
+        torch.autograd.backward(outs, grads)
+        return None, None, xd.grad, hd.grad
 
 
 class Zero3Trainer:
     """Same ``train_step`` contract as :class:`mxllm.train.trainer.Trainer`."""
 
     def __init__(self, cfg, env: DistEnv, optim=None, *, seed: int = 0, activation_checkpointing: bool = False,
-                 process_group=None):
+                 process_group=None, emulate_world: int = 0, max_inflight: int | None = None):
         from ..models.llama import Llama
         from ..train.trainer import OptimConfig
 
-        if activation_checkpointing:
-            raise NotImplementedError("ZeRO-3 + activation checkpointing is not supported yet")
         self.env, self.opt = env, optim or OptimConfig()
+        self.act_ckpt = activation_checkpointing
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        if emulate_world and emulate_world > 1:
+            self.world, self.rank = emulate_world, 0
+            comm = Comm(self.world, 0, emulate=emulate_world)
+        else:
+            self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+            self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+            rs_pg = process_group
+            if self.world > 1 and os.environ.get("MXLLM_Z3_SPLIT_COMMS", "1") != "0":
+                ranks = dist.get_process_group_ranks(process_group) if process_group is not None else None
+                rs_pg = dist.new_group(ranks=ranks)  # second communicator: reduce-scatters on their own stream
+            comm = Comm(self.world, self.rank, process_group, rs_pg)
+        self.comm = comm
+        self.emulated = comm.emulate
+        self.max_inflight = max_inflight or int(os.environ.get("MXLLM_Z3_INFLIGHT", "2"))
         dev = env.device
         self.device = dev
         model = Llama(cfg, device="meta", init=False)
         _realize_on(model, dev)
         self.model = model
         units = unit_layout(model)
-        self.units = [Unit(k, ps, self.world, self.rank, self.pg, res) for k, (_, ps, res) in enumerate(units)]
+        self.units = [Unit(k, ps, self.world, self.rank, comm, res) for k, (_, ps, res) in enumerate(units)]
         self.unit_names = [u[0] for u in units]
         for u in self.units:
             u.device, u.dtype = dev, torch.bfloat16
@@ -238,15 +381,23 @@ class Zero3Trainer:
                 p.requires_grad_(True)
                 self._param_unit[id(p)] = u
                 p.register_post_accumulate_grad_hook(self._grad_hook)
-                if not u.resident:  # gradient about to be accumulated: the unit must be materialised
-                    p.register_hook(self._make_pre_grad_hook(u))
-        self._accumulate = False
+                p._mx_on_grad_ready = self._grad_hook  # dW written by the GEMM itself (param_weight_grad)
+                if not u.resident and len(u.params) == 1 and not getattr(p, "_mx_no_direct", False):
+                    p._mx_grad_sink = self._sink  # e.g. the embedding: its unit is not gathered in backward
+        self._inflight: deque = deque()
         self.step_num = 0
         self.last_grad_norm = None
         self._units_by_layer = {i: self.units[2 + i] for i in range(len(model.layers))}
         self._head = self.units[-1] if model.lm_head is not None else self.units[1]
+        self._below = {}  # unit -> the unit whose backward follows it (prefetch target)
+        order = [self._head] + [self._units_by_layer[i] for i in reversed(range(len(model.layers)))]
+        for a, b in zip(order, order[1:]):
+            if a is not b:
+                self._below[a.uid] = b
+        self._B = self._S = 0
         model._zero3 = self
-        log.info("ZeRO-3: %d units, %.2f M params/rank (world %d)", len(self.units), total / 1e6, self.world)
+        log.info("ZeRO-3: %d units, %.2f M params/rank (world %d%s, act-ckpt %s)", len(self.units), total / 1e6,
+                 self.world, " emulated" if self.emulated else "", self.act_ckpt)
 
     # ---------------------------------------------------------------- init
     @torch.no_grad()
@@ -260,20 +411,52 @@ class Zero3Trainer:
         self.units[0].materialize()  # norms stay resident
 
     # ---------------------------------------------------------------- hooks
-    def _make_pre_grad_hook(self, u):
-        def hook(g):
-            if u.full is None:
-                self._gather(u, async_op=False)
-            u.materialize()
-            return g
-        return hook
-
     def _grad_hook(self, p):
         u = self._param_unit[id(p)]
-        u.pending -= 1
-        if u.pending == 0 and not u.resident:
-            u.reduce_grads(self._accumulate)
-            self._done(u)
+        if u.resident or u.reduced or id(p) in u.seen:
+            return
+        u.seen.add(id(p))
+        if len(u.seen) == u.n_trainable:
+            self._reduce(u)
+
+    def _sink(self, p, g):
+        """A full gradient delivered by its op (grad_ready.deliver_grad)."""
+        u = self._param_unit[id(p)]
+        if u.gbuf is None and g.is_contiguous() and g.numel() == u.full_numel:
+            u.gbuf = g.view(-1)
+        else:
+            if u.gbuf is None:
+                u.gbuf = torch.zeros(u.full_numel, dtype=u.dtype, device=u.device)
+            k = u.params.index(p)
+            u.gbuf[u.offsets[k]:u.offsets[k] + u.numels[k]].copy_(g.reshape(-1))
+        self._grad_hook(p)
+
+    def _reduce(self, u: Unit):
+        work, out = u.reduce_async()
+        self._inflight.append((u, work, out))
+        self._done(u)
+        while len(self._inflight) > self.max_inflight:
+            self._drain_one()
+
+    def _drain_one(self):
+        u, work, out = self._inflight.popleft()
+        if work is not None:
+            work.wait()  # the compute stream waits for the RCCL stream; the host does not
+        u.grad_shard.add_(out)  # fp32 += bf16 (AdamW zeroes the shard every step)
+
+    def _drain(self):
+        while self._inflight:
+            self._drain_one()
+
+    def _pre_backward(self, uid: int):
+        u = self.units[uid]
+        if u.full is None:
+            self._gather(u)
+        nxt = self._below.get(uid)
+        if nxt is not None and nxt.full is None:
+            self._gather(nxt)
+        u.materialize()
+        u.attach_grads()
 
     def _pack(self, t):
         if t.device.type == "meta" or not isinstance(t, torch.Tensor):
@@ -291,9 +474,8 @@ class Zero3Trainer:
         if isinstance(obj, tuple) and len(obj) == 5 and obj[0] == "mxz3":
             _, uid, off, shape, stride = obj
             u = self.units[uid]
-            if u.full is None:
+            if u.full is None:  # _PreBackward normally gathered it already
                 self._gather(u)
-                self._prefetch_below(u)
             u.materialize()
             return torch.as_strided(u.full, shape, stride, off)
         return obj
@@ -301,12 +483,6 @@ class Zero3Trainer:
     def _gather(self, u: Unit, async_op=True):
         u.gather(async_op=async_op)
         self._by_storage[u.full.untyped_storage().data_ptr()] = u
-
-    def _prefetch_below(self, u: Unit):
-        if 2 < u.uid < len(self.units):
-            nxt = self.units[u.uid - 1]
-            if nxt.full is None:
-                self._gather(nxt)
 
     def _use(self, u: Unit, prefetch: Unit | None = None):
         if u.full is None:
@@ -316,6 +492,8 @@ class Zero3Trainer:
         u.materialize()
 
     def _done(self, u: Unit):
+        if u.resident:
+            return
         if u.full is not None:
             self._by_storage.pop(u.full.untyped_storage().data_ptr(), None)
         u.release()
@@ -325,49 +503,57 @@ class Zero3Trainer:
         m = self.model
         cfg = m.cfg
         B, S = ids.shape
+        self._B, self._S = B, S
         for u in self.units:
-            u.pending = sum(1 for p in u.params if p.requires_grad)
+            u.seen.clear()
+            u.reduced = False
         with torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack):
             emb = self.units[1]
             self._use(emb, self._units_by_layer.get(0))
             h = ops.embedding(ids.reshape(-1), m.tok_emb)
-            if not self._head is emb:
+            if self._head is not emb:
                 self._done(emb)
             x = ops.rms_norm(h, m.layers[0].attn_norm, cfg.norm_eps)
             for i in range(len(m.layers)):
                 u = self._units_by_layer[i]
                 nxt = self._units_by_layer.get(i + 1, self._head)
                 self._use(u, nxt)
-                x, h = m._layer(i, x, h, B, S)
+                if self.act_ckpt:
+                    x, h = _CkptLayer.apply(self, i, x, h)
+                else:
+                    x, h = m._layer(i, x, h, B, S)
+                    x, h = _PreBackward.apply(self, u.uid, x, h)
                 self._done(u)
             self._use(self._head)
             loss = ops.linear_cross_entropy(x, m.head_weight, labels.reshape(-1))
+            loss = _PreBackward.apply(self, self._head.uid, loss)
             self._done(self._head)
         return loss
 
     def train_step(self, micro_batches):
         n = len(micro_batches)
         total = None
-        for i, (ids, labels) in enumerate(micro_batches):
-            self._accumulate = i > 0
+        for ids, labels in micro_batches:
             loss = self._forward(ids, labels)
-            (loss / n if n > 1 else loss).backward()
+            loss.backward()  # 1/n folded into the optimizer's grad scale
+            for u in self.units[1:]:  # units whose hooks did not all fire (unused params)
+                if not u.reduced and (u.seen or any(p.grad is not None for p in u.params)):
+                    self._reduce(u)
+                elif u.full is not None:
+                    self._done(u)
             total = loss.detach() if total is None else total + loss.detach()
-        # resident unit (norms): all-reduce-scatter its grads now
-        norms = self.units[0]
-        norms.reduce_grads(accumulate=False)
-        for u in self.units[1:]:  # any unit whose hooks did not all fire (unused params)
-            if any(p.grad is not None for p in u.params):
-                u.reduce_grads(accumulate=True)
-            if u.full is not None:
-                self._done(u)
+        self._drain()
+        norms = self.units[0]  # resident unit: one (small) reduce-scatter per step
+        work, out = norms.reduce_async()
+        if work is not None:
+            work.wait()
+        norms.grad_shard.add_(out)
         scale = 1.0 / (self.world * n)
         self.step_num += 1
         o = self.opt
         if o.grad_clip and o.grad_clip > 0:
             sq = ops.sq_norm(self.grads)
-            if self.world > 1:
-                dist.all_reduce(sq, group=self.pg)
+            self.comm.all_reduce(sq)
             gnorm = sq.sqrt() * scale
             self.last_grad_norm = gnorm
             gscale = torch.clamp(o.grad_clip / (gnorm + 1e-6), max=1.0) * scale
@@ -398,6 +584,20 @@ class Zero3Trainer:
         self.v.copy_(sd["v"])
         self.shard_params.copy_(self.master)
         self._refresh_resident()
+
+    def full_master_state(self) -> dict:
+        """Every fp32 master weight, gathered unit by unit (collective: all ranks
+        call it; tests / export)."""
+        out = {}
+        for u in self.units:
+            full = torch.empty(u.full_numel, dtype=torch.float32, device=self.device)
+            if self.comm.real:
+                dist.all_gather_into_tensor(full, u.master_view.contiguous(), group=self.pg)
+            else:
+                full.view(self.world, -1).copy_(u.master_view.unsqueeze(0).expand(self.world, -1))
+            for name, o, n, shp in zip(u.names, u.offsets, u.numels, u.shapes):
+                out[name] = full[o:o + n].view(shp).clone()
+        return out
 
     def full_state_dict(self) -> dict:
         """Gather every unit (one at a time) into named CPU tensors (rank 0 keeps them)."""

@@ -1,0 +1,69 @@
+"""bench.py launch contract on CPU (gloo):
+
+* ``--gpus N`` without a torchrun environment spawns N ranks itself and
+  reports ``n_gpus: N`` (one JSON line on stdout);
+* under torchrun, WORLD_SIZE != --gpus exits 1 before touching any device;
+* the config-4 phase (ZeRO-3 full fine-tune in a fresh child job) is reported
+  inside the SAME JSON line;
+* the ZeRO-3 world-N emulation proxy is labelled as such.
+Reference launch contract: /root/reference/scripts/run_node0.sh:10-16.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, env=None, timeout=400):
+    e = dict(os.environ if env is None else env)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        if env is None:
+            e.pop(k, None)
+    return subprocess.run([sys.executable, "bench.py", "--device", "cpu", "--model", "tiny", "--steps", "2",
+                           "--warmup", "1", "--seq-len", "64", *args], cwd=ROOT, env=e, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def _json_lines(stdout):
+    return [json.loads(x) for x in stdout.splitlines() if x.startswith("{")]
+
+
+def test_self_launch_two_ranks():
+    r = _bench("--gpus", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["value"] > 0
+    assert j["config"]["global_batch"] == 4
+
+
+def test_world_size_mismatch_exits_1():
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    r = _bench("--gpus", "2", env=env, timeout=120)
+    assert r.returncode == 1
+    assert "WORLD_SIZE=4" in r.stderr
+    assert not _json_lines(r.stdout)
+
+
+def test_config4_phase_in_same_line():
+    r = _bench("--gpus", "2", "--config4", "on", "--config4-model", "tiny", "--config4-steps", "1",
+               "--config4-warmup", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    c4 = j["config4_full_zero3"]
+    assert "error" not in c4, c4
+    assert c4["config"]["parallelism"] == "zero3-dp2" and c4["config"]["activation_checkpointing"]
+    assert c4["n_gpus"] == 2 and c4["value"] > 0 and "config 4" in c4["label"]
+    assert j["config"]["parallelism"] == "dp2"  # the headline itself is unchanged
+
+
+def test_zero3_emulation_is_labelled():
+    r = _bench("--finetune", "full", "--parallel", "zero3", "--act-ckpt", "--emulate-world", "4")
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _json_lines(r.stdout)[0]
+    assert j["emulated_world"] == 4 and "EMULATED" in j["config"]["parallelism"] and "PROXY" in j["note"]

@@ -197,27 +197,50 @@ def test_bench_contract_tiny(gpu, tmp_path):
 
 
 def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
-    """Rehearse the multi-rank bench path (DDP hooks, bucketed all-reduce of GPU
-    grads, barrier, max-over-ranks timing) with 2 ranks sharing the one GPU of
-    the test box over gloo (RCCL needs one GPU per rank)."""
+    """Rehearse the multi-rank bench path (self-launch of N ranks by
+    ``bench.py --gpus 2``, DDP hooks, bucketed all-reduce of GPU grads, barrier,
+    max-over-ranks timing) with 2 ranks sharing the one GPU of the test box over
+    gloo (RCCL needs one GPU per rank)."""
     import json
-    import socket
     import subprocess
     import sys
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = tmp_path / "b2.json"
     env = dict(os.environ, MXLLM_BACKEND="gloo")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-                        "--model", "tiny-d128", "--steps", "2", "--warmup", "1", "--seq-len", "256",
-                        "--json-out", str(out)], cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--model", "tiny-d128", "--steps", "2",
+                        "--warmup", "1", "--seq-len", "256", "--json-out", str(out)], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(out.read_text())
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["value"] > 0
+
+
+def test_zero3_emulated_world8_tiny_gpu(gpu):
+    """ZeRO-3 with activation checkpointing and the world-8 emulation on the GPU
+    (HIP kernels, direct dW into the unit gradient buffer, async reduce path)."""
+    from mxllm.models import get_config
+    from mxllm.parallel.runtime import DistEnv
+    from mxllm.parallel.zero3 import Zero3Trainer
+    from mxllm.train.trainer import OptimConfig
+
+    cfg = get_config("tiny-d128").replace(n_layers=3, vocab_size=1024)
+    env = DistEnv(device=gpu, backend="nccl")
+    ids = torch.randint(0, cfg.vocab_size, (2, 128), device=gpu)
+    losses = {}
+    for ck in (False, True):
+        tr = Zero3Trainer(cfg, env, OptimConfig(lr=1e-3), seed=3, activation_checkpointing=ck)
+        losses[ck] = [float(tr.train_step([(ids, ids)])) for _ in range(3)]
+    assert losses[True][-1] < losses[True][0]
+    for a, b in zip(losses[False], losses[True]):
+        assert abs(a - b) < 1e-3 * max(1.0, abs(a)), losses
+    tr8 = Zero3Trainer(cfg, env, OptimConfig(lr=1e-3), seed=3, activation_checkpointing=True, emulate_world=8)
+    assert tr8.master.numel() * 8 == sum(u.full_numel for u in tr8.units)
+    for _ in range(2):
+        loss = tr8.train_step([(ids, ids)])
+    assert torch.isfinite(loss).all()
 
 
 def test_gpu_monitor_samples(gpu):
