@@ -56,8 +56,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama3.1-70b")
     ap.add_argument("--finetune", choices=["lora", "full"], default="lora")
-    ap.add_argument("--parallel", choices=["ddp", "zero3"], default="ddp",
-                    help="zero3 = sharded params/grads/optimizer (full fine-tuning of 70B on 8 GPUs)")
+    ap.add_argument("--parallel", choices=["ddp", "zero1", "zero3"], default="ddp",
+                    help="zero1 = DDP with a sharded optimizer (reduce-scatter / all-gather); "
+                         "zero3 = sharded params/grads/optimizer (full fine-tuning of 70B on 8 GPUs)")
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--lora-alpha", type=float, default=32.0)
     ap.add_argument("--micro-batch", type=int, default=2)
@@ -256,11 +257,11 @@ def run(a, env) -> dict:
     else:
         model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
                       activation_checkpointing=a.act_ckpt)
-        trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb)
+        trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb, shard_optimizer=a.parallel == "zero1")
     sp_group, data_rank = None, env.rank
     if a.sp > 1:
-        if a.parallel != "ddp":
-            raise SystemExit("--sp is supported with --parallel ddp")
+        if a.parallel == "zero3":
+            raise SystemExit("--sp is supported with --parallel ddp / zero1")
         from mxllm.parallel.sequence import new_groups, shard_sequence
 
         sp_group, data_rank, _ = new_groups(a.sp)
@@ -314,6 +315,8 @@ def run(a, env) -> dict:
                                     if emulated else "")
     else:
         par = f"dp{env.world_size // a.sp}-sp{a.sp}" if a.sp > 1 else f"dp{env.world_size}"
+        if a.parallel == "zero1":
+            par += "-zero1" if getattr(trainer, "zero1", None) is not None else " (zero1 requested: world 1 = ddp)"
     out = {
         "metric": METRIC,
         "value": round(tps, 2),
@@ -349,9 +352,9 @@ def run(a, env) -> dict:
         "init_s": round(init_s, 1),
         "final_loss": round(loss_v, 4),
         "allreduce_mb_per_step": (round(trainer.ddp.bytes_per_step / 2 ** 20, 1)
-                                  if a.parallel == "ddp" and trainer.ddp.enabled else 0.0),
+                                  if a.parallel != "zero3" and trainer.ddp.enabled else 0.0),
         "exposed_comm_ms_last_step": (round(trainer.ddp.exposed_comm_ms(), 3)
-                                      if a.parallel == "ddp" and trainer.ddp.enabled and a.steps
+                                      if a.parallel != "zero3" and trainer.ddp.enabled and a.steps
                                       and trainer.ddp.exposed_comm_ms() is not None else None),
         "gpu_after_timed_steps": {k: gpu_sample[k] for k in ("gfx_clock_mhz", "socket_power_w", "temp_hotspot_c")
                                   if k in gpu_sample},

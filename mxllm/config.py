@@ -52,7 +52,7 @@ class RunConfig:
     # fine-tuning
     model: str = "tiny"
     finetune: str = "lora"  # lora | full
-    parallel: str = "ddp"  # ddp | zero3
+    parallel: str = "ddp"  # ddp | zero1 (sharded optimizer) | zero3 (sharded everything)
     sequence_parallel: int = 1  # Ulysses SP degree (ranks per sequence); world = dp x sp
     lora_r: int = 16
     lora_alpha: float = 32.0

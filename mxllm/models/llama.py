@@ -159,6 +159,9 @@ class Llama(nn.Module):
         train_base = not self.lora
         self.activation_checkpointing = activation_checkpointing
         self.seq_parallel = None  # UlyssesAttention when the sequence is sharded (set_sequence_parallel)
+        # optional ``fn(params)`` called before the parameters are first used in a forward (ZeRO-1: wait for
+        # their all-gather; mxllm/parallel/zero1.py) — None = parameters are always resident
+        self.param_wait = None
         self.tok_emb = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden, dtype=dtype, device=device),
                                     requires_grad=train_base)
         self.layers = nn.ModuleList([
@@ -222,19 +225,40 @@ class Llama(nn.Module):
                                 grad_pad=self._pad(layer.wd))
         return x, h
 
+    def _wait_groups(self):
+        """Parameter groups in first-use order: embedding (+ first norm), layer i
+        (+ the next layer's attn_norm it applies), head (+ final norm)."""
+        if getattr(self, "_wgroups", None) is None:
+            L = len(self.layers)
+            g = [[self.tok_emb] + ([self.layers[0].attn_norm] if L else [])]
+            for i, layer in enumerate(self.layers):
+                nxt = self.final_norm if i + 1 == L else self.layers[i + 1].attn_norm
+                g.append(list(layer.parameters()) + [nxt])
+            g.append([self.final_norm] + ([self.lm_head] if self.lm_head is not None else []))
+            self._wgroups = g
+        return self._wgroups
+
     def hidden_states(self, ids: torch.Tensor) -> torch.Tensor:
         """ids [B, S] -> final normed hidden [B*S, H]."""
         B, S = ids.shape
+        wait = self.param_wait
+        groups = self._wait_groups() if wait is not None else None
+        if wait is not None:
+            wait(groups[0])
         h = ops.embedding(ids.reshape(-1), self.tok_emb)
         x = (ops.rms_norm(h, self.layers[0].attn_norm, self.cfg.norm_eps, out_pad=self._pad(self.layers[0].wqkv))
              if len(self.layers) else h)
         for i in range(len(self.layers)):
+            if wait is not None:
+                wait(groups[i + 1])
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 x, h = ckpt.checkpoint(self._layer, i, x, h, B, S, use_reentrant=False)
             else:
                 x, h = self._layer(i, x, h, B, S)
         if not len(self.layers):
             x = ops.rms_norm(h, self.final_norm, self.cfg.norm_eps)
+        if wait is not None:
+            wait(groups[-1])
         return x
 
     def forward(self, ids: torch.Tensor, labels: torch.Tensor | None = None, ignore_index: int = -100):

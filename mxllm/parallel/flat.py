@@ -38,7 +38,7 @@ class FlatParams:
     """
 
     def __init__(self, named_params: list[tuple[str, torch.nn.Parameter]], grad_dtype: torch.dtype | None = None,
-                 reverse: bool = True):
+                 reverse: bool = True, align: int = ALIGN):
         if not named_params:
             raise ValueError("no trainable parameters")
         order = list(reversed(named_params)) if reverse else list(named_params)
@@ -50,7 +50,7 @@ class FlatParams:
         off = 0
         for n, p in order:
             self.slots.append(Slot(n, off, p.numel(), tuple(p.shape)))
-            off += _round(p.numel())
+            off += _round(p.numel(), align)
         self.numel = off
         self.device = dev
         self.param_dtype = pdt

@@ -45,18 +45,34 @@ class OptimConfig:
 
 class Trainer:
     def __init__(self, model: torch.nn.Module, env: DistEnv, optim: OptimConfig | None = None, *,
-                 bucket_mb: float = 128.0, first_bucket_mb: float = 16.0, broadcast_init: bool = False):
+                 bucket_mb: float = 128.0, first_bucket_mb: float = 16.0, broadcast_init: bool = False,
+                 shard_optimizer: bool = False):
+        """``shard_optimizer``: ZeRO-1 (mxllm/parallel/zero1.py) — gradients are
+        reduce-scattered, each rank updates its 1/N slice, parameters are
+        all-gathered back.  At world 1 it is plain DDP (nothing to shard)."""
         self.model = model
         self.env = env
         self.opt = optim or OptimConfig()
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
-        self.flat = FlatParams(named)
-        self.ddp = DDP(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
+        world = env.world_size
+        self.zero1 = None
+        if shard_optimizer and world > 1:
+            from ..parallel.zero1 import Zero1
+
+            self.flat = FlatParams(named, align=64 * world)
+            self.ddp = self.zero1 = Zero1(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
+            self._master = self.zero1.master
+            if getattr(model, "param_wait", "absent") is None:
+                model.param_wait = self.zero1.wait_params  # per-layer wait in the next forward
+        else:
+            self.flat = FlatParams(named)
+            self.ddp = DDP(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
+            self._master = self.flat.master
         if broadcast_init:
             self.ddp.broadcast_params(0)
         self._sync_adapters()
-        self.m = torch.zeros_like(self.flat.master)
-        self.v = torch.zeros_like(self.flat.master)
+        self.m = torch.zeros_like(self._master)
+        self.v = torch.zeros_like(self._master)
         self.step_num = 0
         self.last_grad_norm: torch.Tensor | None = None
 
@@ -69,6 +85,8 @@ class Trainer:
         Returns the mean loss as a device tensor (no host sync)."""
         n = len(micro_batches)
         self.model.train()
+        if self.zero1 is not None and getattr(self.model, "param_wait", None) is None:
+            self.zero1.wait_params()  # model without per-layer waits: all parameters first
         total = None
         for i, (ids, labels) in enumerate(micro_batches):
             last = i == n - 1
@@ -89,19 +107,34 @@ class Trainer:
 
     def _optimizer_step(self, scale: float):
         o = self.opt
+        z = self.zero1
+        grads = z.gshard if z is not None else self.flat.grads
         if o.grad_clip and o.grad_clip > 0:
             # global grad norm on device; the clip coefficient is applied inside
             # the fused AdamW kernel via grad_scale (host read only for logging)
-            sq = ops.sq_norm(self.flat.grads)
+            sq = ops.sq_norm(grads)
+            if z is not None:
+                from ..parallel.runtime import all_reduce_small_
+
+                all_reduce_small_(sq)  # sum of the shards' squares
             gnorm = sq.sqrt() * scale
             self.last_grad_norm = gnorm
             coef = torch.clamp(o.grad_clip / (gnorm + 1e-6), max=1.0)
             gscale = coef * scale
         else:
             gscale = scale
-        ops.adamw_step_(self.flat.master, self.flat.grads, self.m, self.v, self.lowp, lr=o.lr_at(self.step_num),
-                        beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
-                        step=self.step_num, grad_scale=gscale, zero_grad=True)  # grads cleared in the same pass
+        if z is not None:
+            lowp = None if z.master is z.pshard else z.pshard
+            ops.adamw_step_(z.master, grads, self.m, self.v, lowp, lr=o.lr_at(self.step_num), beta1=o.beta1,
+                            beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay, step=self.step_num,
+                            grad_scale=gscale, zero_grad=True)
+            z.gather_params()  # async, forward order; the next forward waits per layer
+            if getattr(self.model, "sync_adapters_", None) is not None and getattr(self.model, "lora", False):
+                z.wait_params()
+        else:
+            ops.adamw_step_(self.flat.master, grads, self.m, self.v, self.lowp, lr=o.lr_at(self.step_num),
+                            beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
+                            step=self.step_num, grad_scale=gscale, zero_grad=True)  # grads cleared in the same pass
         self._sync_adapters()
         self.flat.attach_grads()
 
@@ -112,16 +145,27 @@ class Trainer:
             fn()
 
     # ------------------------------------------------------------------ state
+    @property
+    def sharded_state(self) -> bool:
+        """True when each rank's optimizer state differs (ZeRO-1): save every rank."""
+        return self.zero1 is not None
+
     def state_dict(self) -> dict:
-        return {"step": self.step_num, "master": self.flat.master, "m": self.m, "v": self.v,
+        return {"step": self.step_num, "master": self._master, "m": self.m, "v": self.v,
                 "layout": self.flat.state_dict()}
 
     def load_state_dict(self, sd: dict):
         self.step_num = int(sd["step"])
-        self.flat.master.copy_(sd["master"])
+        self._master.copy_(sd["master"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
-        if self.flat.master is not self.flat.params:
+        z = self.zero1
+        if z is not None:
+            if z.master is not z.pshard:
+                z.pshard.copy_(z.master)
+            z.gather_params()
+            z.wait_params()
+        elif self.flat.master is not self.flat.params:
             self.flat.params.copy_(self.flat.master)
         self._sync_adapters()
 

@@ -63,7 +63,7 @@ def build_trainer(run, env):
         return Zero3Trainer(cfg, env, opt, seed=run.seed, activation_checkpointing=run.activation_checkpointing)
     model = Llama(cfg, device=env.device, lora_r=lora_r, lora_alpha=run.lora_alpha, seed=run.seed,
                   activation_checkpointing=run.activation_checkpointing)
-    return Trainer(model, env, opt, bucket_mb=run.bucket_mb)
+    return Trainer(model, env, opt, bucket_mb=run.bucket_mb, shard_optimizer=run.parallel == "zero1")
 
 
 def main(argv=None):
@@ -84,8 +84,8 @@ def main(argv=None):
         trainer = build_trainer(run, env)
         sp_group, data_rank, data_world = None, rank, world_size
         if run.sequence_parallel > 1:
-            if run.parallel != "ddp":
-                raise ValueError("--sequence-parallel is supported with --parallel ddp")
+            if run.parallel not in ("ddp", "zero1"):
+                raise ValueError("--sequence-parallel is supported with --parallel ddp / zero1")
             from mxllm.parallel.sequence import new_groups, shard_sequence
 
             sp_group, data_rank, data_world = new_groups(run.sequence_parallel)
@@ -104,7 +104,7 @@ def main(argv=None):
                 loader.restore(extra["loader"])
                 start = trainer.step_num
                 logging.info(f"Resumed at step {start}")
-        sync_check = run.check_sync_every >= 0 and run.parallel == "ddp"
+        sync_check = run.check_sync_every >= 0 and run.parallel in ("ddp", "zero1")
         if sync_check:
             from mxllm.parallel.consistency import check_in_sync
 
@@ -152,7 +152,7 @@ def main(argv=None):
                 check_in_sync(trainer.flat.params, what=f"trainable parameters after step {step}")
             if run.ckpt_dir and run.save_every and (step + 1) % run.save_every == 0:
                 checkpoint.save(run.ckpt_dir, trainer, step + 1, extra={"loader": loader.state()},
-                                sharded=run.parallel == "zero3")
+                                sharded=run.parallel in ("zero3", "zero1"))
         loader.close()
         if monitor is not None:
             monitor.stop()
