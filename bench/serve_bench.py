@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--e2e-prompt-len", type=int, default=256)
     ap.add_argument("--fp8", action="store_true", help="e4m3 projection weights (serving quantisation)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--top-p", type=float, default=1.0, help="e2e requests: nucleus sampling (with --temperature)")
+    ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--tp-shard-proxy", type=int, default=0,
                     help="one GPU: run rank 0's TP-N shard without the collectives (per-GPU compute floor)")
     a = ap.parse_args()
@@ -135,6 +137,19 @@ def main():
                               "tokens_per_s": round(bs / dt, 1),
                               "weight_stream_tb_s": round(wbytes / dt / 1e12, 2),
                               "hbm_tb_s_weights_plus_kv": round((wbytes + kv_bytes) / dt / 1e12, 2)})
+        if bs == bmax:  # decode step + batched sampling + token read-back: greedy vs T 0.8 / top-p 0.9
+            from mxllm.ops import decode as dops
+
+            for mode, (tt, tp_) in (("greedy", (0.0, 1.0)), ("t0.8_top_p0.9", (0.8, 0.9))):
+                for s in slots:
+                    eng.lens[s] = a.ctx
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for i in range(a.decode_steps):
+                    lg = eng.decode(slots, tok)
+                    dops.sample_rows(lg[:bs], [tt] * bs, [tp_] * bs, [0] * bs, list(range(bs)), [i] * bs).tolist()
+                dt2 = (time.perf_counter() - t) / a.decode_steps
+                out.setdefault("decode_plus_sampling", {})[mode] = {"batch": bs, "ms_per_step": round(1e3 * dt2, 3)}
         for s in slots:
             eng.lens[s] = 0
 
@@ -146,11 +161,12 @@ def main():
         f0, ttft0, n0 = eng2.finished, eng2.ttft_sum, eng2.tokens_generated
         torch.cuda.synchronize()
         t = time.perf_counter()
-        outs = eng2.generate(prompts, max_new_tokens=a.new_tokens)
+        outs = eng2.generate(prompts, max_new_tokens=a.new_tokens, temperature=a.temperature, top_p=a.top_p)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
         ntok = sum(len(o) for o in outs)
         out["e2e"] = {"requests": a.requests, "prompt_len": a.e2e_prompt_len, "new_tokens": a.new_tokens,
+                      "temperature": a.temperature, "top_p": a.top_p,
                       "max_batch": eng2.max_batch, "wall_s": round(dt, 3),
                       "output_tokens_per_s": round(ntok / dt, 1),
                       "total_tokens_per_s": round((ntok + a.requests * a.e2e_prompt_len) / dt, 1),

@@ -1,7 +1,8 @@
 """Inference ops: prefill attention into a KV cache, decode attention, sampling.
 
-GPU: csrc/kernels/decode.hip (rope_append, split-K decode attention, Gumbel-max
-sampler) and attn_fwd.hip for prefill.  CPU: reference implementations.
+GPU: csrc/kernels/decode.hip (rope_append, split-K decode attention, greedy /
+Gumbel-max sampler), sampling.hip (batched top-k / top-p / temperature) and
+attn_fwd.hip for prefill.  CPU: reference implementations.
 """
 from __future__ import annotations
 
@@ -66,29 +67,61 @@ def decode_attention(qkv: torch.Tensor, cos, sin, k_cache, v_cache, pos: torch.T
 
 def sample(logits: torch.Tensor, temperature: float = 0.0, seed: int = 0, step: int = 0,
            top_p: float = 1.0, top_k: int = 0) -> torch.Tensor:
-    """logits [B, V] -> token ids [B] int64.  Greedy when temperature <= 0.
-    Temperature sampling is exact (Gumbel-max) in one pass on GPU; top-k /
-    top-p first mask the logits (torch sort) then sample the same way."""
-    if top_k > 0 or top_p < 1.0:
-        logits = _mask_top(logits.float(), top_k, top_p)
+    """logits [B, V] -> token ids [B] int64, every row with the same parameters
+    (see ``sample_rows``)."""
+    B = logits.shape[0]
+    return sample_rows(logits, [temperature] * B, [top_p] * B, [top_k] * B, [seed] * B, [step] * B)
+
+
+def sample_rows(logits: torch.Tensor, temps, top_ps, top_ks, seeds, steps) -> torch.Tensor:
+    """Batched sampling with per-row parameters (OpenAI semantics): softmax of
+    logits / T, keep the top_k most likely (k <= 0: all), then the smallest
+    most-likely prefix whose mass reaches top_p, renormalise, draw; T <= 0 is
+    greedy.  GPU: ONE launch for the whole batch (csrc/kernels/sampling.hip:
+    radix-select thresholds + Gumbel-max over the kept set, keyed by
+    (seed, step, token) so a request's draws do not depend on batching).
+    CPU: ``filter_probs`` + torch.multinomial."""
+    B = logits.shape[0]
     if use_native(logits):
-        return native().sample(logits.contiguous(), float(temperature), int(seed), int(step))
-    if temperature <= 0:
-        return logits.float().argmax(-1)
-    g = torch.Generator(device=logits.device)
-    g.manual_seed(seed * 1000003 + step)
-    probs = torch.softmax(logits.float() / temperature, -1)
-    return torch.multinomial(probs, 1, generator=g).view(-1)
+        ops = native()
+        x = logits if logits.dtype in (torch.bfloat16, torch.float32) else logits.float()
+        x = x.contiguous()
+        if all(t <= 0 for t in temps):
+            return ops.sample(x, 0.0, 0, 0)  # batched greedy: one argmax pass
+        dev = logits.device
+        prm = torch.tensor([[float(t), float(p), float(k)] for t, p, k in zip(temps, top_ps, top_ks)],
+                           dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
+        st = torch.tensor([[int(sd), int(sp)] for sd, sp in zip(seeds, steps)], dtype=torch.int64).pin_memory()
+        st = st.to(dev, non_blocking=True)
+        return ops.sample_rows(x, prm[:, 0].contiguous(), prm[:, 1].contiguous(), prm[:, 2].int().contiguous(),
+                               st[:, 0].contiguous(), st[:, 1].int().contiguous())
+    out = torch.empty(B, dtype=torch.long)
+    for i in range(B):
+        if temps[i] <= 0:
+            out[i] = logits[i].float().argmax()
+            continue
+        g = torch.Generator(device=logits.device)
+        g.manual_seed(int(seeds[i]) * 1000003 + int(steps[i]))
+        pr = filter_probs(logits[i], temps[i], top_ks[i], top_ps[i])
+        out[i] = torch.multinomial(pr, 1, generator=g)[0]
+    return out.to(logits.device)
 
 
-def _mask_top(logits: torch.Tensor, top_k: int, top_p: float) -> torch.Tensor:
-    if top_k > 0:
-        kth = torch.topk(logits, min(top_k, logits.shape[-1]), -1).values[..., -1:]
-        logits = logits.masked_fill(logits < kth, float("-inf"))
+def filter_probs(row: torch.Tensor, temperature: float, top_k: int = 0, top_p: float = 1.0) -> torch.Tensor:
+    """fp32 reference of the sampling distribution of one logits row: softmax(row / T)
+    restricted to the top_k most likely tokens, then to the smallest most-likely
+    prefix reaching top_p of that mass (the crossing token kept), renormalised.
+    Ties at a boundary are kept (the GPU kernel's threshold semantics)."""
+    x = row.float() / max(float(temperature), 1e-20)
+    keep = torch.ones_like(x, dtype=torch.bool)
+    if 0 < top_k < x.numel():
+        kth = torch.topk(x, top_k).values[-1]
+        keep &= x >= kth
+    p = torch.softmax(x.masked_fill(~keep, float("-inf")), -1)
     if top_p < 1.0:
-        srt, idx = torch.sort(logits, -1, descending=True)
-        cp = torch.softmax(srt, -1).cumsum(-1)
-        drop = cp - torch.softmax(srt, -1) > top_p
-        srt = srt.masked_fill(drop, float("-inf"))
-        logits = torch.full_like(logits, float("-inf")).scatter(-1, idx, srt)
-    return logits
+        srt, idx = torch.sort(p, descending=True)
+        before = srt.cumsum(0) - srt  # mass strictly above each token
+        cut = srt[(before < top_p * srt.sum()).nonzero().max()]  # smallest kept probability
+        keep &= p >= cut
+        p = torch.softmax(x.masked_fill(~keep, float("-inf")), -1)
+    return p

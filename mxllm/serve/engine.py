@@ -386,11 +386,9 @@ class Engine:
             try:
                 t0 = time.perf_counter()
                 logits = self.prefill_batch([r.slot for r in grp], [r.prompt for r in grp])
-                toks = []
-                for i, r in enumerate(grp):
+                for r in grp:
                     self.active[r.slot] = r
-                    toks.append(int(dops.sample(logits[i:i + 1], r.params.temperature, r.params.seed, 0,
-                                                r.params.top_p, r.params.top_k)[0]))
+                toks = self._sample(logits, grp, first=True)
                 self.prefill_s += time.perf_counter() - t0
                 for r, tok in zip(grp, toks):
                     self.prefill_tokens += len(r.prompt)
@@ -409,16 +407,22 @@ class Engine:
         tokens = torch.tensor([r.output[-1] for r in reqs], dtype=torch.long)
         logits = self.decode(slots, tokens)
         self.steps += 1
-        if all(r.params.temperature <= 0 and r.params.top_p >= 1.0 and r.params.top_k == 0 for r in reqs):
-            nxt = dops.sample(logits, 0.0).tolist()  # batched greedy
-        else:  # per-request RNG stream: (seed, token index) -> reproducible regardless of batching
-            nxt = [int(dops.sample(logits[i:i + 1], r.params.temperature, r.params.seed, len(r.output),
-                                   r.params.top_p, r.params.top_k)[0]) for i, r in enumerate(reqs)]
+        nxt = self._sample(logits, reqs)
         self.decode_s += time.perf_counter() - t0  # includes the sampling read-back (a sync)
         self.decode_tokens += len(reqs)
         for r, t in zip(reqs, nxt):
             self._accept(r, int(t))
         return True
+
+    @staticmethod
+    def _sample(logits: torch.Tensor, reqs, first: bool = False) -> list[int]:
+        """One batched draw for every row of ``logits`` with each request's own
+        temperature / top-k / top-p; per-request RNG stream keyed by (seed, token
+        index), so draws do not depend on batching.  One host read-back."""
+        ps = [r.params for r in reqs]
+        steps = [0 if first else len(r.output) for r in reqs]
+        return dops.sample_rows(logits[:len(reqs)], [p.temperature for p in ps], [p.top_p for p in ps],
+                                [p.top_k for p in ps], [p.seed for p in ps], steps).tolist()
 
     def generate(self, prompts: list[list[int]], max_new_tokens: int = 32, temperature: float = 0.0,
                  top_p: float = 1.0, top_k: int = 0, stop_ids=(), seed: int = 0) -> list[list[int]]:
