@@ -157,6 +157,25 @@ def test_two_node_emulation_finetune():
     assert "step 2" in p0.stdout + p0.stderr
 
 
+@pytest.mark.parametrize("parallel", ["zero3", "zero1"])
+def test_two_node_emulation_sharded(parallel):
+    """BASELINE config 5 with sharding (CPU rehearsal): two torchrun agents x 2
+    ranks each = world 4 across two 'nodes', full fine-tune with ZeRO-3 (sharded
+    params/grads/optimizer, activation checkpointing) or ZeRO-1."""
+    port = _port()
+    env = _env(NPROC_PER_NODE=2, NNODES=2, MASTER_PORT=port, MASTER_ADDR="127.0.0.1")
+    args = ["--steps", "3", "--seq-len", "32", "--micro-batch", "1", "--log-every", "1", "--finetune", "full",
+            "--parallel", parallel] + (["--activation-checkpointing", "1"] if parallel == "zero3" else [])
+    p1 = subprocess.Popen(["bash", "scripts/run_node1.sh"] + args, cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                          stderr=subprocess.STDOUT, text=True)
+    p0 = subprocess.run(["bash", "scripts/run_node0.sh"] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                        timeout=300)
+    out1, _ = p1.communicate(timeout=120)
+    log = p0.stdout + p0.stderr
+    assert p0.returncode == 0 and p1.returncode == 0, log[-2000:] + out1[-2000:]
+    assert "step 2" in log
+
+
 def test_fault_injection_fails_fast():
     """A rank that dies mid-run must take the job down (non-zero exit), not hang."""
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
