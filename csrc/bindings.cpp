@@ -492,7 +492,8 @@ at::Tensor sample_rows(const at::Tensor& logits, const at::Tensor& temps, const 
 // ---------------------------------------------------------------- fp8 weights (serving)
 // y[M, N] = x[M, K] . (scale[:, None] * q[N, K])^T ; q: e4m3 codes (uint8), scale f32 [N].
 // M <= 32: the fused weight-streaming kernel; otherwise dequantise to bf16 and run the
-// hipBLASLt GEMM (mxllm/serve/quant.py routes large calls to the fp8 x fp8 GEMM instead).
+// hipBLASLt GEMM.  mxllm/serve/quant.py calls this only up to SMALL_M (8) tokens and
+// routes larger calls to the fp8 x fp8 hipBLASLt GEMM.
 at::Tensor w8_linear(const at::Tensor& x, const at::Tensor& q, const at::Tensor& scale) {
   MX_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "x: bf16 [M, K] rows");
   MX_CHECK(q.is_cuda() && q.scalar_type() == at::kByte && q.dim() == 2 && q.is_contiguous(), "q: uint8 [N, K]");

@@ -194,6 +194,9 @@ extern "C" int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, c
   // two channel groups per wave for 6..16 tokens when that still leaves >= 256 workgroups
   // (70B fp8 decode step, one group -> two: 22.0 -> 21.1 ms at 8 tokens, but 18.5 -> 19.3 ms
   // at 4; profiles/r1g_fp8_decode_ab.md).  MXLLM_W8_NC=1 forces one group (A/B switch).
+  // Effective routing: mxllm/serve/quant.py sends calls of more than SMALL_M (8) tokens to
+  // hipBLASLt's fp8 GEMM, so from Python the two-group variant runs at 6..8 tokens; 9..16
+  // reach it only through a direct w8_linear call (or MXLLM_W8_SMALL_M=16).
   static const bool nc1 = [] {
     const char* e = getenv("MXLLM_W8_NC");
     return e && e[0] == '1';

@@ -30,12 +30,16 @@ import torch.nn as nn
 from ..ops._ext import native, use_native
 
 E4M3_MAX = 448.0
-# decode batches up to this many tokens use the weight-only HIP kernel (it streams the
-# fp8 weights once per call); above it the activations are quantised per token too and
-# hipBLASLt's fp8 MFMA GEMM runs.  Measured (70B decode step, profiles/r1g_fp8_decode_ab.md):
-# HIP kernel 16.4 / 18.5 / 21.1 / 24.6 ms at 1 / 4 / 8 / 12 tokens, hipBLASLt's fp8 GEMM
-# 27.7 ms at 8 but 24.0 ms at 12 and 21.7 ms at 32, so the crossover is near 10 tokens.
-SMALL_M = int(os.environ.get("MXLLM_W8_SMALL_M", "10"))
+# Calls of up to SMALL_M tokens use the weight-only HIP kernel (bf16 activations, the fp8
+# weights streamed once per call); larger calls quantise the activations per token too
+# and run hipBLASLt's fp8 MFMA GEMM (W8A8).  The threshold is aligned to the graphed
+# decode's power-of-two batch buckets (mxllm/serve/engine.py), which is where it was
+# measured (70B decode step, profiles/r1g_fp8_decode_ab.md): the 8-row bucket 21.1 ms on
+# the HIP kernel vs 27.7 ms on hipBLASLt, the 16-row bucket (9..16 live sequences; the
+# profile's "12 tokens" row also ran 16-row GEMMs) 25.2 vs 24.6 ms.  Eager calls with 9..15
+# rows were not measured separately.  Decode accuracy of both routings at the 16-row
+# bucket: tests/test_model_gpu.py::test_engine_fp8_graphed_decode_b16_close_to_bf16.
+SMALL_M = int(os.environ.get("MXLLM_W8_SMALL_M", "8"))
 
 
 def quantize_e4m3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
@@ -72,16 +76,19 @@ class W8Linear(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x2 = x.reshape(-1, self.in_features)
+        if x2.stride(1) != 1 or x2.stride(0) % 8:
+            x2 = x2.contiguous()  # the HIP kernels take 16-B-aligned rows
         M = x2.shape[0]
         if not use_native(x2):
             y = torch.matmul(x2, dequantize_e4m3(self.q, self.scale).to(x2.dtype).t())
-        elif M <= SMALL_M:
+        elif M <= SMALL_M or self.in_features % 16:
             # weight-streaming HIP kernel: bf16 activations, weights dequantised in registers
-            y = native().w8_linear(x2 if x2.stride(1) == 1 else x2.contiguous(), self.q, self.scale)
+            # (it falls back to dequantise + hipBLASLt for shapes it does not take)
+            y = native().w8_linear(x2, self.q, self.scale)
         else:
             # larger batches / prefill: fp8 x fp8 MFMA GEMM (hipBLASLt), per-token activation
             # scales and the per-channel weight scales applied by the GEMM epilogue
-            xq, sa = native().quant_rows_e4m3(x2 if x2.stride(1) == 1 else x2.contiguous())  # one HIP pass
+            xq, sa = native().quant_rows_e4m3(x2)  # one HIP pass
             y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), self.q.view(torch.float8_e4m3fn).t(), scale_a=sa,
                                  scale_b=self.scale.view(1, -1), out_dtype=x2.dtype)
         return y.view(*x.shape[:-1], self.out_features)

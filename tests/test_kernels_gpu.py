@@ -307,14 +307,17 @@ def test_w8_linear(gpu, M, K):
     assert rel_err(_ops().w8_dequant(q, s), dequantize_e4m3(q, s)) < 5e-3
 
 
-@pytest.mark.parametrize("M", [1, 4, 8, 16])
-def test_w8_linear_wide(gpu, M):
+@pytest.mark.parametrize("M,K", [(1, 1536), (4, 1536), (8, 1536), (16, 1536), (8, 8192), (16, 8192),
+                                 (8, 4608)])
+def test_w8_linear_wide(gpu, M, K):
     """FP8-weight decode GEMM at a projection-sized N (>= 8192: the two-channel-group
-    variant for 6..16 tokens) vs an fp32 matmul with the reference-decoded weights."""
+    variant for 6..16 tokens) vs an fp32 matmul with the reference-decoded weights.
+    K = 8192 / 4608 give every wave enough k-chunks for the unrolled batch loop
+    (and, at 4608, a remainder for its tail loop)."""
     from mxllm.serve.quant import dequantize_e4m3, quantize_e4m3
 
     torch.manual_seed(12)
-    N, K = 8192, 1536
+    N = 8192
     w = torch.randn(N, K, device=gpu) * 0.02
     q, s = quantize_e4m3(w)
     x = torch.randn(M, K + 64, device=gpu, dtype=torch.bfloat16)[:, :K]

@@ -320,6 +320,35 @@ def test_engine_fp8_weights_close_to_bf16(gpu):
     assert _rel(lin(x), yr) < 3e-2
 
 
+@pytest.mark.parametrize("small_m", [8, 16])
+def test_engine_fp8_graphed_decode_b16_close_to_bf16(gpu, small_m, monkeypatch):
+    """Graphed decode of 16 sequences (the 16-row bucket): per-row logits of the fp8
+    engine vs the bf16 engine, both with the default routing (SMALL_M = 8: the
+    16-row calls quantise activations per token, W8A8 on hipBLASLt) and with the
+    weight-only kernel forced (SMALL_M = 16: W8A16)."""
+    from mxllm.models import Llama, get_config
+    from mxllm.serve import quant
+    from mxllm.serve.engine import Engine
+
+    monkeypatch.setattr(quant, "SMALL_M", small_m)
+    cfg = get_config("tiny-d128").replace(n_layers=4)
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(3, cfg.vocab_size, (20 + i,), generator=g).tolist() for i in range(16)]
+    tok = torch.randint(3, cfg.vocab_size, (16,), generator=g)
+    logits = {}
+    for kind in ("bf16", "fp8"):
+        m = Llama(cfg, device=gpu, seed=21).eval()
+        if kind == "fp8":
+            quant.quantize_model_fp8_(m)
+        eng = Engine(m, max_batch=16, max_seq=128)
+        assert eng.use_graphs
+        for i, p in enumerate(prompts):
+            eng.prefill(i, p)
+        logits[kind] = eng.decode(list(range(16)), tok)[:16].float()
+    cos = torch.nn.functional.cosine_similarity(logits["fp8"], logits["bf16"], dim=1)
+    assert cos.min().item() > 0.99, cos
+
+
 def _tp_gpu_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MXLLM_BACKEND="gloo", LOCAL_RANK=str(rank))
     import torch.distributed as dist
