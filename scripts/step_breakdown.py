@@ -1,0 +1,30 @@
+"""Per-step kernel time breakdown from a rocprofv3 kernel trace: the window
+between the last two fused-AdamW launches (one per optimizer step) -> one step.
+usage: python scripts/step_breakdown.py <run_kernel_trace.csv> [top]"""
+import collections
+import csv
+import sys
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+    a, b = marks[-2], marks[-1]
+    win = rows[a + 1:b + 1]
+    t0, t1 = int(win[0]["Start_Timestamp"]), int(win[-1]["End_Timestamp"])
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in win:
+        n = r["Kernel_Name"]
+        key = n.split("(")[0][:90]
+        agg[key][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        agg[key][1] += 1
+    busy = sum(v[0] for v in agg.values())
+    print(f"step window {1e-6 * (t1 - t0):.2f} ms, kernel busy {1e-6 * busy:.2f} ms, {len(win)} launches")
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
+        print(f"{1e-6 * t:9.3f} ms {c:6d}  {100 * t / busy:5.1f}%  {k}")
+
+
+if __name__ == "__main__":
+    main()

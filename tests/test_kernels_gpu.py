@@ -246,6 +246,33 @@ def test_attention_bwd_deterministic(gpu, causal, S):
         assert torch.equal(r1[1], ra[1]) and torch.equal(r1[2], ra[2])
 
 
+@pytest.mark.parametrize("mode", [3, 1])
+def test_attention_training_shape_vs_fp32(gpu, mode):
+    """The exact Llama-3.1-70B training attention shape (S=2048, Hq=64, Hkv=8,
+    D=128, causal; one sequence) against an fp32 PyTorch reference: forward
+    output and every gradient, through the default split backward (3) and the
+    f32-atomic dQ path (1)."""
+    torch.manual_seed(5)
+    B, Hq, Hkv, S, D = 1, 64, 8, 2048, 128
+    q = torch.randn(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    sc = 1.0 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, True, sc)
+    do = torch.randn(B, S, Hq, D, device=gpu, dtype=torch.bfloat16)
+    dq, dkp, dvp = _ops().attn_bwd(do.view(B, S, Hq * D), q, k, v, o, lse, True, sc, mode)
+    rep = Hq // Hkv
+    dk = dkp.view(B, Hkv, rep, S, D).sum(2)
+    dv = dvp.view(B, Hkv, rep, S, D).sum(2)
+    qf, kf, vf = [t.float().requires_grad_(True) for t in (q, k, v)]
+    orf = ref.attention(qf.transpose(1, 2), kf.transpose(1, 2), vf.transpose(1, 2), causal=True)
+    assert rel_err(o.view(B, S, Hq, D), orf) < 2e-2
+    orf.backward(do.float())
+    assert rel_err(dq, qf.grad) < 3e-2
+    assert rel_err(dk, kf.grad) < 3e-2
+    assert rel_err(dv, vf.grad) < 3e-2
+
+
 def test_attention_block_autograd(gpu):
     """Full split+rope+attention autograd node vs the reference path."""
     from mxllm.ops.attention import attention_block
