@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--act-ckpt", action="store_true", help="activation checkpointing per layer")
     ap.add_argument("--sp", type=int, default=1,
                     help="sequence-parallel degree (Ulysses all-to-all around attention; long-context runs)")
+    ap.add_argument("--cp", type=int, default=1,
+                    help="context-parallel degree (ring attention, zigzag sequence layout; long-context runs)")
     ap.add_argument("--bucket-mb", type=float, default=128.0)
     ap.add_argument("--device", default=None, help="force 'cpu' for a plumbing run")
     ap.add_argument("--layers", type=int, default=None, help="override n_layers (NOT valid for the headline)")
@@ -258,14 +260,23 @@ def run(a, env) -> dict:
         model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
                       activation_checkpointing=a.act_ckpt)
         trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb, shard_optimizer=a.parallel == "zero1")
-    sp_group, data_rank = None, env.rank
-    if a.sp > 1:
+    sp_group, data_rank, shard_fn = None, env.rank, None
+    if a.sp > 1 and a.cp > 1:
+        raise SystemExit("--sp and --cp are alternatives")
+    if a.sp > 1 or a.cp > 1:
         if a.parallel == "zero3":
-            raise SystemExit("--sp is supported with --parallel ddp / zero1")
+            raise SystemExit("--sp / --cp are supported with --parallel ddp / zero1")
         from mxllm.parallel.sequence import new_groups, shard_sequence
 
-        sp_group, data_rank, _ = new_groups(a.sp)
-        model.set_sequence_parallel(sp_group)
+        sp_group, data_rank, _ = new_groups(max(a.sp, a.cp))
+        if a.cp > 1:
+            from mxllm.parallel.context import zigzag_shard
+
+            model.set_context_parallel(sp_group)
+            shard_fn = zigzag_shard
+        else:
+            model.set_sequence_parallel(sp_group)
+            shard_fn = shard_sequence
     data = SyntheticTokens(cfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1, rank=data_rank)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -273,8 +284,8 @@ def run(a, env) -> dict:
 
     def step():
         mbs = [data.next() for _ in range(a.grad_accum)]
-        if sp_group is not None:  # every rank of an SP group gets the same sequences, keeps its slice
-            mbs = [(shard_sequence(i, sp_group), shard_sequence(l, sp_group)) for i, l in mbs]
+        if sp_group is not None:  # every rank of an SP/CP group gets the same sequences, keeps its slice
+            mbs = [(shard_fn(i, sp_group), shard_fn(l, sp_group)) for i, l in mbs]
         return trainer.train_step(mbs)
 
     def sync():
@@ -302,7 +313,8 @@ def run(a, env) -> dict:
     elapsed = runtime.all_reduce_scalars([elapsed], op="max")[0]
     loss_v = float(loss.float().item()) if loss is not None else float("nan")
     world = emulated or env.world_size  # emulation: tokens of ONE rank of that world
-    tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size // a.sp
+    sq = max(a.sp, a.cp)
+    tokens_per_step = a.micro_batch * a.seq_len * a.grad_accum * env.world_size // sq
     tps = tokens_per_step * a.steps / elapsed if a.steps else 0.0
     ms = 1e3 * elapsed / max(1, a.steps)
     peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else 0.0
@@ -314,7 +326,8 @@ def run(a, env) -> dict:
         par = f"zero3-dp{world}" + (" (EMULATED on 1 GPU: world-%d shard sizes, no link traffic)" % world
                                     if emulated else "")
     else:
-        par = f"dp{env.world_size // a.sp}-sp{a.sp}" if a.sp > 1 else f"dp{env.world_size}"
+        par = (f"dp{env.world_size // a.sp}-sp{a.sp}" if a.sp > 1 else
+               f"dp{env.world_size // a.cp}-cp{a.cp}" if a.cp > 1 else f"dp{env.world_size}")
         if a.parallel == "zero1":
             par += "-zero1" if getattr(trainer, "zero1", None) is not None else " (zero1 requested: world 1 = ddp)"
     out = {
@@ -332,7 +345,7 @@ def run(a, env) -> dict:
         "data": "synthetic (random token ids, random-init weights)",
         "config": {
             "model": PRETTY.get(cfg.name, cfg.name) + (f" ({cfg.n_layers} layers)" if a.layers else ""),
-            "global_batch": a.micro_batch * a.grad_accum * env.world_size // a.sp,
+            "global_batch": a.micro_batch * a.grad_accum * env.world_size // sq,
             "seq_len": a.seq_len,
             "parallelism": par,
             "finetune": (f"lora r={lora_r} alpha={a.lora_alpha} on q,k,v,o,gate,up,down; frozen bf16 base"

@@ -54,6 +54,7 @@ class RunConfig:
     finetune: str = "lora"  # lora | full
     parallel: str = "ddp"  # ddp | zero1 (sharded optimizer) | zero3 (sharded everything)
     sequence_parallel: int = 1  # Ulysses SP degree (ranks per sequence); world = dp x sp
+    context_parallel: int = 1  # ring-attention CP degree (zigzag sequence shards); world = dp x cp
     lora_r: int = 16
     lora_alpha: float = 32.0
     lr: float = 1e-4

@@ -316,6 +316,17 @@ class Llama(nn.Module):
 
         self.seq_parallel = UlyssesAttention(group)
 
+    def set_context_parallel(self, group) -> None:
+        """Shard sequences over ``group`` in the zigzag layout (ring attention,
+        mxllm/parallel/context.py); ``None`` turns it off.  Inputs passed to
+        forward are then this rank's [B, S/P] zigzag tokens (``zigzag_shard``)."""
+        if group is None:
+            self.seq_parallel = None
+            return
+        from ..parallel.context import RingAttention
+
+        self.seq_parallel = RingAttention(group)
+
     # ------------------------------------------------------------------ utilities
     def trainable_parameters(self):
         return [p for p in self.parameters() if p.requires_grad]

@@ -82,14 +82,23 @@ def main(argv=None):
         from mxllm.train import checkpoint
 
         trainer = build_trainer(run, env)
-        sp_group, data_rank, data_world = None, rank, world_size
-        if run.sequence_parallel > 1:
+        sp_group, data_rank, data_world, shard = None, rank, world_size, None
+        if run.sequence_parallel > 1 and run.context_parallel > 1:
+            raise ValueError("--sequence-parallel and --context-parallel are alternatives")
+        if run.sequence_parallel > 1 or run.context_parallel > 1:
             if run.parallel not in ("ddp", "zero1"):
-                raise ValueError("--sequence-parallel is supported with --parallel ddp / zero1")
+                raise ValueError("--sequence-parallel / --context-parallel are supported with --parallel ddp / zero1")
             from mxllm.parallel.sequence import new_groups, shard_sequence
 
-            sp_group, data_rank, data_world = new_groups(run.sequence_parallel)
-            trainer.model.set_sequence_parallel(sp_group)
+            sp_group, data_rank, data_world = new_groups(max(run.sequence_parallel, run.context_parallel))
+            if run.context_parallel > 1:  # ring attention over zigzag-sharded sequences
+                from mxllm.parallel.context import zigzag_shard
+
+                trainer.model.set_context_parallel(sp_group)
+                shard = zigzag_shard
+            else:  # Ulysses all-to-all around attention
+                trainer.model.set_sequence_parallel(sp_group)
+                shard = shard_sequence
         mcfg = get_config(run.model)
         tok = get_tokenizer(mcfg.vocab_size, run.tokenizer or None, mcfg.bos_id, mcfg.eos_id)
         texts, _ = load_text_dataset(run.dataset, run.split, run.n_rows, run.seed)
@@ -124,7 +133,7 @@ def main(argv=None):
             for _ in range(run.grad_accum):
                 ids, lab, epoch, _i = loader.next_device()
                 if sp_group is not None:
-                    ids, lab = shard_sequence(ids, sp_group), shard_sequence(lab, sp_group)
+                    ids, lab = shard(ids, sp_group), shard(lab, sp_group)
                 mbs.append((ids, lab))
             loss = trainer.train_step(mbs)
             n_since += 1

@@ -349,6 +349,37 @@ def test_engine_fp8_graphed_decode_b16_close_to_bf16(gpu, small_m, monkeypatch):
     assert cos.min().item() > 0.99, cos
 
 
+def test_ring_attention_one_rank_gpu(gpu):
+    """Context-parallel attention path on the GPU kernels (HIP rope_split at
+    gathered zigzag positions, flash fwd/bwd per block, LSE merge, rope_merge):
+    a one-rank ring equals the plain attention block, forward and backward.
+    (Multi-rank rings: tests/test_context_parallel.py on gloo.)"""
+    import socket
+
+    import torch.distributed as dist
+
+    from mxllm import ops
+    from mxllm.ops import reference as ref
+    from mxllm.parallel.context import RingAttention
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        B, S, Hq, Hkv, D = 2, 256, 8, 2, 128
+        cos, sin = ref.rope_tables(S, D, 500000.0, None, gpu)
+        qkv = (torch.randn(B * S, (Hq + 2 * Hkv) * D, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_(True)
+        g = torch.randn(B * S, Hq * D, device=gpu).to(torch.bfloat16)
+        o1 = RingAttention(dist.group.WORLD)(qkv, cos, sin, B, S, Hq, Hkv, D)
+        (d1,) = torch.autograd.grad(o1, qkv, g)
+        o2 = ops.attention_block(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True)
+        (d2,) = torch.autograd.grad(o2, qkv, g)
+        assert _rel(o1, o2) < 1e-2 and _rel(d1, d2) < 2e-2, (_rel(o1, o2), _rel(d1, d2))
+    finally:
+        dist.destroy_process_group()
+
+
 def _tp_gpu_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MXLLM_BACKEND="gloo", LOCAL_RANK=str(rank))
     import torch.distributed as dist
