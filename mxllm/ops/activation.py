@@ -1,6 +1,7 @@
 """SwiGLU ``silu(gate) * up`` over a fused [gate | up] projection.
 
-GPU: csrc/kernels/swiglu.hip (vectorised 16-B bf16, fwd + bwd in one pass each).
+GPU: csrc/kernels/elementwise.hip ``swiglu_fwd_kernel`` / ``swiglu_bwd_kernel`` (vectorised 16-B
+bf16, fwd + bwd in one pass each).
 """
 from __future__ import annotations
 
