@@ -43,30 +43,42 @@ class FusedLinear(nn.Module):
     """
 
     def __init__(self, in_features: int, splits: list[int], *, dtype, device, lora_r: int = 0,
-                 lora_alpha: float = 16.0, train_base: bool = True, dx_image: bool = False):
+                 lora_alpha: float = 16.0, train_base: bool = True, dx_image: bool = False,
+                 transposed: bool = False):
         super().__init__()
         self.in_features = in_features
         self.splits = list(splits)
         N = sum(splits)
         self.lora_r = lora_r
         self.pad = 0
+        self.transposed = False
         if lora_r > 0:
             n = len(splits)
             self.scaling = lora_alpha / lora_r
             self.pad = (n * lora_r + 63) // 64 * 64
-            self.register_buffer("wbuf", torch.zeros(N + self.pad, in_features + self.pad, dtype=dtype,
-                                                     device=device), persistent=False)
+            # ``transposed``: the augmented buffer is stored as its transpose
+            # [[W^T, A^T], [B^T, 0]] [in + pad, N + pad] -> the forward GEMM runs in
+            # hipBLASLt's NN form and the input-gradient GEMM in the TN form (the reverse
+            # of the row-major layout), with no second copy of W; A is kept as a small
+            # k-contiguous copy ``wa`` for the rank-r kernel
+            self.transposed = transposed and not train_base
+            shape = (in_features + self.pad, N + self.pad) if self.transposed else (N + self.pad, in_features + self.pad)
+            self.register_buffer("wbuf", torch.zeros(*shape, dtype=dtype, device=device), persistent=False)
             # B^T [pad, N] (zero rows past n*r): the k-contiguous operand of the
             # backward s dy B kernel (csrc/kernels/lora.hip), refreshed with wbuf
             self.register_buffer("wbt", torch.zeros(self.pad, N, dtype=dtype, device=device), persistent=False)
+            if self.transposed:
+                self.register_buffer("wa", torch.zeros(self.pad, in_features, dtype=dtype, device=device),
+                                     persistent=False)
             # optional [W; A]^T image [in, N + pad]: the input-gradient GEMM then runs in
             # hipBLASLt's reduction-contiguous form (dx = dy_aug @ wxt^T) instead of the
             # ~15-30 % slower NN form; frozen W part refreshed by refresh_images_(), the A^T
             # columns by every adapter sync.  Costs one more copy of W (qkv/o only by default)
-            if dx_image and not train_base:
+            if dx_image and not train_base and not self.transposed:
                 self.register_buffer("wxt", torch.zeros(in_features, N + self.pad, dtype=dtype, device=device),
                                      persistent=False)
-            self.weight = nn.Parameter(self.wbuf[:N, :in_features], requires_grad=train_base)
+            w = self.wbuf[:in_features, :N].t() if self.transposed else self.wbuf[:N, :in_features]
+            self.weight = nn.Parameter(w, requires_grad=train_base)
             # A: all splits' down-projections stacked; B: block-diagonal up-projection
             self.lora_a = nn.Parameter(torch.empty(n * lora_r, in_features, dtype=dtype, device=device))
             self.lora_b = nn.Parameter(torch.zeros(N, n * lora_r, dtype=dtype, device=device))
@@ -90,6 +102,9 @@ class FusedLinear(nn.Module):
     def adapter_copies(self):
         """(src, dst) pairs: adapter parameters -> their slots in ``wbuf``."""
         N, K, R = sum(self.splits), self.in_features, self.lora_a.shape[0]
+        if self.transposed:
+            return [(self.lora_a.data, self.wbuf[:K, N:N + R].t()), (self.lora_b.data, self.wbuf[K:K + R, :N].t()),
+                    (self.lora_b.data, self.wbt[:R, :N].t()), (self.lora_a.data, self.wa[:R, :K])]
         out = [(self.lora_a.data, self.wbuf[N:N + R, :K]), (self.lora_b.data, self.wbuf[:N, K:K + R]),
                (self.lora_b.data, self.wbt[:R, :N].t())]
         if getattr(self, "wxt", None) is not None:
@@ -124,7 +139,8 @@ class FusedLinear(nn.Module):
         if self.lora_r > 0:
             if self.augmented():
                 return ops.lora_linear_aug(x, self.lora_a, self.lora_b, self.wbuf, self.splits, self.scaling,
-                                           self.pad, self.wbt, getattr(self, "wxt", None))
+                                           self.pad, self.wbt, getattr(self, "wxt", None),
+                                           getattr(self, "wa", None) if self.transposed else None)
             return ops.lora_linear(x, self.weight, self.lora_a, self.lora_b, self.splits, self.scaling)
         return ops.linear(x, self.weight)
 
@@ -134,6 +150,9 @@ class FusedLinear(nn.Module):
 # (qkv) and 0.395 -> 0.333 ms (o) for +24 GB of HBM; gate/up and down would need
 # +113 GB, which a 70B LoRA step (240 GB peak) cannot spare.
 DX_IMAGE = tuple(x for x in os.environ.get("MXLLM_DX_IMAGE", "qkv,o").split(",") if x)
+# LoRA projections whose augmented buffer is stored transposed (FusedLinear ``transposed``):
+# forward GEMM in the NN form, input gradient in the TN form, same memory
+LORA_T = tuple(x for x in os.environ.get("MXLLM_LORA_T", "").split(",") if x)
 
 
 class LlamaLayer(nn.Module):
@@ -143,10 +162,11 @@ class LlamaLayer(nn.Module):
         h = cfg.hidden
         self.attn_norm = nn.Parameter(torch.ones(h, dtype=dtype, device=device), requires_grad=train_base)
         self.mlp_norm = nn.Parameter(torch.ones(h, dtype=dtype, device=device), requires_grad=train_base)
-        self.wqkv = FusedLinear(h, [cfg.q_dim, cfg.kv_dim, cfg.kv_dim], dx_image="qkv" in DX_IMAGE, **kw)
-        self.wo = FusedLinear(cfg.q_dim, [h], dx_image="o" in DX_IMAGE, **kw)
-        self.wgu = FusedLinear(h, [cfg.ffn, cfg.ffn], **kw)
-        self.wd = FusedLinear(cfg.ffn, [h], **kw)
+        self.wqkv = FusedLinear(h, [cfg.q_dim, cfg.kv_dim, cfg.kv_dim], dx_image="qkv" in DX_IMAGE,
+                                transposed="qkv" in LORA_T, **kw)
+        self.wo = FusedLinear(cfg.q_dim, [h], dx_image="o" in DX_IMAGE, transposed="o" in LORA_T, **kw)
+        self.wgu = FusedLinear(h, [cfg.ffn, cfg.ffn], transposed="gu" in LORA_T, **kw)
+        self.wd = FusedLinear(cfg.ffn, [h], transposed="d" in LORA_T, **kw)
 
 
 class Llama(nn.Module):

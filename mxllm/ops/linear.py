@@ -137,32 +137,38 @@ class _LoRAAugFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt, wxt=None):
-        N, K = wbuf.shape[0] - pad, wbuf.shape[1] - pad
+    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt, wxt=None, wa=None):
+        tr = wa is not None  # transposed buffer [[W^T, A^T], [B^T, 0]] (FusedLinear ``transposed``)
+        if tr:
+            K, N = wbuf.shape[0] - pad, wbuf.shape[1] - pad
+        else:
+            N, K = wbuf.shape[0] - pad, wbuf.shape[1] - pad
         x2 = x.reshape(-1, K)
         xa = _augment(x2, pad)
         nat = _lora_native(x2, N, K, splits, r, wbt)
+        amat = wa if tr else wbuf[N:, :K]  # A rows [pad, K] (zero rows past n*r), k-contiguous
         if nat:
-            native().lora_xwt(x2, wbuf[N:, :K], xa[:, K:], scaling)  # s t, zero in the pad columns
+            native().lora_xwt(x2, amat, xa[:, K:], scaling)  # s t, zero in the pad columns
         else:
-            xa[:, K:].addmm_(x2, wbuf[N:, :K].t(), beta=0.0, alpha=scaling)
-        y = torch.mm(xa, wbuf[:N, :].t())
+            xa[:, K:].addmm_(x2, amat.t(), beta=0.0, alpha=scaling)
+        y = torch.mm(xa, wbuf[:, :N]) if tr else torch.mm(xa, wbuf[:N, :].t())
         ctx.save_for_backward(xa, wbuf)
         ctx.lora_a, ctx.lora_b, ctx.wbt, ctx.wxt = a, b, wbt, wxt
-        ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat)
+        ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat, tr)
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
         xa, wbuf = ctx.saved_tensors
-        N, K, s, splits, r, pad, xshape, nat = ctx.dims
+        N, K, s, splits, r, pad, xshape, nat, tr = ctx.dims
         R = r * len(splits)
         dy2 = dy.reshape(-1, N)
         dya = _augment(dy2, pad)
         if nat:
             native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s)  # g = s dy B, zero in the pad columns
         else:
-            dya[:, N:].addmm_(dy2, wbuf[:N, K:], beta=0.0, alpha=s)
+            bmat = wbuf[K:, :N].t() if tr else wbuf[:N, K:]  # B [N, pad]
+            dya[:, N:].addmm_(dy2, bmat, beta=0.0, alpha=s)
         g = dya[:, N:N + R]
         x2, st = xa[:, :K], xa[:, K:K + R]
         da = db = None
@@ -198,20 +204,23 @@ class _LoRAAugFn(torch.autograd.Function):
                     mark_ready(ctx.lora_b)
                 else:
                     db = tgt
-        if ctx.wxt is not None:  # reduction-contiguous image of [W; A]: hipBLASLt "TN"
+        if tr:  # [W; A]^T is the leading K rows of the transposed buffer: TN form
+            dx = torch.mm(dya, wbuf[:K, :].t())
+        elif ctx.wxt is not None:  # reduction-contiguous image of [W; A]: hipBLASLt "TN"
             dx = torch.mm(dya, ctx.wxt.t())
         else:
             dx = torch.mm(dya, wbuf[:, :K])
-        return dx.view(xshape), da, db, None, None, None, None, None, None, None
+        return dx.view(xshape), da, db, None, None, None, None, None, None, None, None
 
 
 def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: torch.Tensor, splits: Sequence[int],
                     scaling: float, pad: int, wbt: torch.Tensor | None = None,
-                    wxt: torch.Tensor | None = None) -> torch.Tensor:
+                    wxt: torch.Tensor | None = None, wa: torch.Tensor | None = None) -> torch.Tensor:
     """LoRA projection through the augmented weight buffer (see _LoRAAugFn);
-    ``wxt``: optional [K, N+pad] transposed image of wbuf[:, :K] for dX."""
+    ``wxt``: optional [K, N+pad] transposed image of wbuf[:, :K] for dX;
+    ``wa``: given for a TRANSPOSED buffer [[W^T, A^T], [B^T, 0]] (A rows, k-contiguous)."""
     r = a.shape[0] // len(splits)
-    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt)
+    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt, wa)
 
 
 def transpose2d(t: torch.Tensor) -> torch.Tensor:

@@ -349,6 +349,35 @@ def test_engine_fp8_graphed_decode_b16_close_to_bf16(gpu, small_m, monkeypatch):
     assert cos.min().item() > 0.99, cos
 
 
+def test_lora_transposed_buffers_match_gpu(gpu, monkeypatch):
+    """LoRA projections with TRANSPOSED augmented buffers (forward NN, dX TN GEMM,
+    A kept as a k-contiguous copy for the HIP rank-r kernel) give the same loss and
+    adapter gradients as the row-major layout, on the HIP path."""
+    import mxllm.models.llama as L
+    from mxllm.models import get_config
+
+    cfg = get_config("tiny-d128").replace(n_layers=2)
+
+    def run(flag):
+        monkeypatch.setattr(L, "LORA_T", flag)
+        m = L.Llama(cfg, device=gpu, lora_r=16, seed=3)
+        with torch.no_grad():
+            g = torch.Generator(device=gpu).manual_seed(0)
+            for n, p in m.named_parameters():
+                p.copy_(torch.randn(p.shape, device=gpu, generator=g).to(p.dtype) * 0.02)
+        m.sync_adapters_()
+        ids = torch.randint(0, cfg.vocab_size, (2, 128), device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
+        loss = m(ids, ids)
+        loss.backward()
+        return float(loss), {n: p.grad.float() for n, p in m.named_parameters() if p.requires_grad}
+
+    l0, g0 = run(())
+    l1, g1 = run(("qkv", "o", "gu", "d"))
+    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0)), (l0, l1)
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 2e-2, k
+
+
 def test_ring_attention_one_rank_gpu(gpu):
     """Context-parallel attention path on the GPU kernels (HIP rope_split at
     gathered zigzag positions, flash fwd/bwd per block, LSE merge, rope_merge):
