@@ -42,6 +42,21 @@ def project(step_ms: float, tokens_per_gpu: int, grad_bytes: float, bw_gbs: floa
     return rows
 
 
+def project_zero3(step_ms: float, tokens_per_gpu: int, param_bytes: float, bw_gbs: float, n: int = 8,
+                  unit_bytes: float = 1.71e9, contention: float = 0.02):
+    """BASELINE config 4 at n GPUs from the measured world-n EMULATED step (per-rank
+    compute, memory traffic and shard sizes of the real run, no link traffic): per
+    step every rank receives (n-1)/n of the model twice (forward + backward
+    all-gathers) and sends it once (gradient reduce-scatter), overlapped with the
+    compute (prefetch one unit ahead, asynchronous reduce-scatter); exposed = what
+    outlasts the compute plus the first unit's gather."""
+    comm = 3.0 * param_bytes * (n - 1) / n / (bw_gbs * 1e9) * 1e3
+    first = unit_bytes * (n - 1) / n / (bw_gbs * 1e9) * 1e3
+    exposed = max(0.0, comm - step_ms) + first
+    ms = step_ms * (1 + contention) + exposed
+    return {"n": n, "ms": ms, "tok_s": n * tokens_per_gpu * 1e3 / ms, "comm_ms": comm, "exposed_ms": exposed}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", action="store_true")
@@ -58,6 +73,13 @@ def main():
     if a.json:
         print(json.dumps(out))
         return
+    z3 = {"act-ckpt, micro-batch 4 (bench default for config 4)": dict(step_ms=3726.1, tokens_per_gpu=8192),
+          "no checkpointing, micro-batch 2": dict(step_ms=1570.8, tokens_per_gpu=4096)}
+    z3_rows = {name: {f"{bw} GB/s": project_zero3(param_bytes=70.554e9 * 2, bw_gbs=bw, **kw) for bw in (150, 350)}
+               for name, kw in z3.items()}
+    if a.json:
+        print(json.dumps({"ddp": out, "zero3_config4": z3_rows}))
+        return
     for name, d in out.items():
         print(f"### {name}\n")
         print("| GPUs | bus bw | ms/step | tokens/s (node) | exposed comm ms | efficiency |")
@@ -67,6 +89,14 @@ def main():
                 print(f"| {r['n']} | {bw} | {r['ms']:.1f} | {r['tok_s']:,.0f} | {r['exposed_ms']:.1f} | "
                       f"{r['efficiency']:.3f} |")
         print()
+    print("### Llama-3.1-70B FULL fine-tune, ZeRO-3, 8 GPUs (BASELINE config 4), from the world-8 emulated step\n")
+    print("| config | bus bw | compute ms (measured, emulated) | comm ms | exposed ms | ms/step | tokens/s (node) |")
+    print("|---|---|---|---|---|---|---|")
+    for name, d in z3_rows.items():
+        for bw, r in d.items():
+            print(f"| {name} | {bw} | {z3[name]['step_ms']:.0f} | {r['comm_ms']:.0f} | {r['exposed_ms']:.0f} | "
+                  f"{r['ms']:.0f} | {r['tok_s']:,.0f} |")
+    print()
 
 
 if __name__ == "__main__":
