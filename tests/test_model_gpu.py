@@ -366,6 +366,7 @@ def test_lora_transposed_buffers_match_gpu(gpu, monkeypatch):
             for n, p in m.named_parameters():
                 p.copy_(torch.randn(p.shape, device=gpu, generator=g).to(p.dtype) * 0.02)
         m.sync_adapters_()
+        m.refresh_images_()  # the transposed [W; A] dX images of the row-major layout follow W
         ids = torch.randint(0, cfg.vocab_size, (2, 128), device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
         loss = m(ids, ids)
         loss.backward()
