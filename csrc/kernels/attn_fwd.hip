@@ -5,7 +5,7 @@
 // lse [B,Hq,S] f32 in the log2 domain of the scaled scores.
 //
 // Structure (CDNA HIP guide App. B "Fused attention prefill"):
-//  * workgroup = 4 waves = 128 query rows (32 per wave), KV tile = 64 keys;
+//  * workgroup = NW waves = 32 NW query rows (4 by default), KV tile = 64 keys;
 //  * "swapped" QK^T: S^T = K . Q^T with v_mfma_f32_32x32x16_bf16, so each lane
 //    owns one query column and the tile's keys sit in its 16+16 accumulator
 //    registers -> row max / row sum are in-register (+1 cross-half shuffle);
@@ -25,6 +25,7 @@
 //  * causal blocks scheduled heaviest-first, XCD-aware block remap so the
 //    q-heads sharing one KV head run on the same XCD (shared L2).
 #include "common.h"
+#include <stdlib.h>
 
 namespace mx {
 
@@ -48,14 +49,18 @@ __device__ __forceinline__ u16x4 tr_read(const char* p) {
   return __builtin_bit_cast(u16x4, v);
 }
 
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2)
+// NW waves per workgroup = 32 NW query rows sharing every streamed K/V tile (2 waves per SIMD
+// either way).  4 by default; 8 halves the K/V tile traffic per FLOP but measured the same
+// (0.259 vs 0.257 ms at B2 S2048 Hq64 Hkv8 D128 causal: the stream is not the limiter)
+template <int D, bool CAUSAL, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
                 int causal_off, float sl, int ldo) {
-  constexpr int BM = 128, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int BM = 32 * NW, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int TILE = BN * ROWB;
-  constexpr int LPT = BN * CH / 256;
+  constexpr int LPT = BN * CH / (64 * NW);
+  static_assert(LPT >= 1 && BN * CH % (64 * NW) == 0, "K/V tile must split evenly over the waves");
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
 
   const int nqb = (S + BM - 1) / BM;
@@ -270,14 +275,21 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
                            hipStream_t stream) {
   if (B <= 0 || S <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv || ldo < Hq * D || ldo % 8) return -1;
-  const int nqb = (S + 127) / 128;
-  const int grid = nqb * B * Hq;
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
-#define FWD(DD, C) attn_fwd_kernel<DD, C><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo)
-  if (D == 128) { if (causal) FWD(128, true); else FWD(128, false); }
-  else if (D == 64) { if (causal) FWD(64, true); else FWD(64, false); }
-  else if (D == 32) { if (causal) FWD(32, true); else FWD(32, false); }
+  static const int nw128 = [] {  // MXLLM_ATTN_FWD_WAVES=8: the 8-wave (256-row) variant for D = 128 (A/B)
+    const char* e = getenv("MXLLM_ATTN_FWD_WAVES");
+    return (e && e[0] == '8') ? 8 : 4;
+  }();
+#define FWD(DD, C, NWV)                                                                                  \
+  attn_fwd_kernel<DD, C, NWV><<<((S + 32 * NWV - 1) / (32 * NWV)) * B * Hq, 64 * NWV, 0, stream>>>(     \
+      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo)
+  if (D == 128) {
+    if (nw128 == 8) { if (causal) FWD(128, true, 8); else FWD(128, false, 8); }
+    else { if (causal) FWD(128, true, 4); else FWD(128, false, 4); }
+  }
+  else if (D == 64) { if (causal) FWD(64, true, 4); else FWD(64, false, 4); }
+  else if (D == 32) { if (causal) FWD(32, true, 4); else FWD(32, false, 4); }
   else return -1;
 #undef FWD
   return (int)hipGetLastError();
