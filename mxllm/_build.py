@@ -110,6 +110,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
             f.write(link_key)
         if verbose:
             print(f"[mxllm build] linked {os.path.relpath(LIB_PATH, ROOT)}", flush=True)
+    _write_buildinfo(hip_srcs + cpp_srcs, hdrs, hip_flags, cxx_flags, len(todo), link_key)
     # drop stale objects from older source versions
     keep = set(objs)
     for o in glob.glob(os.path.join(OUT_DIR, "*.o")):
@@ -119,6 +120,34 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
             except OSError:
                 pass
     return LIB_PATH
+
+
+def _write_buildinfo(srcs, hdrs, hip_flags, cxx_flags, compiled: int, link_key: str) -> None:
+    """Provenance record next to the library (``mxllm/_C.buildinfo.json``): what was
+    compiled, with which compiler/flags, and a hash of every source that went in."""
+    import json
+    import time
+
+    try:
+        ver = subprocess.run([os.path.join(ROCM, "bin", "hipcc"), "--version"], stdout=subprocess.PIPE,
+                             stderr=subprocess.STDOUT, text=True).stdout.strip().splitlines()
+    except OSError:
+        ver = []
+    info = {
+        "library": os.path.relpath(LIB_PATH, ROOT),
+        "arch": ARCH,
+        "built_at_unix": int(time.time()),
+        "objects_compiled_this_build": compiled,
+        "objects_total": len(srcs),
+        "link_key": link_key,
+        "sources_sha1_16": _hash(srcs + hdrs, ""),
+        "sources": [os.path.relpath(x, ROOT) for x in srcs],
+        "hipcc": ver[:2],
+        "hip_flags": hip_flags,
+        "cxx_flags": [f for f in cxx_flags if not f.startswith("-I")],
+    }
+    with open(LIB_PATH.replace(".so", ".buildinfo.json"), "w") as f:
+        json.dump(info, f, indent=1)
 
 
 def main(argv=None):
