@@ -146,10 +146,11 @@ class FusedLinear(nn.Module):
 
 
 # LoRA projections that keep a transposed [W; A] image for the input-gradient GEMM
-# (FusedLinear.wxt).  Default qkv + o: measured at the 70B shapes, dX 0.625 -> 0.427 ms
-# (qkv) and 0.395 -> 0.333 ms (o) for +24 GB of HBM; gate/up and down would need
-# +113 GB, which a 70B LoRA step (240 GB peak) cannot spare.
-DX_IMAGE = tuple(x for x in os.environ.get("MXLLM_DX_IMAGE", "qkv,o").split(",") if x)
+# (FusedLinear.wxt): hipBLASLt's TN form instead of the ~15 % slower NN form, for one more
+# copy of W.  Measured 70B LoRA step, same box (profiles/r2n_dx_image_ab.md): qkv,o 1001.3 ms
+# (267.4 GB reserved) / qkv,d 990.8 ms (294.3 GB) / qkv,o,d 985.5 ms (305.3 GB of 309: too
+# little headroom for multi-GPU runs).  Default qkv + d.
+DX_IMAGE = tuple(x for x in os.environ.get("MXLLM_DX_IMAGE", "qkv,d").split(",") if x)
 # LoRA projections whose augmented buffer is stored transposed (FusedLinear ``transposed``):
 # forward GEMM in the NN form, input gradient in the TN form, same memory
 LORA_T = tuple(x for x in os.environ.get("MXLLM_LORA_T", "").split(",") if x)
@@ -165,8 +166,8 @@ class LlamaLayer(nn.Module):
         self.wqkv = FusedLinear(h, [cfg.q_dim, cfg.kv_dim, cfg.kv_dim], dx_image="qkv" in DX_IMAGE,
                                 transposed="qkv" in LORA_T, **kw)
         self.wo = FusedLinear(cfg.q_dim, [h], dx_image="o" in DX_IMAGE, transposed="o" in LORA_T, **kw)
-        self.wgu = FusedLinear(h, [cfg.ffn, cfg.ffn], transposed="gu" in LORA_T, **kw)
-        self.wd = FusedLinear(cfg.ffn, [h], transposed="d" in LORA_T, **kw)
+        self.wgu = FusedLinear(h, [cfg.ffn, cfg.ffn], dx_image="gu" in DX_IMAGE, transposed="gu" in LORA_T, **kw)
+        self.wd = FusedLinear(cfg.ffn, [h], dx_image="d" in DX_IMAGE, transposed="d" in LORA_T, **kw)
 
 
 class Llama(nn.Module):
