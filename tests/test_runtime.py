@@ -186,12 +186,14 @@ def test_fault_injection_fails_fast():
     assert r.returncode != 0
 
 
-def test_fault_restart_resumes_from_checkpoint(tmp_path):
-    """--max-restarts 1 + checkpoints: the restarted job resumes and finishes."""
+@pytest.mark.parametrize("parallel", ["ddp", "zero1"])
+def test_fault_restart_resumes_from_checkpoint(tmp_path, parallel):
+    """--max-restarts 1 + checkpoints: the restarted job resumes and finishes
+    (ZeRO-1: every rank restores its own optimizer shard)."""
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--max-restarts", "1",
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()), "src/distributed_finetuning.py",
                         "--steps", "6", "--seq-len", "32", "--micro-batch", "1", "--save-every", "2", "--ckpt-dir",
-                        str(tmp_path)], cwd=ROOT,
+                        str(tmp_path), "--parallel", parallel], cwd=ROOT,
                        env=_env(MXLLM_FAULT_RANK=0, MXLLM_FAULT_STEP=3, MXLLM_FAULT_KIND="raise",
                                 MXLLM_PG_TIMEOUT_S=60), capture_output=True, text=True, timeout=400)
     log = r.stdout + r.stderr
