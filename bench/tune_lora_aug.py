@@ -4,7 +4,7 @@ uses (row strides K+64 / N+64), and append them to the selection table.
 
   fwd: y  = x_aug[T, K+64] @ wbuf[:N, :]^T        (wbuf row stride K+64)
   bwd: dx = dy_aug[T, N+64] @ wbuf[:, :K]         (row stride K+64)
-  bwd_tn: dx = dy_aug @ wxt^T  (wxt = [W; A]^T image, qkv/o projections)
+  bwd_tn: dx = dy_aug @ wxt^T  (wxt = [W; A]^T image: qkv and down projections by default)
 
 The table is written after every shape, so a time limit loses at most one.
 """
@@ -52,12 +52,13 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tunableop_lora_aug.csv"))
     ap.add_argument("--max-ms", type=int, default=60)
     ap.add_argument("--shapes", default="qkv,o,gu,down")
+    ap.add_argument("--ops", default="fwd,bwd,bwd_tn", help="subset of fwd,bwd,bwd_tn to tune")
     a = ap.parse_args()
     tun = torch.cuda.tunable
     res = {}
     for name in a.shapes.split(","):
         N, K = SHAPES[name]
-        fns = ops_for(N, K)
+        fns = {k: f for k, f in ops_for(N, K).items() if k in a.ops.split(",")}
         base = {k: timeit(f) for k, f in fns.items()}
         tun.enable(True)
         tun.tuning_enable(True)
