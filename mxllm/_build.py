@@ -32,6 +32,13 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("MXLLM_ARCH", "gfx950")
 
 
+# per-kernel-file compiler options (A/B experiments: MXLLM_FILE_FLAGS="file.hip=-opt1 -opt2;other.hip=...")
+PER_FILE_HIP_FLAGS: dict[str, list[str]] = {}
+for _item in filter(None, os.environ.get("MXLLM_FILE_FLAGS", "").split(";")):
+    _f, _, _opts = _item.partition("=")
+    PER_FILE_HIP_FLAGS.setdefault(_f.strip(), []).extend(shlex.split(_opts))
+
+
 def _torch_paths():
     import torch  # noqa: F401  (only for its install location)
 
@@ -77,9 +84,10 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
 
     jobs_list = []
     for src in hip_srcs:
-        key = _hash([src] + hdrs, " ".join(hip_flags))
+        flags = hip_flags + PER_FILE_HIP_FLAGS.get(os.path.basename(src), [])
+        key = _hash([src] + hdrs, " ".join(flags))
         obj = os.path.join(OUT_DIR, os.path.basename(src) + f".{key}.o")
-        cmd = [os.path.join(ROCM, "bin", "hipcc")] + hip_flags + ["-c", src, "-o", obj]
+        cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + ["-c", src, "-o", obj]
         jobs_list.append((src, obj, cmd))
     for src in cpp_srcs:
         key = _hash([src] + hdrs, " ".join(cxx_flags))

@@ -19,7 +19,8 @@ import torch
 _LOCK = threading.Lock()
 _LOADED = False
 _ERR: str | None = None
-LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+LIB = os.environ.get("MXLLM_NATIVE_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                         "_C.so")  # MXLLM_NATIVE_LIB: A/B builds only
 
 
 def _load() -> bool:
