@@ -75,6 +75,11 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const uint16_t* Vp = V + ((size_t)(b * Hkv + hk) * Sk) * D;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (no divergent branches)
+  // 8 waves = two per SIMD from the same workgroup: give the upper four priority 1 so the pair
+  // desynchronises and one wave's softmax runs under the other's MFMAs (guide T5, static form)
+  if constexpr (NW == 8) {
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   const int r = lane & 31, hh = lane >> 5;
   const int q0 = qb * BM;
   const int qrow = q0 + 32 * w + r;
