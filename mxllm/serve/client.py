@@ -15,6 +15,12 @@ Routing:
     ``api_key`` / ``OPENAI_API_KEY``.
 Failures are retried with exponential backoff + full jitter and a per-request
 timeout (the reference has neither — SURVEY D11 / A5).
+
+Also the other LiteLLM entry points a caller of the reference is likely to
+reach for: ``completion(..., stream=True)`` (an iterator of chunks with
+``.choices[0].delta.content``; SSE from the server, token deltas from the local
+engine), ``acompletion`` (awaitable; ``stream=True`` gives an async iterator)
+and ``batch_completion`` (one in-process engine pass for many conversations).
 """
 from __future__ import annotations
 
@@ -48,6 +54,25 @@ class Choice:
     message: Message
     index: int = 0
     finish_reason: str | None = "stop"
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+@dataclass
+class Delta:
+    content: str | None = None
+    role: str | None = None
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+@dataclass
+class StreamChoice:
+    delta: Delta
+    index: int = 0
+    finish_reason: str | None = None
 
     def __getitem__(self, k):
         return getattr(self, k)
@@ -154,14 +179,89 @@ class _Retryable(Exception):
     pass
 
 
+def _is_local(base) -> bool:
+    return base in (None, "", "local", "inproc") or str(base).startswith("local://")
+
+
+def _local_stream(model, messages, max_tokens, temperature, **kw):
+    """Token deltas from the in-process engine's background loop as they are produced."""
+    from .engine import SamplingParams
+
+    if model in _LOCAL:
+        eng, tok = _LOCAL[model]
+    elif len(_LOCAL) == 1:
+        eng, tok = next(iter(_LOCAL.values()))
+    else:
+        raise CompletionError(f"no local engine registered for model {model!r}")
+    eng.start()
+    ids = tok.apply_chat_template(messages)
+    r = eng.submit(ids, SamplingParams(max_new_tokens=max_tokens, temperature=temperature,
+                                       top_p=kw.get("top_p", 1.0), top_k=kw.get("top_k", 0), seed=kw.get("seed", 0)))
+    sent, first = 0, True
+    while True:
+        done = r.done.wait(0.002)
+        toks = r.output[sent:]
+        if toks:
+            sent += len(toks)
+            text = tok.decode([t for t in toks if t not in eng.eos_ids])
+            yield ModelResponse([StreamChoice(Delta(text, "assistant" if first else None))], model=model)
+            first = False
+        if done and sent >= len(r.output):
+            break
+    if r.error:
+        raise CompletionError(f"local engine: {r.error}")
+    yield ModelResponse([StreamChoice(Delta(None), finish_reason=r.finish_reason or "stop")], model=model)
+
+
+def _http_stream(model, messages, base, key, timeout, max_tokens, temperature, **kw):
+    """Server-sent-event chunks of an OpenAI-compatible endpoint."""
+    import json
+
+    import httpx
+
+    url = base.rstrip("/")
+    if not url.endswith("/chat/completions"):
+        url += "/chat/completions"
+    headers = {"Content-Type": "application/json"}
+    if key:
+        headers["Authorization"] = f"Bearer {key}"
+    body = {"model": model, "messages": messages, "max_tokens": max_tokens, "temperature": temperature,
+            "stream": True}
+    body.update({k: v for k, v in kw.items() if k in ("top_p", "stop", "seed", "top_k")})
+    with httpx.stream("POST", url, json=body, headers=headers, timeout=timeout) as r:
+        if r.status_code != 200:
+            r.read()
+            raise CompletionError(f"HTTP {r.status_code}: {r.text[:200]}")
+        for line in r.iter_lines():
+            if not line.startswith("data: "):
+                continue
+            data = line[6:]
+            if data.strip() == "[DONE]":
+                break
+            j = json.loads(data)
+            ch = j["choices"][0]
+            d = ch.get("delta") or {}
+            yield ModelResponse([StreamChoice(Delta(d.get("content"), d.get("role")), ch.get("index", 0),
+                                              ch.get("finish_reason"))], model=j.get("model", model),
+                                id=j.get("id", ""))
+
+
 def completion(model: str, messages: list[dict], *, api_base: str | None = None, api_key: str | None = None,
                timeout: float | None = None, num_retries: int | None = None, max_tokens: int = 128,
-               temperature: float = 0.0, backoff_base: float = 0.5, backoff_max: float = 8.0, **kw) -> ModelResponse:
+               temperature: float = 0.0, backoff_base: float = 0.5, backoff_max: float = 8.0, stream: bool = False,
+               **kw):
+    """LiteLLM ``completion``: a ModelResponse, or with ``stream=True`` an iterator of
+    chunks (``chunk.choices[0].delta.content``).  A stream is not retried once it
+    has started."""
     base = api_base if api_base is not None else globals()["api_base"]
     key = api_key or globals()["api_key"] or os.environ.get("OPENAI_API_KEY")
     timeout = timeout if timeout is not None else request_timeout
     retries = num_retries if num_retries is not None else globals()["num_retries"]
-    if base in (None, "", "local", "inproc") or str(base).startswith("local://"):
+    if stream:
+        if _is_local(base):
+            return _local_stream(model, messages, max_tokens, temperature, **kw)
+        return _http_stream(model, messages, base, key, timeout, max_tokens, temperature, **kw)
+    if _is_local(base):
         return _local(model, messages, max_tokens, temperature, **kw)
     attempt = 0
     while True:
@@ -176,3 +276,45 @@ def completion(model: str, messages: list[dict], *, api_base: str | None = None,
             delay = random.uniform(0, min(backoff_max, backoff_base * 2 ** (attempt - 1)))
             log.warning("completion attempt %d failed (%s); retrying in %.2fs", attempt, e, delay)
             time.sleep(delay)
+
+
+async def acompletion(model: str, messages: list[dict], **kw):
+    """LiteLLM ``acompletion``: awaitable ``completion`` (the blocking work runs in a
+    worker thread); with ``stream=True`` an async iterator of chunks."""
+    import asyncio
+
+    if kw.get("stream"):
+        it = completion(model, messages, **kw)
+
+        async def agen():
+            loop = asyncio.get_running_loop()
+            sentinel = object()
+            while True:
+                chunk = await loop.run_in_executor(None, next, it, sentinel)
+                if chunk is sentinel:
+                    return
+                yield chunk
+        return agen()
+    return await asyncio.to_thread(completion, model, messages, **kw)
+
+
+def batch_completion(model: str, messages: list[list[dict]], *, api_base: str | None = None, max_tokens: int = 128,
+                     temperature: float = 0.0, **kw) -> list[ModelResponse]:
+    """LiteLLM ``batch_completion``: one response per conversation.  In-process
+    engine: ONE batched generation (continuous batching over all of them);
+    HTTP: the requests run concurrently."""
+    base = api_base if api_base is not None else globals()["api_base"]
+    if _is_local(base):
+        eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+        ids = [tok.apply_chat_template(m) for m in messages]
+        outs = eng.generate(ids, max_new_tokens=max_tokens, temperature=temperature, top_p=kw.get("top_p", 1.0),
+                            top_k=kw.get("top_k", 0), seed=kw.get("seed", 0))
+        return [ModelResponse([Choice(Message(tok.decode([t for t in o if t not in eng.eos_ids])))], model=model,
+                              usage={"prompt_tokens": len(i), "completion_tokens": len(o)})
+                for i, o in zip(ids, outs)]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=min(16, max(1, len(messages)))) as ex:
+        futs = [ex.submit(completion, model, m, api_base=base, max_tokens=max_tokens, temperature=temperature, **kw)
+                for m in messages]
+        return [f.result() for f in futs]

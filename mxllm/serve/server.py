@@ -136,8 +136,10 @@ def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = 
 
     async def _stream(ids, body, chat: bool):
         r = engine.submit(ids, SamplingParams(
-            max_new_tokens=int(body.get("max_tokens") or 128), temperature=float(body.get("temperature", 0.0) or 0.0),
-            top_p=float(body.get("top_p", 1.0) or 1.0), stop_ids=_stop_ids(tokenizer, body.get("stop"))))
+            max_new_tokens=int(body.get("max_tokens") or body.get("max_completion_tokens") or 128),
+            temperature=float(body.get("temperature", 0.0) or 0.0), top_p=float(body.get("top_p", 1.0) or 1.0),
+            top_k=int(body.get("top_k", 0) or 0), stop_ids=_stop_ids(tokenizer, body.get("stop")),
+            seed=int(body.get("seed", 0) or 0)))
         sent = 0
         cid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
         while True:

@@ -157,6 +157,39 @@ def test_local_inproc_route(tiny_engine):
         client.unregister_local("tiny-local")
 
 
+def test_http_stream_and_async_and_batch(server):
+    """LiteLLM streaming (SSE deltas), acompletion and batch_completion over HTTP."""
+    import asyncio
+
+    msgs = [{"role": "user", "content": "hello"}]
+    full = client.completion("tiny-test", msgs, api_base=server, api_key="sekret", max_tokens=6, timeout=30)
+    chunks = list(client.completion("tiny-test", msgs, api_base=server, api_key="sekret", max_tokens=6,
+                                    timeout=30, stream=True))
+    assert chunks[-1].choices[0].finish_reason is not None
+    streamed = "".join(c.choices[0].delta.content or "" for c in chunks)
+    assert streamed == full.choices[0].message.content  # greedy: same text either way
+    r = asyncio.run(client.acompletion("tiny-test", msgs, api_base=server, api_key="sekret", max_tokens=6,
+                                       timeout=30))
+    assert r.choices[0].message.content == full.choices[0].message.content
+    many = client.batch_completion("tiny-test", [msgs, [{"role": "user", "content": "other"}]], api_base=server,
+                                   api_key="sekret", max_tokens=4, timeout=30)
+    assert len(many) == 2 and all(isinstance(m.choices[0].message.content, str) for m in many)
+
+
+def test_local_stream_and_batch(tiny_engine):
+    client.register_local("tiny-local2", tiny_engine, ByteTokenizer(512))
+    try:
+        msgs = [{"role": "user", "content": "abc"}]
+        full = client.completion("tiny-local2", msgs, api_base="local", max_tokens=5)
+        chunks = list(client.completion("tiny-local2", msgs, api_base="local", max_tokens=5, stream=True))
+        assert "".join(c.choices[0].delta.content or "" for c in chunks) == full.choices[0].message.content
+        outs = client.batch_completion("tiny-local2", [msgs, msgs], api_base="local", max_tokens=5)
+        assert [o.choices[0].message.content for o in outs] == [full.choices[0].message.content] * 2
+    finally:
+        client.unregister_local("tiny-local2")
+        tiny_engine.stop()
+
+
 def test_fp8_weight_engine_cpu():
     """Serving with e4m3 projection weights (CPU reference path): the model keeps
     generating and its prefill logits stay close to the bf16 model's."""
