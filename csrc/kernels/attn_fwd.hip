@@ -269,6 +269,360 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// D = 128 forward, software-pipelined (opt-in: MXLLM_ATTN_FWD=p; measured SLOWER than the kernel
+// above -- 0.300 vs 0.265 ms at B2 S2048 Hq64 Hkv8, see profiles/r1d_experiments.md -- and kept for
+// the record and further work).  One wave per SIMD owning the whole register file and 64 query rows (two 32-row blocks
+// that share every K / V^T fragment read, so LDS reads, LDS-DMA and address work per MFMA halve),
+// 4 waves = 256 rows per workgroup.  Per 64-key tile t a wave runs two phases:
+//   A(t): S(t) = K(t) Q^T for both row blocks (32 MFMAs; K fragments three k-steps ahead)
+//   B(t): O += V(t-1) P(t-1) (32 MFMAs)  ||  the whole softmax of S(t) -> P(t) (bf16) and l
+// so the softmax VALU of one tile runs under the PV MFMAs of the previous one instead of between
+// a wave's own dependent MFMA chains.  The deferred rescale (guide T13) decided in B(t) is
+// applied to O at the start of B(t+1), between PV(t-1) and PV(t).  K / V tiles arrive by
+// buffer_load ... lds (per-lane source offsets loop-invariant, the tile step one VALU add; rows
+// past Sk come back as zeros from the descriptor's range check) into 2-slot rings, issued one
+// tile ahead right after the tile's single barrier.
+// register-class pins: O stays in AGPRs (touched by VALU only in the rare rescale, which must not
+// turn the loop-carried O into a VGPR phi), S / P values in VGPRs (VALU softmax)
+__device__ __forceinline__ void pin_a(f32x16& v) { asm volatile("" : "+a"(v)); }
+__device__ __forceinline__ void pin_v(f32x16& v) { asm volatile("" : "+v"(v)); }
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+attn_fwd_p_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                  uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
+                  int causal_off, float sl, int ldo) {
+  constexpr int D = 128, BM = 256, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int TILE = BN * ROWB;  // 16 KiB
+  constexpr int KPF = 2;           // K / Q k-steps in flight
+  // LDS: K slot 0 | K slot 1 | V slot 0 | V slot 1 | Q image (256 rows; Q fragments are read
+  // per k-step like K's, which keeps the register file for S, P and O)
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + BM * ROWB];
+  typedef __attribute__((address_space(3))) void* lptr_t;
+
+  const int nqb = (S + BM - 1) / BM;
+  const int BH = B * Hq;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = nqb - 1 - bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / Hq, h = bh % Hq;
+  const int hk = h / (Hq / Hkv);
+  const uint16_t* Qp = Q + ((size_t)(b * Hq + h) * S) * D;
+  const uint16_t* Kp = K + ((size_t)(b * Hkv + hk) * Sk) * D;
+  const uint16_t* Vp = V + ((size_t)(b * Hkv + hk) * Sk) * D;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = qb * BM;
+  const int qw = q0 + 64 * w;  // first row of this wave
+
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM + causal_off);
+  const int T = kend > 0 ? (kend + BN - 1) / BN : 0;
+
+  // K / V tile pieces: 16 x 1 KiB per tile, 4 per wave; lane-linear LDS writes, so the XOR swizzle
+  // is applied by permuting each lane's source chunk
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)Kp, 0, Sk * ROWB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)Vp, 0, Sk * ROWB, 0x00020000);
+  int voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int seg = w * 4 + i;
+    const int row = seg * 4 + (lane >> 4), slot = lane & 15;
+    voff[i] = row * ROWB + 16 * (slot ^ swz<CH>(row));
+  }
+  {  // Q image: 64 x 1 KiB pieces, 16 per wave (rows past S read as zeros; never stored)
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(Qp + (size_t)q0 * D), 0,
+                                                                         (S - q0) * ROWB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int seg = w * 16 + i;
+      const int row = seg * 4 + (lane >> 4), slot = lane & 15;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(smem + 4 * TILE + seg * 1024), 16,
+                                               row * ROWB + 16 * (slot ^ swz<CH>(row)), 0, 0, 0);
+    }
+  }
+  auto dma_k = [&](int kt, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(smem + slot * TILE + (w * 4 + i) * 1024), 16,
+                                               voff[i] + kt * TILE, 0, 0, 0);
+  };
+  auto dma_v = [&](int kt, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(smem + (2 + slot) * TILE + (w * 4 + i) * 1024), 16,
+                                               voff[i] + kt * TILE, 0, 0, 0);
+  };
+
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t ka_base[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) ka_base[s] = lds0 + r * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(r));
+  uint32_t qa_base[KS];  // Q image rows 64w + r (+32 for the second block: an immediate)
+#pragma unroll
+  for (int s = 0; s < KS; ++s) qa_base[s] = ka_base[s] + 4 * TILE + 64 * w * ROWB;
+  uint32_t va_base[DB][2];
+#pragma unroll
+  for (int db = 0; db < DB; ++db) {
+    const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+    const int rA = 4 * hh + tq, rB = 8 + 4 * hh + tq;
+    va_base[db][0] = lds0 + 2 * TILE + rA * ROWB + 16 * (chunk ^ swz<CH>(rA)) + 8 * (tp & 1);
+    va_base[db][1] = lds0 + 2 * TILE + rB * ROWB + 16 * (chunk ^ swz<CH>(rB)) + 8 * (tp & 1);
+  }
+
+  f32x16 o[2][DB];
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+    for (int d = 0; d < DB; ++d)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o[qi][d][j] = 0.f;
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) pin_a(o[qi][d]);
+  f32x16 sa[2][2];   // S(t) of the current tile: [row block][32-key half]
+  u16x8 pb[2][4];    // P of the previous tile, bf16: [row block][16-key step]
+  float m_i[2] = {-1e30f, -1e30f}, l_i[2] = {0.f, 0.f};
+  float alpha_p[2] = {1.f, 1.f};
+  bool resc_p = false;  // O rescale pending (decided in B(t), applied before PV(t))
+
+  // ---- phase A: S(t) = K(t) Q^T (K slot KSLOT)
+  auto phase_a = [&](int kso) __attribute__((always_inline)) {
+    uint32_t kad[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) kad[s] = ka_base[s] + kso;
+    // per k-step: K rows n*32 + r (shared by both row blocks) and Q rows 64w + 32qi + r (shared
+    // by both key halves); the Q image row 64w + 32qi + r has the same swizzle as K row r
+    u16x8 kf[KS][2], qf[KS][2];
+#pragma unroll
+    for (int s = 0; s < KPF; ++s) {
+      kf[s][0] = rd128_off(kad[s], 0);
+      kf[s][1] = rd128_off(kad[s], 32 * ROWB);
+      qf[s][0] = rd128_off(qa_base[s], 0);
+      qf[s][1] = rd128_off(qa_base[s], 32 * ROWB);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + KPF < KS) {
+        kf[s + KPF][0] = rd128_off(kad[s + KPF], 0);
+        kf[s + KPF][1] = rd128_off(kad[s + KPF], 32 * ROWB);
+        qf[s + KPF][0] = rd128_off(qa_base[s + KPF], 0);
+        qf[s + KPF][1] = rd128_off(qa_base[s + KPF], 32 * ROWB);
+      }
+      lds_wait_le(4 * ((s + KPF < KS ? s + KPF : KS - 1) - s));
+      pin(kf[s][0]);
+      pin(kf[s][1]);
+      pin(qf[s][0]);
+      pin(qf[s][1]);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) {
+          if (s == 0) {
+            f32x16 z;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) z[j] = 0.f;
+            sa[qi][n] = mfma32(kf[s][n], qf[s][qi], z);
+          } else {
+            sa[qi][n] = mfma32(kf[s][n], qf[s][qi], sa[qi][n]);
+          }
+        }
+    }
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) pin_v(sa[qi][n]);
+  };
+
+  // ---- PV(t-1) from V slot VSLOT with pb
+  auto pv = [&](int vso, auto&& hook) __attribute__((always_inline)) {
+    uint32_t vad[DB][2];
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      vad[db][0] = va_base[db][0] + vso;
+      vad[db][1] = va_base[db][1] + vso;
+    }
+    u16x4 fv[4][DB][2];
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      fv[0][db][0] = trd_off(vad[db][0], 0);
+      fv[0][db][1] = trd_off(vad[db][1], 0);
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      if (st + 1 < 4) {
+        const int off = (32 * ((st + 1) >> 1) + 16 * ((st + 1) & 1)) * ROWB;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          fv[st + 1][db][0] = trd_off(vad[db][0], off);
+          fv[st + 1][db][1] = trd_off(vad[db][1], off);
+        }
+      }
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        lds_wait_le((st + 1 < 4 ? 2 * DB : 0) + 2 * (DB - 1 - db));
+        pin(fv[st][db][0]);
+        pin(fv[st][db][1]);
+        const u16x4 va = fv[st][db][0], vc = fv[st][db][1];
+        const u16x8 a = u16x8{va[0], va[1], va[2], va[3], vc[0], vc[1], vc[2], vc[3]};
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) o[qi][db] = mfma32(a, pb[qi][st], o[qi][db]);
+      }
+      hook(st);
+    }
+  };
+
+  // ---- softmax of S(t) -> pb, l (and the rescale decision for O), in pieces that the PV(t-1)
+  // steps interleave: mask (diagonal / inactive / tail tiles, its own wave-uniform branch before
+  // PV), row max per block, the rescale decision, exps + row sums + bf16 P per block
+  auto mask = [&](int kt) __attribute__((always_inline)) {
+    const bool need_mask = (kt * BN + BN > Sk) || (CAUSAL && (kt * BN + BN - 1 > qw + causal_off));
+    if (need_mask) {
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        const int qrow = qw + 32 * qi + r;
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int key = kt * BN + n * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+            const bool dead = (key >= Sk) | (CAUSAL & (key > qrow + causal_off));
+            sa[qi][n][j] = dead ? -INFINITY : sa[qi][n][j];
+          }
+      }
+    }
+  };
+  float mt[2];
+  auto sm_max = [&](int qi) __attribute__((always_inline)) {
+    float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      m0 = fmaxf(m0, sa[qi][0][j]);
+      m1 = fmaxf(m1, sa[qi][1][j]);
+    }
+    float mx = fmaxf(m0, m1);
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    mt[qi] = mx * sl;
+  };
+  auto sm_decide = [&]() __attribute__((always_inline)) {
+    constexpr float kThr = 8.f;
+    const bool flag = __any((mt[0] > m_i[0] + kThr) | (mt[1] > m_i[1] + kThr));
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      const float mnew = flag ? fmaxf(m_i[qi], mt[qi]) : m_i[qi];
+      alpha_p[qi] = __builtin_amdgcn_exp2f(m_i[qi] - mnew);
+      m_i[qi] = mnew;
+    }
+    resc_p = flag;
+  };
+  auto sm_exp = [&](int qi) __attribute__((always_inline)) {
+    const float nm = -m_i[qi];
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[qi][n][j], sl, nm));
+        sa[qi][n][j] = p;
+        if (j & 1) s1 += p; else s0 += p;
+      }
+    l_i[qi] = l_i[qi] * alpha_p[qi] + (s0 + s1);
+  };
+  auto sm_pack = [&](int qi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[qi][st][j] = f2bf(sa[qi][st >> 1][8 * (st & 1) + j]);
+  };
+  // the softmax pieces placed after PV step st
+  auto sm_hook = [&](int st) __attribute__((always_inline)) {
+    if (st == 0) { sm_max(0); sm_max(1); }
+    if (st == 1) { sm_decide(); sm_exp(0); }
+    if (st == 2) sm_exp(1);
+    if (st == 3) { sm_pack(0); sm_pack(1); }
+  };
+  auto softmax = [&](int kt) __attribute__((always_inline)) {
+    mask(kt);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) sm_hook(st);
+  };
+  auto rescale = [&]() __attribute__((always_inline)) {
+    if (__builtin_expect(resc_p, 0)) {
+      asm volatile("s_nop 0" ::: "memory");  // keeps the rare rescale a real branch (no if-conversion)
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int d = 0; d < DB; ++d) o[qi][d] *= alpha_p[qi];
+    }
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int d = 0; d < DB; ++d) pin_a(o[qi][d]);
+  };
+
+  if (T > 0) {
+    dma_k(0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's Q and K(0) pieces
+    __builtin_amdgcn_s_barrier();
+    dma_v(0, 0);
+    if (T > 1) dma_k(1, 1);
+    phase_a(0);
+    softmax(0);
+  }
+  // tile t: [wait own DMA, barrier, DMA V(t) + K(t+1)] A(t) from K slot t&1, B(t) = PV(t-1) from
+  // V slot (t-1)&1 + softmax(t).  One body with run-time slots (a VALU add per fragment base per
+  // tile) so the loop-carried accumulators keep one register assignment.
+  for (int t = 1; t < T; ++t) {
+    const int par = t & 1;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int d = 0; d < DB; ++d) pin_a(o[qi][d]);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_barrier();
+    dma_v(t, par);
+    if (t + 1 < T) dma_k(t + 1, par ^ 1);
+    phase_a(par * TILE);
+    mask(t);
+    rescale();
+    pv((par ^ 1) * TILE, sm_hook);
+  }
+  if (T > 0) {  // PV of the last tile
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_barrier();
+    rescale();
+    pv(((T - 1) & 1) * TILE, [](int) {});
+  }
+
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_i[qi]), __float_as_uint(l_i[qi]), false, false);
+    const float l_tot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    const int qrow = qw + 32 * qi + r;
+    if (qrow < S) {
+      uint16_t* op = O + ((size_t)b * S + qrow) * (size_t)ldo + (size_t)h * D;
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int d = db * 32 + 8 * gq + 4 * hh;
+          u16x4 v4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v4[j] = f2bf(o[qi][db][4 * gq + j] * inv);
+          *reinterpret_cast<u16x4*>(op + d) = v4;
+        }
+      if (hh == 0) LSE[(size_t)(b * Hq + h) * S + qrow] = m_i[qi] + __log2f(l_tot);
+    }
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -282,6 +636,16 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   if (Hkv <= 0 || Hq % Hkv || ldo < Hq * D || ldo % 8) return -1;
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
+  static const bool pipe = [] {  // MXLLM_ATTN_FWD=p: the software-pipelined 64-row-per-wave kernel (A/B)
+    const char* e = getenv("MXLLM_ATTN_FWD");
+    return e && e[0] == 'p';
+  }();
+  if (D == 128 && pipe) {
+    const unsigned grid = ((S + 255) / 256) * B * Hq;
+    if (causal) attn_fwd_p_kernel<true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
+    else attn_fwd_p_kernel<false><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
+    return (int)hipGetLastError();
+  }
   static const int nw128 = [] {  // MXLLM_ATTN_FWD_WAVES=8: the 8-wave (256-row) variant for D = 128 (A/B)
     const char* e = getenv("MXLLM_ATTN_FWD_WAVES");
     return (e && e[0] == '8') ? 8 : 4;

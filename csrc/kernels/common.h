@@ -105,21 +105,28 @@ __device__ __forceinline__ u16x4 trd_off(uint32_t base, int off) {
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(base + (uint32_t)off));
   return v;
 }
+// 16-B row read at base + off (immediate when constant), same waitcnt contract as trd_off
+__device__ __forceinline__ u16x8 rd128_off(uint32_t base, int off) {
+  u16x8 v;
+  if (__builtin_constant_p(off) && off >= 0 && off < 65536)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(off));
+  else
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(base + (uint32_t)off));
+  return v;
+}
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // at most n LDS operations of this wave still outstanding (n folds to a constant after unrolling)
 __device__ __forceinline__ void lds_wait_le(int n) {
   switch (n) {
-    case 14: asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory"); break;
+#define MX_LGKM(N) case N: asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory"); break;
+    MX_LGKM(15) MX_LGKM(14) MX_LGKM(13) MX_LGKM(12) MX_LGKM(11) MX_LGKM(10) MX_LGKM(9) MX_LGKM(8)
+    MX_LGKM(7) MX_LGKM(6) MX_LGKM(5) MX_LGKM(4) MX_LGKM(3) MX_LGKM(2) MX_LGKM(1)
+#undef MX_LGKM
     default: asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); break;
   }
 }
 __device__ __forceinline__ void pin(u16x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(u16x8& v) { asm volatile("" : "+v"(v)); }
 // byte address of a __shared__ object in the LDS aperture
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(size_t)(__attribute__((address_space(3))) const char*)p;

@@ -156,6 +156,8 @@ ATTN_SHAPES = [
     (1, 4, 2, 77, 77, 32, True),
     (2, 16, 2, 512, 512, 128, True),
     (1, 8, 2, 64, 320, 128, True),   # prefill with a cached prefix (bottom-right causal)
+    (1, 4, 2, 100, 300, 128, False),  # non-causal, key tail past the last full 64-key tile
+    (1, 4, 1, 700, 700, 128, True),   # several 256-row query blocks, partial last block
 ]
 
 
