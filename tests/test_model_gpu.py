@@ -218,6 +218,43 @@ def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["value"] > 0
 
 
+@pytest.mark.parametrize("parallel", ["ddp", "zero3"])
+def test_two_node_scripts_on_one_gpu(gpu, parallel):
+    """BASELINE config 5 rehearsal on the GPU: scripts/run_node0.sh + run_node1.sh
+    start two torchrun agents ('nodes', one rank each) that rendezvous on
+    127.0.0.1 and train the tiny Llama on the box's one GPU through the HIP
+    kernels (gloo between the two ranks: RCCL needs one GPU per rank).  ZeRO-3
+    with activation checkpointing shards parameters / gradients / optimizer over
+    the two nodes.  Reference: /root/reference/scripts/run_node0.sh:10-16."""
+    import socket
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MXLLM_BACKEND="gloo", NPROC_PER_NODE="1", NNODES="2", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), MXLLM_PG_TIMEOUT_S="120")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        env.pop(k, None)
+    args = ["--model", "tiny-d128", "--steps", "3", "--seq-len", "128", "--micro-batch", "1", "--log-every", "1",
+            "--finetune", "full", "--parallel", parallel]
+    if parallel == "zero3":
+        args += ["--activation-checkpointing", "1"]
+    p1 = subprocess.Popen(["bash", "scripts/run_node1.sh"] + args, cwd=root, env=env, stdout=subprocess.PIPE,
+                          stderr=subprocess.STDOUT, text=True)
+    try:
+        p0 = subprocess.run(["bash", "scripts/run_node0.sh"] + args, cwd=root, env=env, capture_output=True,
+                            text=True, timeout=240)
+        out1, _ = p1.communicate(timeout=120)
+    finally:
+        if p1.poll() is None:
+            p1.kill()
+    log = p0.stdout + p0.stderr
+    assert p0.returncode == 0 and p1.returncode == 0, log[-2000:] + out1[-2000:]
+    assert "step 2" in log and "cuda" in log
+
+
 def test_zero3_emulated_world8_tiny_gpu(gpu):
     """ZeRO-3 with activation checkpointing and the world-8 emulation on the GPU
     (HIP kernels, direct dW into the unit gradient buffer, async reduce path)."""
