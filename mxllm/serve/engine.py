@@ -87,6 +87,12 @@ class Engine:
         self.device = device or model.tok_emb.device
         self.max_batch = max_batch
         self.max_seq = min(max_seq, self.cfg.max_seq_len)
+        if self.device.type == "cuda":
+            # tuned hipBLASLt/rocBLAS solution table (read-only; incl. the 70B decode shapes,
+            # bench/tune_decode_gemms.py); MXLLM_GEMM_TUNING=0 keeps the library defaults
+            from ..utils import gemm_tuning
+
+            gemm_tuning.enable()
         if use_graphs is None:
             use_graphs = self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_GRAPHS", "1") != "0"
             if self.tp is not None:  # RCCL collectives are graph-capturable, gloo's are not
