@@ -50,7 +50,7 @@ class RunConfig:
     request_timeout: float = 120.0
     num_retries: int = 3
     # fine-tuning
-    model: str = "tiny"
+    model: str = "tiny"  # preset name, or a Hugging Face Llama directory (config.json + safetensors)
     finetune: str = "lora"  # lora | full
     parallel: str = "ddp"  # ddp | zero1 (sharded optimizer) | zero3 (sharded everything)
     sequence_parallel: int = 1  # Ulysses SP degree (ranks per sequence); world = dp x sp
@@ -69,6 +69,7 @@ class RunConfig:
     activation_checkpointing: bool = False
     ckpt_dir: str = ""
     save_every: int = 0
+    save_hf: str = ""  # at the end: write the model as a Hugging Face Llama directory (LoRA merged)
     resume: bool = True
     log_every: int = 10
     metrics_file: str = ""

@@ -329,7 +329,8 @@ class Zero3Trainer:
     """Same ``train_step`` contract as :class:`mxllm.train.trainer.Trainer`."""
 
     def __init__(self, cfg, env: DistEnv, optim=None, *, seed: int = 0, activation_checkpointing: bool = False,
-                 process_group=None, emulate_world: int = 0, max_inflight: int | None = None):
+                 process_group=None, emulate_world: int = 0, max_inflight: int | None = None,
+                 init_from: str | None = None):
         from ..models.llama import Llama
         from ..train.trainer import OptimConfig
 
@@ -372,7 +373,7 @@ class Zero3Trainer:
             u.grad_shard = self.grads[off:off + u.shard_numel]
             u.master_view = self.master[off:off + u.shard_numel]
             off += u.shard_numel
-        self._materialize_shards(seed)
+        self._materialize_shards(seed, init_from)
         self.master.copy_(self.shard_params)
         self._by_storage: dict[int, Unit] = {}
         self._param_unit: dict[int, Unit] = {}
@@ -401,11 +402,22 @@ class Zero3Trainer:
 
     # ---------------------------------------------------------------- init
     @torch.no_grad()
-    def _materialize_shards(self, seed: int):
-        """Initialise every unit on device (per-unit seed: identical on every rank),
-        keep this rank's slice, free the rest — never the whole model at once."""
+    def _materialize_shards(self, seed: int, init_from: str | None = None):
+        """Initialise every unit on device (per-unit seed: identical on every rank) or
+        read it from a Hugging Face checkpoint directory (``init_from``,
+        mxllm/models/hf.py), keep this rank's slice, free the rest — never the whole
+        model at once."""
+        fill = None
+        if init_from:
+            from ..models.hf import hf_unit_filler
+
+            fill = hf_unit_filler(init_from, self.model.cfg)
         for u in self.units:
-            full = init_unit_full(u.uid, u.names, u.numels, u.full_numel, seed, self.device)
+            if fill is not None:
+                full = torch.zeros(u.full_numel, dtype=torch.bfloat16, device=self.device)
+                fill(u.names, u.shapes, full)
+            else:
+                full = init_unit_full(u.uid, u.names, u.numels, u.full_numel, seed, self.device)
             u.shard.copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
             del full
         self.units[0].materialize()  # norms stay resident

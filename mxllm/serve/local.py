@@ -28,15 +28,17 @@ def preset_for(model_name: str, device: torch.device) -> str:
 def ensure_local_engine(model_name: str, device, engine_model: str = "", max_batch: int = 8, max_seq: int = 2048,
                         tokenizer_path: str = "", checkpoint: str = "", seed: int = 0, weights: str = "bf16"):
     from ..data.tokenizer import get_tokenizer
-    from ..models import Llama, get_config
+    from ..models import build_model, tokenizer_path_for
 
     if model_name in client._LOCAL:
         return client._LOCAL[model_name]
     device = torch.device(device)
+    # a preset name, or a Hugging Face Llama directory (real weights + its tokenizer.json)
     preset = engine_model or preset_for(model_name, device)
-    cfg = get_config(preset)
     log.info("local engine: %s (%s) on %s", model_name, preset, device)
-    model = Llama(cfg, device=device, seed=seed)
+    model = build_model(preset, device=device, seed=seed)
+    cfg = model.cfg
+    tokenizer_path = tokenizer_path_for(preset, tokenizer_path)
     if checkpoint:
         from ..train.checkpoint import load_model_weights
 
@@ -47,8 +49,6 @@ def ensure_local_engine(model_name: str, device, engine_model: str = "", max_bat
 
         quantize_model_fp8_(model)
     tok = get_tokenizer(cfg.vocab_size, tokenizer_path or None, cfg.bos_id, cfg.eos_id)
-    if cfg.vocab_size > 512 and not tokenizer_path:
-        max_seq = max_seq
     eng = Engine(model, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id,))
     client.register_local(model_name, eng, _Truncating(tok, max_seq - 64))
     return client._LOCAL[model_name]

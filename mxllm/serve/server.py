@@ -178,12 +178,14 @@ def build_default(model: str = "tiny", device: str | None = None, max_batch: int
     shard (mxllm/parallel/tensor.py) of the model; the full model is built (or
     loaded) on the rank's GPU, sliced and freed."""
     from ..data.tokenizer import get_tokenizer
-    from ..models import Llama, get_config
+    from ..models import build_model, tokenizer_path_for
 
-    cfg = get_config(model)
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
-    m = Llama(cfg, device=device, seed=seed)
+    # ``model``: a preset name or a Hugging Face Llama directory (its weights and tokenizer.json)
+    m = build_model(model, device=device, seed=seed)
+    cfg = m.cfg
+    tokenizer_path = tokenizer_path_for(model, tokenizer_path)
     if checkpoint:
         from ..train.checkpoint import load_model_weights
 
@@ -209,7 +211,8 @@ def build_default(model: str = "tiny", device: str | None = None, max_batch: int
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default=os.environ.get("MXLLM_MODEL", "tiny"))
+    ap.add_argument("--model", default=os.environ.get("MXLLM_MODEL", "tiny"),
+                    help="preset name, or a Hugging Face Llama directory (config.json + safetensors + tokenizer.json)")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--max-batch", type=int, default=8)
@@ -245,7 +248,7 @@ def main(argv=None):
             finally:
                 runtime.cleanup()
             return
-    app = build_app(eng, tok, a.served_name or a.model, a.api_key)
+    app = build_app(eng, tok, a.served_name or os.path.basename(os.path.normpath(a.model)), a.api_key)
     import uvicorn
 
     try:

@@ -50,20 +50,39 @@ def cleanup():
 
 
 def build_trainer(run, env):
-    from mxllm.models import Llama, get_config
+    """``run.model``: a preset (random init) or a Hugging Face Llama directory (its
+    weights; ZeRO-3 reads them unit by unit, so no rank holds the whole model)."""
+    from mxllm.models import build_model, is_hf_dir, model_config
     from mxllm.train.trainer import OptimConfig, Trainer
 
-    cfg = get_config(run.model)
+    cfg = model_config(run.model)
     lora_r = run.lora_r if run.finetune == "lora" else 0
     opt = OptimConfig(lr=run.lr, weight_decay=run.weight_decay, grad_clip=run.grad_clip,
                       warmup_steps=run.warmup_steps, total_steps=run.steps)
     if run.parallel == "zero3":
         from mxllm.parallel.zero3 import Zero3Trainer
 
-        return Zero3Trainer(cfg, env, opt, seed=run.seed, activation_checkpointing=run.activation_checkpointing)
-    model = Llama(cfg, device=env.device, lora_r=lora_r, lora_alpha=run.lora_alpha, seed=run.seed,
-                  activation_checkpointing=run.activation_checkpointing)
+        return Zero3Trainer(cfg, env, opt, seed=run.seed, activation_checkpointing=run.activation_checkpointing,
+                            init_from=run.model if is_hf_dir(run.model) else None)
+    model = build_model(run.model, device=env.device, lora_r=lora_r, lora_alpha=run.lora_alpha, seed=run.seed,
+                        activation_checkpointing=run.activation_checkpointing)
     return Trainer(model, env, opt, bucket_mb=run.bucket_mb, shard_optimizer=run.parallel == "zero1")
+
+
+def export_hf(run, trainer, rank):
+    """--save-hf DIR: the trained model as a Hugging Face Llama checkpoint (LoRA merged;
+    ZeRO-3 gathers unit by unit to rank 0).  Collective for ZeRO-3 / ZeRO-1."""
+    from mxllm.models import save_hf_llama
+
+    if run.parallel == "zero3":
+        state = trainer.full_state_dict()
+        if rank == 0:
+            save_hf_llama(state, run.save_hf, cfg=trainer.model.cfg)
+    elif rank == 0:
+        save_hf_llama(trainer.model, run.save_hf)
+    runtime.barrier()
+    if rank == 0:
+        logging.info(f"Hugging Face checkpoint written to {run.save_hf}")
 
 
 def main(argv=None):
@@ -78,7 +97,7 @@ def main(argv=None):
 
         from mxllm.data.loader import TokenLoader, pack_texts
         from mxllm.data.tokenizer import get_tokenizer
-        from mxllm.models import get_config
+        from mxllm.models import model_config, tokenizer_path_for
         from mxllm.train import checkpoint
 
         trainer = build_trainer(run, env)
@@ -99,8 +118,9 @@ def main(argv=None):
             else:  # Ulysses all-to-all around attention
                 trainer.model.set_sequence_parallel(sp_group)
                 shard = shard_sequence
-        mcfg = get_config(run.model)
-        tok = get_tokenizer(mcfg.vocab_size, run.tokenizer or None, mcfg.bos_id, mcfg.eos_id)
+        mcfg = model_config(run.model)
+        tok = get_tokenizer(mcfg.vocab_size, tokenizer_path_for(run.model, run.tokenizer or None), mcfg.bos_id,
+                            mcfg.eos_id)
         texts, _ = load_text_dataset(run.dataset, run.split, run.n_rows, run.seed)
         tokens = pack_texts(texts, tok, getattr(tok, "eos_id", mcfg.eos_id))
         loader = TokenLoader(tokens, run.seq_len, run.micro_batch, data_rank, data_world, run.seed, env.device)
@@ -165,6 +185,8 @@ def main(argv=None):
         loader.close()
         if monitor is not None:
             monitor.stop()
+        if run.save_hf:
+            export_hf(run, trainer, rank)
         runtime.barrier()
     except Exception as e:
         logging.error(f"An error occurred in the main function: {e}")

@@ -499,3 +499,40 @@ def test_tp_engine_two_ranks_one_gpu(gpu):
     err = ((logits - ref_logits).norm() / ref_logits.norm()).item()
     assert err < 2e-2, err
     assert len(outs[0]) == 4
+
+
+def test_hf_checkpoint_on_gpu_matches_transformers(gpu, tmp_path):
+    """A Hugging Face Llama directory loaded onto the GPU (bf16, HIP kernels) against
+    transformers' fp32 CPU forward of the same checkpoint; then one LoRA training
+    step on it and a merged export that transformers reads back."""
+    transformers = pytest.importorskip("transformers")
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from mxllm.models import load_hf_llama, save_hf_llama
+
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=131072,
+                      rope_theta=500000.0, rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                                         "high_freq_factor": 4.0,
+                                                         "original_max_position_embeddings": 8192},
+                      rms_norm_eps=1e-5, tie_word_embeddings=False)
+    torch.manual_seed(0)
+    ref = LlamaForCausalLM(cfg).float().eval()
+    ref.save_pretrained(tmp_path / "src", safe_serialization=True)
+    m = load_hf_llama(str(tmp_path / "src"), device=gpu, dtype=torch.bfloat16, lora_r=16)
+    ids = torch.randint(0, 512, (2, 256))
+    with torch.no_grad():
+        want = ref(ids).logits
+        got = m(ids.to(gpu)).float().cpu()
+    assert _rel(got, want) < 2e-2
+    opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=1e-2)
+    loss = m(ids.to(gpu), labels=ids.to(gpu))
+    loss.backward()
+    opt.step()
+    m.sync_adapters_()
+    save_hf_llama(m, str(tmp_path / "out"))
+    back = LlamaForCausalLM.from_pretrained(str(tmp_path / "out")).float().eval()
+    with torch.no_grad():
+        got2 = m(ids.to(gpu)).float().cpu()
+        want2 = back(ids).logits
+    assert _rel(got2, want2) < 2e-2
