@@ -136,11 +136,13 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const int kld = min(key, Sk - 1);
 
   // K image (whole WG) + per-wave K/V fragments (clamped rows; masked later)
+  if constexpr (DQM != 3) {  // the split mode computes dQ in attn_bwd_dq_kernel: no K image here
 #pragma unroll
-  for (int i = 0; i < LPT_K; ++i) {
-    const int c = tid + 256 * i, row = c / CH, ch = c % CH, kk = min(k0 + row, Sk - 1);
-    *reinterpret_cast<u16x8*>(kimg + row * ROWB + 16 * (ch ^ swzb<CH>(row))) =
-        *reinterpret_cast<const u16x8*>(Kp + (size_t)kk * D + ch * 8);
+    for (int i = 0; i < LPT_K; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH, kk = min(k0 + row, Sk - 1);
+      *reinterpret_cast<u16x8*>(kimg + row * ROWB + 16 * (ch ^ swzb<CH>(row))) =
+          *reinterpret_cast<const u16x8*>(Kp + (size_t)kk * D + ch * 8);
+    }
   }
   u16x8 kf[KS], vf[KS];
 #pragma unroll
