@@ -318,3 +318,83 @@ def batch_completion(model: str, messages: list[list[dict]], *, api_base: str | 
         futs = [ex.submit(completion, model, m, api_base=base, max_tokens=max_tokens, temperature=temperature, **kw)
                 for m in messages]
         return [f.result() for f in futs]
+
+
+@dataclass
+class EmbeddingResponse:
+    data: list
+    model: str = ""
+    usage: dict = field(default_factory=dict)
+    object: str = "list"
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+def embedding(model: str, input, *, api_base: str | None = None, api_key: str | None = None,
+              timeout: float | None = None, **kw) -> EmbeddingResponse:
+    """LiteLLM ``embedding``: ``input`` a string or a list of strings; ``.data[i]["embedding"]``
+    (mean-pooled final hidden states of the served model, unit norm)."""
+    base = api_base if api_base is not None else globals()["api_base"]
+    texts = [input] if isinstance(input, str) else list(input)
+    if _is_local(base):
+        eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+        seqs = [tok.encode(t) for t in texts]
+        vec = eng.embed(seqs)
+        n = sum(len(q) for q in seqs)
+        return EmbeddingResponse([{"object": "embedding", "index": i, "embedding": v.tolist()}
+                                  for i, v in enumerate(vec)], model=model,
+                                 usage={"prompt_tokens": n, "total_tokens": n})
+    import httpx
+
+    key = api_key or globals()["api_key"] or os.environ.get("OPENAI_API_KEY")
+    url = base.rstrip("/")
+    if not url.endswith("/embeddings"):
+        url += "/embeddings"
+    headers = {"Authorization": f"Bearer {key}"} if key else {}
+    r = httpx.post(url, json={"model": model, "input": texts}, headers=headers,
+                   timeout=timeout if timeout is not None else request_timeout)
+    if r.status_code != 200:
+        raise CompletionError(f"HTTP {r.status_code}: {r.text[:200]}")
+    j = r.json()
+    return EmbeddingResponse(j["data"], model=j.get("model", model), usage=j.get("usage", {}))
+
+
+@dataclass
+class TextChoice:
+    text: str
+    index: int = 0
+    finish_reason: str | None = "stop"
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+def text_completion(model: str, prompt: str, *, api_base: str | None = None, api_key: str | None = None,
+                    timeout: float | None = None, max_tokens: int = 128, temperature: float = 0.0, **kw):
+    """LiteLLM ``text_completion``: a raw prompt (no chat template); ``.choices[0].text``."""
+    base = api_base if api_base is not None else globals()["api_base"]
+    if _is_local(base):
+        eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+        ids = tok.encode(prompt)
+        out = eng.generate([ids], max_new_tokens=max_tokens, temperature=temperature, top_p=kw.get("top_p", 1.0),
+                           top_k=kw.get("top_k", 0), seed=kw.get("seed", 0))[0]
+        text = tok.decode([t for t in out if t not in eng.eos_ids])
+        return ModelResponse([TextChoice(text, finish_reason="length" if len(out) >= max_tokens else "stop")],
+                             model=model, usage={"prompt_tokens": len(ids), "completion_tokens": len(out)})
+    import httpx
+
+    key = api_key or globals()["api_key"] or os.environ.get("OPENAI_API_KEY")
+    url = base.rstrip("/")
+    if not url.endswith("/completions"):
+        url += "/completions"
+    headers = {"Authorization": f"Bearer {key}"} if key else {}
+    body = {"model": model, "prompt": prompt, "max_tokens": max_tokens, "temperature": temperature}
+    body.update({k: v for k, v in kw.items() if k in ("top_p", "stop", "seed", "top_k")})
+    r = httpx.post(url, json=body, headers=headers, timeout=timeout if timeout is not None else request_timeout)
+    if r.status_code != 200:
+        raise CompletionError(f"HTTP {r.status_code}: {r.text[:200]}")
+    j = r.json()
+    c = j["choices"][0]
+    return ModelResponse([TextChoice(c.get("text", ""), c.get("index", 0), c.get("finish_reason"))],
+                         model=j.get("model", model), usage=j.get("usage", {}))

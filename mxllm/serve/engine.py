@@ -119,6 +119,7 @@ class Engine:
         self._cv = threading.Condition(self._lock)
         self._thread = None
         self._stop = False
+        self._tasks: list = []  # (fn, result box, event): run by the engine thread between steps
         self.steps = 0
         self.tokens_generated = 0
         # latency / throughput counters: exported by the server's
@@ -284,6 +285,52 @@ class Engine:
         return self._graphs[(bb, kl)]
 
     # ------------------------------------------------------------------ scheduling
+    # ------------------------------------------------------------------ embeddings
+    @torch.no_grad()
+    def _embed_now(self, prompts: list[list[int]]) -> torch.Tensor:
+        if self.tp is not None:
+            raise NotImplementedError("embeddings are served by single-GPU engines")
+        out = []
+        for ids in prompts:
+            if not ids:
+                raise ValueError("empty input")
+            if len(ids) >= self.max_seq:
+                raise ValueError(f"input of {len(ids)} tokens exceeds max_seq {self.max_seq}")
+            t = torch.tensor([ids], dtype=torch.long, device=self.device)
+            h = self.model.hidden_states(t).float()  # [S, H], final RMSNorm applied (no KV cache touched)
+            out.append(torch.nn.functional.normalize(h.mean(0), dim=0))
+        return torch.stack(out).cpu()
+
+    def embed(self, prompts: list[list[int]]) -> torch.Tensor:
+        """Sentence embeddings [n, hidden] (f32, unit norm): the mean of the final
+        normed hidden states over each input's tokens.  With the background loop
+        running the pass runs on the engine thread between decode steps (it shares
+        the model's kernels and workspaces with generation); otherwise inline."""
+        if self._thread is None:
+            return self._embed_now(prompts)
+        box, ev = {}, threading.Event()
+
+        def task():
+            try:
+                box["out"] = self._embed_now(prompts)
+            except Exception as e:  # noqa: BLE001
+                box["err"] = e
+            ev.set()
+
+        with self._cv:
+            self._tasks.append(task)
+            self._cv.notify()
+        ev.wait()
+        if "err" in box:
+            raise box["err"]
+        return box["out"]
+
+    def _run_tasks(self) -> None:
+        with self._lock:
+            tasks, self._tasks = self._tasks, []
+        for t in tasks:
+            t()
+
     def submit(self, prompt: list[int], params: SamplingParams | None = None) -> Request:
         r = Request(next(self._ids), list(prompt), params or SamplingParams())
         with self._cv:
@@ -458,10 +505,12 @@ class Engine:
             sync = getattr(self, "tp_sync", False)
             while not self._stop:
                 with self._cv:
-                    while not self._stop and not self.waiting and not self.active:
+                    while not self._stop and not self.waiting and not self.active and not self._tasks:
                         self._cv.wait(timeout=0.5)
                         if sync:  # idle heartbeat: followers wait inside a broadcast
                             break
+                if self._tasks:
+                    self._run_tasks()
                 if self._stop:
                     if sync:
                         self._sync_admit([])  # tells the followers to stop

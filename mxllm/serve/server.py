@@ -134,6 +134,37 @@ def build_app(engine: Engine, tokenizer, model_name: str, api_key: str | None = 
             "model": body.get("model", model_name),
             "choices": [{"index": 0, "text": text, "finish_reason": r.finish_reason}], "usage": usage(r)})
 
+    @app.post("/v1/embeddings")
+    @app.post("/embeddings")
+    async def embeddings(req: Request):
+        """OpenAI embeddings: ``input`` a string, a list of strings, a token list or a
+        list of token lists; mean-pooled final hidden states, unit norm."""
+        auth(req)
+        body = await req.json()
+        stats["requests"] += 1
+        inp = body.get("input", "")
+        if inp == "" or inp == [] or (isinstance(inp, list) and any(x == "" or x == [] for x in inp)):
+            return JSONResponse({"error": {"message": "empty input", "type": "invalid_request_error"}},
+                                status_code=400)
+        if isinstance(inp, str):
+            seqs = [tokenizer.encode(inp)]
+        elif inp and all(isinstance(x, int) for x in inp):
+            seqs = [list(inp)]
+        else:
+            seqs = [tokenizer.encode(x) if isinstance(x, str) else list(x) for x in inp]
+        if not seqs or any(not q for q in seqs):
+            return JSONResponse({"error": {"message": "empty input", "type": "invalid_request_error"}},
+                                status_code=400)
+        try:
+            vec = await asyncio.get_running_loop().run_in_executor(None, engine.embed, seqs)
+        except (ValueError, NotImplementedError) as e:
+            return JSONResponse({"error": {"message": str(e), "type": "invalid_request_error"}}, status_code=400)
+        n = sum(len(q) for q in seqs)
+        return JSONResponse({
+            "object": "list", "model": body.get("model", model_name),
+            "data": [{"object": "embedding", "index": i, "embedding": v.tolist()} for i, v in enumerate(vec)],
+            "usage": {"prompt_tokens": n, "total_tokens": n}})
+
     async def _stream(ids, body, chat: bool):
         r = engine.submit(ids, SamplingParams(
             max_new_tokens=int(body.get("max_tokens") or body.get("max_completion_tokens") or 128),

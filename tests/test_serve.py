@@ -186,8 +186,45 @@ def test_local_stream_and_batch(tiny_engine):
         outs = client.batch_completion("tiny-local2", [msgs, msgs], api_base="local", max_tokens=5)
         assert [o.choices[0].message.content for o in outs] == [full.choices[0].message.content] * 2
     finally:
-        client.unregister_local("tiny-local2")
-        tiny_engine.stop()
+        client.unregister_local("tiny-local2")  # the module's server keeps using the running engine
+
+
+def test_embeddings_http_and_local(server, tiny_engine):
+    """/v1/embeddings + client.embedding(): unit-norm mean-pooled hidden states,
+    deterministic, distinct for distinct inputs, identical over HTTP and in process,
+    and equal to the model's own hidden states."""
+    r = client.embedding("tiny-test", ["hello world", "something else"], api_base=server, api_key="sekret",
+                         timeout=30)
+    v = torch.tensor([d["embedding"] for d in r.data])
+    assert v.shape[0] == 2 and torch.allclose(v.norm(dim=1), torch.ones(2), atol=1e-4)
+    assert (v[0] - v[1]).abs().max() > 1e-3
+    again = client.embedding("tiny-test", "hello world", api_base=server, api_key="sekret", timeout=30)
+    assert torch.allclose(torch.tensor(again.data[0]["embedding"]), v[0], atol=1e-6)
+    tok = ByteTokenizer(512)
+    client.register_local("tiny-emb", tiny_engine, tok)
+    try:
+        loc = client.embedding("tiny-emb", ["hello world"], api_base="local")
+        want = torch.nn.functional.normalize(
+            tiny_engine.model.hidden_states(torch.tensor([tok.encode("hello world")])).float().mean(0), dim=0)
+        torch.testing.assert_close(torch.tensor(loc.data[0]["embedding"]), want, rtol=1e-5, atol=1e-5)
+    finally:
+        client.unregister_local("tiny-emb")
+    import httpx
+
+    bad = httpx.post(server + "/embeddings", json={"model": "tiny-test", "input": ""},
+                     headers={"Authorization": "Bearer sekret"}, timeout=30)
+    assert bad.status_code == 400
+
+
+def test_text_completion_http_and_local(server, tiny_engine):
+    r = client.text_completion("tiny-test", "Once upon", api_base=server, api_key="sekret", max_tokens=5, timeout=30)
+    assert isinstance(r.choices[0].text, str) and r.usage["completion_tokens"] <= 5
+    client.register_local("tiny-tc", tiny_engine, ByteTokenizer(512))
+    try:
+        loc = client.text_completion("tiny-tc", "Once upon", api_base="local", max_tokens=5)
+        assert loc.choices[0].text == r.choices[0].text  # greedy, same weights and tokenizer
+    finally:
+        client.unregister_local("tiny-tc")
 
 
 def test_fp8_weight_engine_cpu():
