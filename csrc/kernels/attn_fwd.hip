@@ -99,18 +99,27 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   // VGPRs are spent on staging (the kernel sits at the 256-VGPR cap).
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
+  // buffer_load ... lds through range-checked descriptors: the per-lane source offset of each
+  // piece is loop-invariant (one VALU add for the tile step), rows past Sk read as zeros (masked)
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)Kp, 0, Sk * ROWB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)Vp, 0, Sk * ROWB, 0x00020000);
+  int voff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int seg = w * LPT + i;            // 1 KiB segment of the tile image
+    const int byte = seg * 1024 + lane * 16;
+    const int row = byte / ROWB, slot = (byte % ROWB) / 16;
+    voff[i] = row * ROWB + 16 * (slot ^ swz<CH>(row));  // logical chunk stored in this slot
+  }
   auto glds = [&](int kt, int buf) {
     char* kb = smem + buf * 2 * TILE;
     char* vb = kb + TILE;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int seg = w * LPT + i;            // 1 KiB segment of the tile image
-      const int byte = seg * 1024 + lane * 16;
-      const int row = byte / ROWB, slot = (byte % ROWB) / 16;
-      const int ch = slot ^ swz<CH>(row);     // logical chunk stored in this slot
-      const int key = min(kt * BN + row, Sk - 1);  // tail rows: duplicate valid row, masked later
-      __builtin_amdgcn_global_load_lds((gptr_t)(Kp + (size_t)key * D + ch * 8), (lptr_t)(kb + seg * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gptr_t)(Vp + (size_t)key * D + ch * 8), (lptr_t)(vb + seg * 1024), 16, 0, 0);
+      const int seg = w * LPT + i;
+      const int off = voff[i] + kt * TILE;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kb + seg * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vb + seg * 1024), 16, off, 0, 0, 0);
     }
   };
 
