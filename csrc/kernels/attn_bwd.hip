@@ -162,21 +162,34 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 
   // LDS-DMA of q tile `it` into buffer `buf`: Q / dO rows (swizzle via source
   // chunk permutation), lse / delta by wave 0 (4 B per lane).
+  // Q / dO rows by range-checked buffer_load ... lds: per-lane source offsets are loop-invariant
+  // (one VALU add per piece for the tile step), rows past S read as zeros (masked: p = 0)
+  const int orec = (int)(((size_t)(S - 1) * dstride + D) * 2);
+  static_assert(SEGS / 4 <= 4, "at most 4 pieces per wave");
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  i32x4_t qoff = {0, 0, 0, 0}, ooff = {0, 0, 0, 0};  // (a vector: a captured int array drops the host stub)
+#pragma unroll
+  for (int i = 0; i < SEGS / 4; ++i) {
+    const int seg = w * (SEGS / 4) + i;
+    const int byte = seg * 1024 + lane * 16;
+    const int row = byte / ROWB, slot = (byte % ROWB) / 16;
+    const int ch = slot ^ swzb<CH>(row);
+    qoff[i] = row * ROWB + ch * 16;
+    ooff[i] = (int)(row * dstride * 2) + ch * 16;
+  }
   auto glds = [&](int it, int buf) {
     char* qt = smem + KIMG + buf * BUF;
     char* dot = qt + QT;
     char* ld = dot + QT;
     const int q0 = qstart + it * BQ;
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp, 0, S * ROWB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp, 0, orec, 0x00020000);
 #pragma unroll
     for (int i = 0; i < SEGS / 4; ++i) {
       const int seg = w * (SEGS / 4) + i;
-      const int byte = seg * 1024 + lane * 16;
-      const int row = byte / ROWB, slot = (byte % ROWB) / 16;
-      const int ch = slot ^ swzb<CH>(row);
-      const int q = min(q0 + row, S - 1);
-      __builtin_amdgcn_global_load_lds((gptr_t)(Qp + (size_t)q * D + ch * 8), (lptr_t)(qt + seg * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gptr_t)(dOp + (size_t)q * dstride + ch * 8), (lptr_t)(dot + seg * 1024), 16,
-                                       0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(qt + seg * 1024), 16, qoff[i] + q0 * ROWB, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (lptr_t)(dot + seg * 1024), 16,
+                                               ooff[i] + (int)(q0 * dstride * 2), 0, 0, 0);
     }
     if (w == 0) {
       const int q = min(q0 + lane, S - 1);

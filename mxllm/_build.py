@@ -64,6 +64,17 @@ def _run(cmd):
     return r.stdout
 
 
+def _check_loadable(path: str) -> None:
+    """dlopen the fresh library in a child process (RTLD_NOW): an unresolved symbol —
+    e.g. a kernel whose host launch stub the compiler dropped — fails the build here
+    instead of at import on the GPU box."""
+    code = f"import ctypes, os; ctypes.CDLL({path!r}, mode=os.RTLD_NOW)"
+    r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        os.remove(path)
+        raise RuntimeError(f"built library does not load: {r.stderr.strip()[-600:]}")
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     inc, tlib, abi = _torch_paths()
     os.makedirs(OUT_DIR, exist_ok=True)
@@ -113,6 +124,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
             f"{tlib}/libamdhip64.so", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed",
         ])
         _run(cmd)
+        _check_loadable(tmp)
         os.replace(tmp, LIB_PATH)
         with open(stamp, "w") as f:
             f.write(link_key)
