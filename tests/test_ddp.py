@@ -88,9 +88,9 @@ def _single_grads(world, full, accum):
     return flat.grads.clone()
 
 
-@pytest.mark.parametrize("full,bucket_mb,accum", [(True, 0.05, 1), (False, 0.01, 1), (True, 0.05, 2)])
-def test_ddp_matches_single_process(full, bucket_mb, accum):
-    world = 2
+@pytest.mark.parametrize("full,bucket_mb,accum,world", [(True, 0.05, 1, 2), (False, 0.01, 1, 2), (True, 0.05, 2, 2),
+                                                         (True, 0.05, 1, 4)])
+def test_ddp_matches_single_process(full, bucket_mb, accum, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
