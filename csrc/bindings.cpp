@@ -489,6 +489,21 @@ at::Tensor sample_rows(const at::Tensor& logits, const at::Tensor& temps, const 
 }  // namespace
 
 
+// ---------------------------------------------------------------- bf16 decode GEMM (serving)
+// y[M, N] = x[M, K] . w[N, K]^T for M <= 32 tokens: the weight-streaming HIP kernel
+// (csrc/kernels/skinny_gemm.hip).  Callers check the shape contract (mxllm/ops/linear.py).
+at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w) {
+  MX_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "x: bf16 [M, K] rows");
+  MX_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1, "w: bf16 [N, K] rows");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  MX_CHECK(w.size(1) == K && M >= 1 && M <= 32 && N % 16 == 0 && K % 512 == 0 && x.stride(0) % 8 == 0 &&
+               w.stride(0) % 8 == 0, "skinny_linear shape contract");
+  DevGuard g(x.device());
+  auto y = at::empty({M, N}, x.options());
+  MX_OK(mx_skinny_gemm(bf(x), x.stride(0), bf(w), w.stride(0), bfm(y), N, (int)M, (int)N, (int)K, cur_stream()));
+  return y;
+}
+
 // ---------------------------------------------------------------- fp8 weights (serving)
 // y[M, N] = x[M, K] . (scale[:, None] * q[N, K])^T ; q: e4m3 codes (uint8), scale f32 [N].
 // M <= 32: the fused weight-streaming kernel; otherwise dequantise to bf16 and run the
@@ -613,6 +628,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("sample_rows(Tensor logits, Tensor temps, Tensor top_p, Tensor top_k, Tensor seeds, Tensor steps) -> Tensor");
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
+  m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
   m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha) -> ()");
@@ -644,6 +660,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("sample_rows", &sample_rows);
   m.impl("w8_linear", &w8_linear);
+  m.impl("skinny_linear", &skinny_linear);
   m.impl("w8_dequant", &w8_dequant);
   m.impl("quant_rows_e4m3", &quant_rows_e4m3);
   m.impl("lora_xwt", &lora_xwt);

@@ -69,6 +69,8 @@ int mx_sample_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, 
 
 extern "C" {
 // fp8_gemm.hip
+int mx_skinny_gemm(const uint16_t* x, int64_t ldx, const uint16_t* w, int64_t ldw, uint16_t* y, int64_t ldy,
+                   int M, int N, int K, hipStream_t stream);
 int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, const float* scale, uint16_t* y, int64_t ldy,
                   int M, int N, int K, hipStream_t stream);
 int mx_w8_dequant(const uint8_t* q, const float* scale, uint16_t* w, int64_t N, int K, hipStream_t stream);

@@ -304,9 +304,31 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw
 
 
+# decode-sized GEMMs (bf16, no autograd) on the weight-streaming HIP kernel
+# (csrc/kernels/skinny_gemm.hip) where it beat hipBLASLt inside the decode step
+# (bench/serve_bench.py A/B, profiles/r2x_skinny_gemm.md): one token row for every projection
+# and the LM head; 2..SKINNY_M rows for weights of <= 128 M elements (all Llama-3.1-8B
+# projections; the 70B ones lost at 4 rows).  MXLLM_SKINNY_M=0 keeps every GEMM on hipBLASLt.
+SKINNY_M = int(os.environ.get("MXLLM_SKINNY_M", "8"))
+_SKINNY_SMALL_W = 128 << 20
+
+
+def _skinny_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    K, M = x2.shape[1], x2.shape[0]
+    if M > 1 and w.shape[0] * K > _SKINNY_SMALL_W:
+        return False
+    return (M <= SKINNY_M and x2.is_cuda and x2.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and K % 512 == 0 and w.shape[0] % 16 == 0 and x2.stride(1) == 1
+            and x2.stride(0) % 8 == 0 and w.stride(1) == 1 and w.stride(0) % 8 == 0 and use_native(x2))
+
+
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if w.requires_grad and torch.is_grad_enabled():
         return _LinearFn.apply(x, w)
+    if SKINNY_M > 0 and x.shape[-1] == w.shape[1] and x.numel() // max(x.shape[-1], 1) <= SKINNY_M:
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.shape[0] > 0 and _skinny_ok(x2, w):
+            return native().skinny_linear(x2, w).view(*x.shape[:-1], w.shape[0])
     return F.linear(x, w)
 
 

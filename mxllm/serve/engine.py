@@ -172,7 +172,7 @@ class Engine:
         return self._logits(xn[-1:]).float()[0]
 
     def _logits(self, xn: torch.Tensor) -> torch.Tensor:
-        out = torch.matmul(xn, self.model.head_weight.t())
+        out = ops.linear(xn, self.model.head_weight)  # decode rows: the weight-streaming HIP GEMM
         if self.tp is not None:  # vocab-parallel head
             out = self.tp.gather_logits(out)
         return out

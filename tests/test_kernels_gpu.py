@@ -458,3 +458,17 @@ def test_weight_grad_tn(gpu, T, N, K):
     want2 = acc.float() + want
     weight_grad_(acc, dy, x)
     assert rel_err(acc, want2) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (5, 4096, 14336), (16, 1040, 512), (17, 2048, 1024),
+                                   (32, 96, 4608)])
+def test_skinny_linear_vs_fp32(gpu, M, N, K):
+    """Decode GEMM (csrc/kernels/skinny_gemm.hip) against fp32 torch, incl. a row-strided x
+    (the view a producer leaves) and both token-block variants (<= 16 and 17..32 rows)."""
+    torch.manual_seed(M + N)
+    xb = torch.randn(M, K + 64, device=gpu, dtype=torch.bfloat16)
+    x = xb[:, :K]
+    w = torch.randn(N, K, device=gpu, dtype=torch.bfloat16) * 0.05
+    y = _ops().skinny_linear(x, w)
+    ref = x.float() @ w.float().t()
+    assert y.shape == (M, N) and rel_err(y, ref) < 1e-2
