@@ -10,7 +10,7 @@ iteration.  The engine runs eager here (MXLLM_DECODE_GRAPHS=0) so every GEMM is
 a plain library call TunableOp sees; the graphed engine replays the same
 solutions.  Prints the default and tuned per-step decode time per bucket.
 
-  python bench/tune_decode_gemms.py --model llama3.1-8b --out gpurun_out/tune_decode.csv
+  python bench/tune_decode_gemms.py --model llama3.1-8b --out gpurun_out/tune_decode.csv [--prefill 1024]
 """
 import argparse
 import json
@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tune_decode.csv"))
     ap.add_argument("--max-ms", type=int, default=30, help="TunableOp time budget per candidate solution")
     ap.add_argument("--rotating-mb", type=int, default=512)
+    ap.add_argument("--prefill", default="", help="also tune the prefill GEMMs of these prompt lengths (e.g. 1024)")
     a = ap.parse_args()
 
     from mxllm.models import Llama, get_config
@@ -59,11 +60,24 @@ def main():
     model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     model.requires_grad_(False)
     batches = [int(b) for b in a.batches.split(",")]
-    eng = Engine(model, max_batch=max(batches), max_seq=a.ctx + 64)
+    plens = [int(x) for x in a.prefill.split(",") if x]
+    eng = Engine(model, max_batch=max(batches), max_seq=max([a.ctx + 64] + [n + 8 for n in plens]))
     res = {"model": a.model, "ctx": a.ctx, "default_ms": {}, "tuned_ms": {}}
+
+    def prefill_ms(n, reps=3):
+        ids = torch.randint(0, cfg.vocab_size, (n,)).tolist()
+        eng.prefill(0, ids)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            eng.prefill(0, ids)
+        torch.cuda.synchronize()
+        return 1e3 * (time.perf_counter() - t) / reps
     gemm_tuning.enable()  # the current table: training shapes; decode shapes fall back to the library default
     for bs in batches:
         res["default_ms"][bs] = round(step_ms(eng, bs, a.ctx, cfg.vocab_size), 3)
+    for n in plens:
+        res["default_ms"][f"prefill{n}"] = round(prefill_ms(n), 3)
     print(json.dumps({"phase": "default", **res["default_ms"]}), flush=True)
 
     tun = torch.cuda.tunable
@@ -75,9 +89,14 @@ def main():
     for bs in batches:
         step_ms(eng, bs, a.ctx, cfg.vocab_size, steps=1)
         print(json.dumps({"phase": "tuning", "batch": bs, "elapsed_s": round(time.time() - t0, 1)}), flush=True)
+    for n in plens:
+        prefill_ms(n, reps=1)
+        print(json.dumps({"phase": "tuning", "prefill": n, "elapsed_s": round(time.time() - t0, 1)}), flush=True)
     tun.tuning_enable(False)  # the results stay in memory; TunableOp writes a.out at process exit
     for bs in batches:
         res["tuned_ms"][bs] = round(step_ms(eng, bs, a.ctx, cfg.vocab_size), 3)
+    for n in plens:
+        res["tuned_ms"][f"prefill{n}"] = round(prefill_ms(n), 3)
     print(json.dumps({"phase": "tuned", **res["tuned_ms"]}), flush=True)
     print(json.dumps(res), flush=True)
 
