@@ -536,3 +536,27 @@ def test_hf_checkpoint_on_gpu_matches_transformers(gpu, tmp_path):
         got2 = m(ids.to(gpu)).float().cpu()
         want2 = back(ids).logits
     assert _rel(got2, want2) < 2e-2
+
+
+def test_engine_embeddings_gpu_match_cpu(gpu):
+    """/v1/embeddings path on the GPU (final hidden states through the HIP kernels, run on
+    the engine thread while it serves) against the CPU reference model."""
+    from mxllm.models import Llama, get_config
+    from mxllm.serve.engine import Engine
+
+    cfg = get_config("tiny-d128")
+    cpu = Llama(cfg, device="cpu", dtype=torch.float32, seed=3).eval()
+    g = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3).eval()
+    with torch.no_grad():
+        for pc, pg in zip(cpu.parameters(), g.parameters()):
+            pg.copy_(pc.to(pg.dtype))
+    eng = Engine(g, max_batch=2, max_seq=256)
+    eng.start()
+    try:
+        seqs = [list(range(5, 70)), list(range(100, 300, 3))]
+        got = eng.embed(seqs)
+        want = Engine(cpu, max_batch=2, max_seq=256).embed(seqs)
+    finally:
+        eng.stop()
+    assert got.shape == want.shape
+    assert (torch.nn.functional.cosine_similarity(got, want, dim=1) > 0.995).all()
