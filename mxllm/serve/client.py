@@ -105,13 +105,18 @@ def unregister_local(model: str | None = None) -> None:
         _LOCAL.pop(model, None)
 
 
-def _local(model, messages, max_tokens, temperature, **kw) -> ModelResponse:
+def _local_engine(model: str):
+    """The in-process (engine, tokenizer) for ``model``: its own registration, or the only
+    one registered; anything else is an error (never a silent pick among several)."""
     if model in _LOCAL:
-        eng, tok = _LOCAL[model]
-    elif len(_LOCAL) == 1:
-        eng, tok = next(iter(_LOCAL.values()))
-    else:
-        raise CompletionError(f"no local engine registered for model {model!r}")
+        return _LOCAL[model]
+    if len(_LOCAL) == 1:
+        return next(iter(_LOCAL.values()))
+    raise CompletionError(f"no local engine registered for model {model!r}")
+
+
+def _local(model, messages, max_tokens, temperature, **kw) -> ModelResponse:
+    eng, tok = _local_engine(model)
     ids = tok.apply_chat_template(messages)
     out = eng.generate([ids], max_new_tokens=max_tokens, temperature=temperature,
                        top_p=kw.get("top_p", 1.0), seed=kw.get("seed", 0))[0]
@@ -122,7 +127,7 @@ def _local(model, messages, max_tokens, temperature, **kw) -> ModelResponse:
 
 def batch_local(model: str, prompts: list[str], max_tokens: int = 32, temperature: float = 0.0) -> list[str]:
     """Batched in-process generation for a list of user prompts (one engine pass)."""
-    eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+    eng, tok = _local_engine(model)
     ids = [tok.apply_chat_template([{"role": "user", "content": p}]) for p in prompts]
     outs = eng.generate(ids, max_new_tokens=max_tokens, temperature=temperature)
     return [tok.decode([t for t in o if t not in eng.eos_ids]) for o in outs]
@@ -134,7 +139,7 @@ def submit_local(model: str, prompts: list[str], max_tokens: int = 32, temperatu
     request handles for ``collect_local``."""
     from .engine import SamplingParams
 
-    eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+    eng, tok = _local_engine(model)
     eng.start()
     ids = [tok.apply_chat_template([{"role": "user", "content": p}]) for p in prompts]
     return [eng.submit(i, SamplingParams(max_new_tokens=max_tokens, temperature=temperature)) for i in ids]
@@ -142,7 +147,7 @@ def submit_local(model: str, prompts: list[str], max_tokens: int = 32, temperatu
 
 def collect_local(model: str, requests: list, timeout: float | None = None) -> list[str]:
     """Wait for requests from ``submit_local`` and detokenize (raises on an engine error)."""
-    eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+    eng, tok = _local_engine(model)
     out = []
     for r in requests:
         if not r.done.wait(timeout):
@@ -187,12 +192,7 @@ def _local_stream(model, messages, max_tokens, temperature, **kw):
     """Token deltas from the in-process engine's background loop as they are produced."""
     from .engine import SamplingParams
 
-    if model in _LOCAL:
-        eng, tok = _LOCAL[model]
-    elif len(_LOCAL) == 1:
-        eng, tok = next(iter(_LOCAL.values()))
-    else:
-        raise CompletionError(f"no local engine registered for model {model!r}")
+    eng, tok = _local_engine(model)
     eng.start()
     ids = tok.apply_chat_template(messages)
     r = eng.submit(ids, SamplingParams(max_new_tokens=max_tokens, temperature=temperature,
@@ -305,7 +305,7 @@ def batch_completion(model: str, messages: list[list[dict]], *, api_base: str | 
     HTTP: the requests run concurrently."""
     base = api_base if api_base is not None else globals()["api_base"]
     if _is_local(base):
-        eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+        eng, tok = _local_engine(model)
         ids = [tok.apply_chat_template(m) for m in messages]
         outs = eng.generate(ids, max_new_tokens=max_tokens, temperature=temperature, top_p=kw.get("top_p", 1.0),
                             top_k=kw.get("top_k", 0), seed=kw.get("seed", 0))
@@ -338,7 +338,7 @@ def embedding(model: str, input, *, api_base: str | None = None, api_key: str | 
     base = api_base if api_base is not None else globals()["api_base"]
     texts = [input] if isinstance(input, str) else list(input)
     if _is_local(base):
-        eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+        eng, tok = _local_engine(model)
         seqs = [tok.encode(t) for t in texts]
         vec = eng.embed(seqs)
         n = sum(len(q) for q in seqs)
@@ -375,7 +375,7 @@ def text_completion(model: str, prompt: str, *, api_base: str | None = None, api
     """LiteLLM ``text_completion``: a raw prompt (no chat template); ``.choices[0].text``."""
     base = api_base if api_base is not None else globals()["api_base"]
     if _is_local(base):
-        eng, tok = _LOCAL.get(model) or next(iter(_LOCAL.values()))
+        eng, tok = _local_engine(model)
         ids = tok.encode(prompt)
         out = eng.generate([ids], max_new_tokens=max_tokens, temperature=temperature, top_p=kw.get("top_p", 1.0),
                            top_k=kw.get("top_k", 0), seed=kw.get("seed", 0))[0]
