@@ -168,3 +168,28 @@ def test_server_builds_from_hf_dir(tmp_path):
     eng, tok = build_default(str(tmp_path), device="cpu", max_batch=2, max_seq=128)
     out = eng.generate([tok.encode("hello")], max_new_tokens=4)
     assert len(out[0]) == 4
+
+
+def test_export_cli_from_checkpoint_equals_driver_export(tmp_path):
+    """``python -m mxllm export-hf`` rebuilds the merged model from the base checkpoint and the
+    adapters a LoRA run saved, identical to the run's own --save-hf export."""
+    from safetensors.torch import load_file
+
+    src, a_out, b_out, ck = tmp_path / "src", tmp_path / "a", tmp_path / "b", tmp_path / "ck"
+    _hf_model(src)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "src/distributed_finetuning.py", "--model", str(src), "--finetune", "lora",
+                        "--lora-r", "8", "--lora-alpha", "16", "--lr", "1e-2", "--steps", "2", "--seq-len", "32",
+                        "--micro-batch", "1", "--save-every", "2", "--ckpt-dir", str(ck), "--save-hf", str(a_out)],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([sys.executable, "-m", "mxllm", "export-hf", "--base", str(src), "--weights",
+                        str(ck / "step_2"), "--lora-r", "8", "--lora-alpha", "16", "--out", str(b_out)],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    a, b = load_file(str(a_out / "model.safetensors")), load_file(str(b_out / "model.safetensors"))
+    assert set(a) == set(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
