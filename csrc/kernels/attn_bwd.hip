@@ -20,6 +20,8 @@
 //    fused into the inverse-RoPE merge kernel (rope.hip), so no atomics and a
 //    deterministic dK/dV;
 //  * heaviest key blocks (most visible q tiles) scheduled first.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mx {
@@ -383,6 +385,232 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   }
 }
 
+// Split-mode (3) key-block kernel at TWO waves per SIMD (D = 128; MXLLM_ATTN_BWD8=0 selects the
+// kernel above).  Workgroup = 8 waves = 128 keys of one q head, as above, but wave (kg = w & 3,
+// m = w >> 2) owns 32 keys x the 32-row half m of every 64-row q tile: S, dP, P, dS and the dV / dK
+// products of one half per wave, so each wave carries half the q work and its K / V fragments come
+// from LDS images of the key block instead of registers — the register file then holds two
+// waves per SIMD (the hardware interleaves one wave's softmax VALU with the other's MFMAs, which
+// the one-wave kernel cannot).  The two halves' dK / dV partials are summed through LDS at the end.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(512, 1)
+attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                 const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                 uint16_t* __restrict__ dST, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq,
+                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad) {
+  constexpr int D = 128, BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int KIMG = BN * ROWB;     // K (or V) image [128][D]
+  constexpr int QT = BQ * ROWB;       // Q / dO tile [64][D]
+  constexpr int BUF = 2 * QT + 2 * BQ * 4;
+  constexpr int SEGS = QT / 1024;     // 16 pieces per tile, 2 per wave
+  constexpr int LDSB = 2 * KIMG + 2 * BUF;
+  static_assert(LDSB >= 4 * 2 * DB * 16 * 64 * 4, "dK/dV pair reduction reuses the tile LDS");
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  char* kimg = smem;
+  char* vimg = smem + KIMG;
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+
+  const int nkb = (Sk + BN - 1) / BN;
+  const int BH = B * Hq;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = bid / BH;
+  const int bh = bid % BH;
+  if (kb >= nkb) return;
+  const int b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
+  const uint16_t* Qp = Q + (size_t)(b * Hq + h) * S * D;
+  const uint16_t* Kp = K + (size_t)(b * Hkv + hk) * Sk * D;
+  const uint16_t* Vp = V + (size_t)(b * Hkv + hk) * Sk * D;
+  const size_t dstride = (size_t)Hq * D;
+  const uint16_t* dOp = dO + (size_t)b * S * dstride + (size_t)h * D;
+  const float* lsep = LSE + (size_t)(b * Hq + h) * S;
+  const float* delp = DELTA + (size_t)(b * Hq + h) * S;
+  uint16_t* dstp = dST + (size_t)(b * Hq + h) * (nkb * BN) * S_pad;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = w & 3, m = w >> 2;
+  const int r = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int k0 = kb * BN;
+  const int key = k0 + 32 * kg + r;
+
+  // K / V images of the key block (rows past Sk read as zeros: masked)
+  {
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)Kp, 0, Sk * ROWB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)Vp, 0, Sk * ROWB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < KIMG / 1024 / 8; ++i) {
+      const int seg = w * (KIMG / 1024 / 8) + i;
+      const int row = seg * (1024 / ROWB) + lane / (ROWB / 16), slot = lane % (ROWB / 16);
+      const int vo = (k0 + row) * ROWB + 16 * (slot ^ swzb<CH>(row));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kimg + seg * 1024), 16, vo, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vimg + seg * 1024), 16, vo, 0, 0, 0);
+    }
+  }
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { dk[d][j] = 0.f; dv[d][j] = 0.f; }
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, (k0 - off) / BQ * BQ);
+  const int nqt = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
+
+  // Q / dO tile pieces: 2 per wave (one Q, one dO), range-checked buffer loads
+  const int orec = (int)(((size_t)(S - 1) * dstride + D) * 2);
+  const int pseg = w * (SEGS / 8);
+  static_assert(SEGS / 8 == 2, "two pieces per wave");
+  typedef int i32x2_t __attribute__((ext_vector_type(2)));
+  i32x2_t qoff = {0, 0}, ooff = {0, 0};  // (a vector: a captured int array drops the host stub)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // the swizzle depends on the row: each piece has its own offsets
+    const int prow = (pseg + i) * (1024 / ROWB) + lane / (ROWB / 16), pslot = lane % (ROWB / 16);
+    const int pch = pslot ^ swzb<CH>(prow);
+    qoff[i] = prow * ROWB + pch * 16;
+    ooff[i] = (int)(prow * dstride * 2) + pch * 16;
+  }
+  auto glds = [&](int it, int buf) {
+    char* qt = smem + 2 * KIMG + buf * BUF;
+    char* dot = qt + QT;
+    char* ld = dot + QT;
+    const int q0 = qstart + it * BQ;
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp, 0, S * ROWB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp, 0, orec, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < SEGS / 8; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(qt + (pseg + i) * 1024), 16, qoff[i] + q0 * ROWB, 0, 0,
+                                               0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (lptr_t)(dot + (pseg + i) * 1024), 16,
+                                               ooff[i] + (int)(q0 * dstride * 2), 0, 0, 0);
+    }
+    if (w == 0) {
+      const int q = min(q0 + lane, S - 1);
+      __builtin_amdgcn_global_load_lds((gptr_t)(lsep + q), (lptr_t)(ld), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(delp + q), (lptr_t)(ld + BQ * 4), 4, 0, 0);
+    }
+  };
+
+  u16x4 dsv[4];
+  int ds_q0 = -1;
+  auto flush_ds = [&]() {
+    if (ds_q0 < 0) return;
+    uint16_t* rowp = dstp + ((size_t)(ds_q0 / BQ) * (nkb * BN) + key) * BQ + 32 * m;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<u16x4*>(rowp + 8 * gq + 4 * hh) = dsv[gq];
+  };
+
+  const int qr = 32 * m + r;                    // this lane's row of the q tile (S, dP A operand)
+  const int krow = 32 * kg + r;                 // this lane's key row of the K / V images (B operand)
+  if (nqt > 0) glds(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  for (int it = 0; it < nqt; ++it) {
+    const int q0 = qstart + it * BQ;
+    const int buf = it & 1;
+    const char* qt = smem + 2 * KIMG + buf * BUF;
+    const char* dot = qt + QT;
+    const float* lse_s = reinterpret_cast<const float*>(dot + QT);
+    const float* del_s = lse_s + BQ;
+    if (it + 1 < nqt) glds(it + 1, buf ^ 1);
+    flush_ds();
+    const bool need_mask = (q0 + BQ > S) || (k0 + BN > Sk) || (CAUSAL && (k0 + 32 * kg + 31 > q0 + 32 * m + off));
+    f32x16 sa, dp;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { sa[j] = 0.f; dp[j] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int oq = qr * ROWB + 16 * ((2 * s + hh) ^ swzb<CH>(qr));
+      const int ok = krow * ROWB + 16 * ((2 * s + hh) ^ swzb<CH>(krow));
+      sa = mfma32b(*reinterpret_cast<const u16x8*>(qt + oq), *reinterpret_cast<const u16x8*>(kimg + ok), sa);
+      dp = mfma32b(*reinterpret_cast<const u16x8*>(dot + oq), *reinterpret_cast<const u16x8*>(vimg + ok), dp);
+    }
+    // rows of sa/dp: q = q0 + 32m + (j&3) + 8(j>>2) + 4hh ; column = key (lane)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_s + 32 * m + 8 * gq + 4 * hh);
+      const f32x4 dl = *reinterpret_cast<const f32x4*>(del_s + 32 * m + 8 * gq + 4 * hh);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * gq + jj;
+        float p = __builtin_amdgcn_exp2f(sa[j] * sl - lv[jj]);
+        if (need_mask) {
+          const int q = q0 + 32 * m + jj + 8 * gq + 4 * hh;
+          const bool dead = (key >= Sk) | (q >= S) | (CAUSAL & (key > q + off));
+          p = dead ? 0.f : p;
+        }
+        sa[j] = p;
+        dp[j] = p * (dp[j] - dl[jj]);
+      }
+    }
+    // dV^T += dO^T P ; dK^T += Q^T dS   (k index = the 32 q rows of this half)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u16x8 pb, sb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pb[j] = f2bf(sa[8 * s2 + j]);
+        sb[j] = f2bf(dp[8 * s2 + j]);
+      }
+      const int rb = 32 * m + 16 * s2 + 4 * hh;
+      const int rowA = rb + tq, rowB = rb + 8 + tq;
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+        const int oA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
+        const int oB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
+        const u16x4 a0 = trd(dot + oA), a1 = trd(dot + oB);
+        dv[db] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]}, pb, dv[db]);
+        const u16x4 b0 = trd(qt + oA), b1 = trd(qt + oB);
+        dk[db] = mfma32b(u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, sb, dk[db]);
+      }
+    }
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq)
+      dsv[gq] = u16x4{f2bf(dp[4 * gq]), f2bf(dp[4 * gq + 1]), f2bf(dp[4 * gq + 2]), f2bf(dp[4 * gq + 3])};
+    ds_q0 = q0;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next tile landed
+    __syncthreads();                     // ... and every wave's; this tile's buffers consumed
+  }
+  flush_ds();
+  // sum the two halves' partials: m = 1 waves park theirs in LDS ([kg][value][lane], conflict-free)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem) + (size_t)kg * (2 * DB * 16) * 64 + lane;
+  if (m == 1) {
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        red[((db * 16) + j) * 64] = dk[db][j];
+        red[((DB * 16) + db * 16 + j) * 64] = dv[db][j];
+      }
+  }
+  __syncthreads();
+  if (m == 0 && key < Sk) {
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        dk[db][j] += red[((db * 16) + j) * 64];
+        dv[db][j] += red[((DB * 16) + db * 16 + j) * 64];
+      }
+    float* dkq = dKp + ((size_t)(b * Hq + h) * Sk + key) * D;
+    float* dvq = dVp + ((size_t)(b * Hq + h) * Sk + key) * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d = db * 32 + 8 * gq + 4 * hh;
+        *reinterpret_cast<f32x4*>(dkq + d) =
+            f32x4{dk[db][4 * gq] * scale, dk[db][4 * gq + 1] * scale, dk[db][4 * gq + 2] * scale,
+                  dk[db][4 * gq + 3] * scale};
+        *reinterpret_cast<f32x4*>(dvq + d) = f32x4{dv[db][4 * gq], dv[db][4 * gq + 1], dv[db][4 * gq + 2],
+                                                  dv[db][4 * gq + 3]};
+      }
+  }
+}
+
 // Deterministic dQ: dq[b,h,q,:] = sum over the key blocks that visited q (ascending kb)
 // of the partials written by attn_bwd_kernel<.., DQM=2>.  One thread per 4 floats.
 template <int D, bool CAUSAL>
@@ -602,6 +830,19 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     return (int)hipGetLastError();
   }
   float* dqk = dq_mode == 1 ? dq : reinterpret_cast<float*>(work);
+  static const bool bwd8 = [] {  // MXLLM_ATTN_BWD8=0: the one-wave-per-SIMD split kernel (A/B)
+    const char* e = getenv("MXLLM_ATTN_BWD8");
+    return !(e && e[0] == '0');
+  }();
+  if (dq_mode == 3 && D == 128 && bwd8) {
+    uint16_t* dst = reinterpret_cast<uint16_t*>(work);
+    if (causal)
+      attn_bwd8_kernel<true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk, off,
+                                                       sl, scale, S_pad);
+    else
+      attn_bwd8_kernel<false><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
+                                                        off, sl, scale, S_pad);
+  } else {
 #define BWD(DD, C)                                                                                                  \
   do {                                                                                                              \
     if (dq_mode == 3)                                                                                               \
@@ -619,6 +860,7 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   else if (D == 32) { if (causal) BWD(32, true); else BWD(32, false); }
   else return -1;
 #undef BWD
+  }
   if (dq_mode == 2) {
     const int64_t n = (int64_t)B * Hq * S * (D / 4);
     const unsigned rg = (unsigned)((n + 255) / 256);

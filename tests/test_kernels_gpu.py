@@ -245,7 +245,11 @@ def test_attention_bwd_deterministic(gpu, causal, S):
             assert torch.equal(a, b), mode
         # mode 3 rounds dS to bf16 before the dQ GEMM (as the atomic path does in LDS)
         torch.testing.assert_close(r1[0], ra[0], rtol=1e-3, atol=1e-3)
-        assert torch.equal(r1[1], ra[1]) and torch.equal(r1[2], ra[2])
+        if mode == 2:  # same key-block kernel: dK / dV summed in the same order
+            assert torch.equal(r1[1], ra[1]) and torch.equal(r1[2], ra[2])
+        else:  # D=128 split mode: the 8-wave kernel sums its two q halves at the end
+            torch.testing.assert_close(r1[1], ra[1], rtol=1e-4, atol=1e-5)
+            torch.testing.assert_close(r1[2], ra[2], rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.parametrize("mode", [3, 1])
