@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(512, 1)
 attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                  const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                  uint16_t* __restrict__ dST, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq,
-                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad) {
+                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad, int prio) {
   constexpr int D = 128, BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int KIMG = BN * ROWB;     // K (or V) image [128][D]
   constexpr int QT = BQ * ROWB;       // Q / dO tile [64][D]
@@ -405,7 +405,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   constexpr int SEGS = QT / 1024;     // 16 pieces per tile, 2 per wave
   constexpr int LDSB = 2 * KIMG + 2 * BUF;
   static_assert(LDSB >= 4 * 2 * DB * 16 * 64 * 4, "dK/dV pair reduction reuses the tile LDS");
-  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  __shared__ __attribute__((aligned(1024))) char smem[LDSB];  // (XOR addressing: 256-B aligned bases)
   char* kimg = smem;
   char* vimg = smem + KIMG;
   typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -475,7 +475,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     char* qt = smem + 2 * KIMG + buf * BUF;
     char* dot = qt + QT;
     char* ld = dot + QT;
-    const int q0 = qstart + it * BQ;
+    const int q0 = (prio & 2) ? qstart : qstart + it * BQ;  // (prio & 2: timing ablation, same tile)
     const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp, 0, S * ROWB, 0x00020000);
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp, 0, orec, 0x00020000);
 #pragma unroll
@@ -501,8 +501,26 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<u16x4*>(rowp + 8 * gq + 4 * hh) = dsv[gq];
   };
 
-  const int qr = 32 * m + r;                    // this lane's row of the q tile (S, dP A operand)
-  const int krow = 32 * kg + r;                 // this lane's key row of the K / V images (B operand)
+  // transposed-read lane offsets into a q tile (rows 32m + 4hh + tq (+8); chunk of d-block db);
+  // the 16-row step s2 and the dO tile are immediates, the buffer a per-tile add
+  // Every address below is (lane base) ^ (step bits): the swizzle XOR only touches byte bits
+  // 4..7 of a 256-B row, row and buffer bases are multiples of 256, so the d-block (bits 6-7)
+  // and the 32-B k step (bits 5-7) apply as one v_xor instead of one offset register each.
+  const uint32_t tile_base = lds_addr(smem + 2 * KIMG);
+  static_assert(ROWB == 256 && (BUF % 256) == 0 && (KIMG % 256) == 0, "XOR addressing assumes 256-B rows");
+  uint32_t trA, trB;  // transposed reads of a q tile: rows 32m + 4hh + tq (+8), d-block 0
+  {
+    const int rowA = 32 * m + 4 * hh + tq, rowB = rowA + 8;
+    const int chunk = (16 * (g & 1) + 4 * tp) >> 3;
+    trA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
+    trB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
+  }
+  // S / dP operand rows: q row 32m + r of the tile and key row 32kg + r of the K image share
+  // row & 15, hence the swizzle: k step s reads chunk (2s + hh) ^ swz at base ^ (32 s)
+  const int swz = swzb<CH>(r);
+  const uint32_t qrowb = (32 * m + r) * ROWB + 16 * (hh ^ swz);
+  const uint32_t krowb = lds_addr(kimg) + (32 * kg + r) * ROWB + 16 * (hh ^ swz);
+  if ((prio & 1) && m == 1) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (waves 4-7)
   if (nqt > 0) glds(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
@@ -519,52 +537,91 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     f32x16 sa, dp;
 #pragma unroll
     for (int j = 0; j < 16; ++j) { sa[j] = 0.f; dp[j] = 0.f; }
+    {  // S = Q K^T, dP = dO V^T: asm row reads one k step ahead of their MFMAs (counted waits)
+      const uint32_t qb = tile_base + buf * BUF + qrowb, kb2 = krowb;
+      u16x8 f[2][4];
+      auto ld = [&](int st, u16x8 (&x)[4]) {
+        const uint32_t qa = qb ^ (uint32_t)(32 * st), ka = kb2 ^ (uint32_t)(32 * st);
+        x[0] = rd128_off(qa, 0);
+        x[1] = rd128_off(ka, 0);
+        x[2] = rd128_off(qa, QT);
+        x[3] = rd128_off(ka, KIMG);
+      };
+      ld(0, f[0]);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int oq = qr * ROWB + 16 * ((2 * s + hh) ^ swzb<CH>(qr));
-      const int ok = krow * ROWB + 16 * ((2 * s + hh) ^ swzb<CH>(krow));
-      sa = mfma32b(*reinterpret_cast<const u16x8*>(qt + oq), *reinterpret_cast<const u16x8*>(kimg + ok), sa);
-      dp = mfma32b(*reinterpret_cast<const u16x8*>(dot + oq), *reinterpret_cast<const u16x8*>(vimg + ok), dp);
+      for (int st = 0; st < KS; ++st) {
+        if (st + 1 < KS) ld(st + 1, f[(st + 1) & 1]);
+        lds_wait_le(st + 1 < KS ? 4 : 0);
+        u16x8(&x)[4] = f[st & 1];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) pin(x[y]);
+        sa = mfma32b(x[0], x[1], sa);
+        dp = mfma32b(x[2], x[3], dp);
+      }
     }
     // rows of sa/dp: q = q0 + 32m + (j&3) + 8(j>>2) + 4hh ; column = key (lane)
+    if (need_mask) {  // wave-uniform: two straight-line bodies, branch-free selects
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_s + 32 * m + 8 * gq + 4 * hh);
-      const f32x4 dl = *reinterpret_cast<const f32x4*>(del_s + 32 * m + 8 * gq + 4 * hh);
+      for (int gq = 0; gq < 4; ++gq) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_s + 32 * m + 8 * gq + 4 * hh);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_s + 32 * m + 8 * gq + 4 * hh);
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int j = 4 * gq + jj;
-        float p = __builtin_amdgcn_exp2f(sa[j] * sl - lv[jj]);
-        if (need_mask) {
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = 4 * gq + jj;
           const int q = q0 + 32 * m + jj + 8 * gq + 4 * hh;
           const bool dead = (key >= Sk) | (q >= S) | (CAUSAL & (key > q + off));
-          p = dead ? 0.f : p;
+          const float p = dead ? 0.f : __builtin_amdgcn_exp2f(sa[j] * sl - lv[jj]);
+          sa[j] = p;
+          dp[j] = p * (dp[j] - dl[jj]);
         }
-        sa[j] = p;
-        dp[j] = p * (dp[j] - dl[jj]);
+      }
+    } else {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_s + 32 * m + 8 * gq + 4 * hh);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_s + 32 * m + 8 * gq + 4 * hh);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = 4 * gq + jj;
+          const float p = __builtin_amdgcn_exp2f(sa[j] * sl - lv[jj]);
+          sa[j] = p;
+          dp[j] = p * (dp[j] - dl[jj]);
+        }
       }
     }
-    // dV^T += dO^T P ; dK^T += Q^T dS   (k index = the 32 q rows of this half)
+    // dV^T += dO^T P ; dK^T += Q^T dS   (k index = the 32 q rows of this half).  The transposed
+    // reads are asm (trd_off) with counted lgkmcnt waits: as builtins, hipcc's waitcnt pass
+    // drains the next tile's LDS-DMA (vmcnt(0)) before the first of them
+    u16x8 pb[2], sb[2];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      u16x8 pb, sb;
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        pb[j] = f2bf(sa[8 * s2 + j]);
-        sb[j] = f2bf(dp[8 * s2 + j]);
+        pb[s2][j] = f2bf(sa[8 * s2 + j]);
+        sb[s2][j] = f2bf(dp[8 * s2 + j]);
       }
-      const int rb = 32 * m + 16 * s2 + 4 * hh;
-      const int rowA = rb + tq, rowB = rb + 8 + tq;
+    const uint32_t tbase = tile_base + buf * BUF;
+    const uint32_t ta = tbase + trA, tb = tbase + trB;
+    u16x4 tr[2][4];
+    auto issue = [&](int i, u16x4 (&t)[4]) {
+      const int s2 = i / DB, db = i % DB;
+      const uint32_t a = ta ^ (uint32_t)(64 * db), bb = tb ^ (uint32_t)(64 * db);
+      t[0] = trd_off(a, s2 * 16 * ROWB + QT);  // dO^T rows (A operand of dV)
+      t[1] = trd_off(bb, s2 * 16 * ROWB + QT);
+      t[2] = trd_off(a, s2 * 16 * ROWB);       // Q^T rows (A operand of dK)
+      t[3] = trd_off(bb, s2 * 16 * ROWB);
+    };
+    issue(0, tr[0]);
 #pragma unroll
-      for (int db = 0; db < DB; ++db) {
-        const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
-        const int oA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
-        const int oB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
-        const u16x4 a0 = trd(dot + oA), a1 = trd(dot + oB);
-        dv[db] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]}, pb, dv[db]);
-        const u16x4 b0 = trd(qt + oA), b1 = trd(qt + oB);
-        dk[db] = mfma32b(u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]}, sb, dk[db]);
-      }
+    for (int i = 0; i < 2 * DB; ++i) {
+      if (i + 1 < 2 * DB) issue(i + 1, tr[(i + 1) & 1]);
+      lds_wait_le(i + 1 < 2 * DB ? 4 : 0);
+      u16x4(&t)[4] = tr[i & 1];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) pin(t[x]);
+      const int s2 = i / DB, db = i % DB;
+      dv[db] = mfma32b(u16x8{t[0][0], t[0][1], t[0][2], t[0][3], t[1][0], t[1][1], t[1][2], t[1][3]}, pb[s2], dv[db]);
+      dk[db] = mfma32b(u16x8{t[2][0], t[2][1], t[2][2], t[2][3], t[3][0], t[3][1], t[3][2], t[3][3]}, sb[s2], dk[db]);
     }
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq)
@@ -834,14 +891,18 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_BWD8");
     return !(e && e[0] == '0');
   }();
+  static const int bwd8_prio = [] {  // MXLLM_ATTN_BWD8_PRIO=1: s_setprio 1 for waves 4-7 (experiment)
+    const char* e = getenv("MXLLM_ATTN_BWD8_PRIO");
+    return e && *e ? atoi(e) : 1;
+  }();
   if (dq_mode == 3 && D == 128 && bwd8) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     if (causal)
       attn_bwd8_kernel<true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk, off,
-                                                       sl, scale, S_pad);
+                                                       sl, scale, S_pad, bwd8_prio);
     else
       attn_bwd8_kernel<false><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
-                                                        off, sl, scale, S_pad);
+                                                        off, sl, scale, S_pad, bwd8_prio);
   } else {
 #define BWD(DD, C)                                                                                                  \
   do {                                                                                                              \
