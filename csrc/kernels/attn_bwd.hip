@@ -808,6 +808,45 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
     if (it + NSTAGE - 1 < nkt) glds(it + NSTAGE - 1);
     if (it < nkt_w) {
       const uint32_t sb = lds0 + (uint32_t)((it % NSTAGE) * BUF);
+      if constexpr (NT == 2 && DB == 4) {
+        // D = 128: this wave's two tiles are (m = 0, db = wl) and (m = 1, db = wl): one set
+        // of K fragments feeds both (3 tr-reads per MFMA instead of 4; the loop is LDS-bound)
+        u16x4 fa[2][4][2], fb[4][2];
+#define MX_DQ_READ2(S)                                                 \
+  fb[S][0] = trd_asm<S * 16 * ROWB>(sb + bA[0]);                       \
+  fb[S][1] = trd_asm<S * 16 * ROWB>(sb + bB[0]);                       \
+  fa[0][S][0] = trd_asm<S * 16 * DSROWB>(sb + aA[0]);                  \
+  fa[0][S][1] = trd_asm<S * 16 * DSROWB>(sb + aB[0]);                  \
+  fa[1][S][0] = trd_asm<S * 16 * DSROWB>(sb + aA[1]);                  \
+  fa[1][S][1] = trd_asm<S * 16 * DSROWB>(sb + aB[1]);
+        MX_DQ_READ2(0) MX_DQ_READ2(1) MX_DQ_READ2(2) MX_DQ_READ2(3)
+#undef MX_DQ_READ2
+        lds_wait_le(12);  // k steps 0 and 1 landed (steps 2 and 3 still in flight)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          pin(fb[s2][0]); pin(fb[s2][1]);
+          pin(fa[0][s2][0]); pin(fa[0][s2][1]); pin(fa[1][s2][0]); pin(fa[1][s2][1]);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < BK / 16; ++s2) {
+          if (s2 == 2) {
+            lds_wait();
+#pragma unroll
+            for (int x = 2; x < 4; ++x) {
+              pin(fb[x][0]); pin(fb[x][1]);
+              pin(fa[0][x][0]); pin(fa[0][x][1]); pin(fa[1][x][0]); pin(fa[1][x][1]);
+            }
+          }
+          const u16x4 b0 = fb[s2][0], b1 = fb[s2][1];
+          const u16x8 bf = u16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const u16x4 a0 = fa[t][s2][0], a1 = fa[t][s2][1];
+            acc[t] = mfma32b(u16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]}, bf, acc[t]);
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if (wl + 4 * t < 2 * DB) {
