@@ -20,7 +20,9 @@
 //    fused into the inverse-RoPE merge kernel (rope.hip), so no atomics and a
 //    deterministic dK/dV;
 //  * heaviest key blocks (most visible q tiles) scheduled first.
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "common.h"
 
@@ -111,7 +113,7 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 
   const int nkb = (Sk + BN - 1) / BN;
   const int BH = B * Hq;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
   const int kb = bid / BH;  // ascending: key block 0 sees the most q tiles (causal) -> heaviest first
   const int bh = bid % BH;
   if (kb >= nkb) return;
@@ -392,12 +394,13 @@ attn_bwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 // from LDS images of the key block instead of registers — the register file then holds two
 // waves per SIMD (the hardware interleaves one wave's softmax VALU with the other's MFMAs, which
 // the one-wave kernel cannot).  The two halves' dK / dV partials are summed through LDS at the end.
-template <bool CAUSAL>
+template <bool CAUSAL, bool PROF = false>
 __global__ void __launch_bounds__(512, 1)
 attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                  const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                  uint16_t* __restrict__ dST, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq,
-                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad, int prio) {
+                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad, int prio,
+                 uint32_t* __restrict__ prof = nullptr) {
   constexpr int D = 128, BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int KIMG = BN * ROWB;     // K (or V) image [128][D]
   constexpr int QT = BQ * ROWB;       // Q / dO tile [64][D]
@@ -411,9 +414,11 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
 
+  uint64_t t_entry = 0;
+  if constexpr (PROF) t_entry = __builtin_amdgcn_s_memtime();
   const int nkb = (Sk + BN - 1) / BN;
   const int BH = B * Hq;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
   const int kb = bid / BH;
   const int bh = bid % BH;
   if (kb >= nkb) return;
@@ -471,34 +476,45 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     qoff[i] = prow * ROWB + pch * 16;
     ooff[i] = (int)(prow * dstride * 2) + pch * 16;
   }
-  auto glds = [&](int it, int buf) {
+  // piece k of the DMA of q tile `it` into buffer `buf`: 0..3 = Q / dO rows, 4 = lse + delta
+  // (wave 0); glds = all of them
+  auto glds_piece = [&](int it, int buf, int k) {
     char* qt = smem + 2 * KIMG + buf * BUF;
     char* dot = qt + QT;
     char* ld = dot + QT;
     const int q0 = (prio & 2) ? qstart : qstart + it * BQ;  // (prio & 2: timing ablation, same tile)
-    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp, 0, S * ROWB, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp, 0, orec, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < SEGS / 8; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(qt + (pseg + i) * 1024), 16, qoff[i] + q0 * ROWB, 0, 0,
-                                               0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (lptr_t)(dot + (pseg + i) * 1024), 16,
-                                               ooff[i] + (int)(q0 * dstride * 2), 0, 0, 0);
-    }
-    if (w == 0) {
+    if (k < 4) {
+      const int i = k >> 1;
+      if ((k & 1) == 0) {
+        const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp, 0, S * ROWB, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(qt + (pseg + i) * 1024), 16, qoff[i] + q0 * ROWB, 0,
+                                                 0, 0);
+      } else {
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp, 0, orec, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (lptr_t)(dot + (pseg + i) * 1024), 16,
+                                                 ooff[i] + (int)(q0 * dstride * 2), 0, 0, 0);
+      }
+    } else if (w == 0) {
       const int q = min(q0 + lane, S - 1);
       __builtin_amdgcn_global_load_lds((gptr_t)(lsep + q), (lptr_t)(ld), 4, 0, 0);
       __builtin_amdgcn_global_load_lds((gptr_t)(delp + q), (lptr_t)(ld + BQ * 4), 4, 0, 0);
     }
   };
+  auto glds = [&](int it, int buf) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) glds_piece(it, buf, k);
+  };
 
   u16x4 dsv[4];
   int ds_q0 = -1;
-  auto flush_ds = [&]() {
+  auto flush_ds_piece = [&](int gq) {
     if (ds_q0 < 0) return;
     uint16_t* rowp = dstp + ((size_t)(ds_q0 / BQ) * (nkb * BN) + key) * BQ + 32 * m;
+    *reinterpret_cast<u16x4*>(rowp + 8 * gq + 4 * hh) = dsv[gq];
+  };
+  auto flush_ds = [&]() {
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq) *reinterpret_cast<u16x4*>(rowp + 8 * gq + 4 * hh) = dsv[gq];
+    for (int gq = 0; gq < 4; ++gq) flush_ds_piece(gq);
   };
 
   // transposed-read lane offsets into a q tile (rows 32m + 4hh + tq (+8); chunk of d-block db);
@@ -524,15 +540,38 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   if (nqt > 0) glds(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
+  // PROF: per-wave cycle sums of the loop phases (s_memtime at phase boundaries; diagnostic
+  // build only, MXLLM_ATTN_PROF=1): issue, S/dP MFMAs issued, softmax done, dV/dK issued, barrier
+  uint32_t ph[5] = {0, 0, 0, 0, 0};
+  uint64_t tp0 = 0;
+  auto mark = [&](int k) {
+    if constexpr (PROF) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph[k] += (uint32_t)(t - tp0);
+      tp0 = t;
+    }
+  };
+  uint64_t t_beg = 0, rt_beg = 0;
+  if constexpr (PROF) {
+    t_beg = __builtin_amdgcn_s_memtime();
+    rt_beg = __builtin_amdgcn_s_memrealtime();
+  }
   for (int it = 0; it < nqt; ++it) {
+    if constexpr (PROF) tp0 = __builtin_amdgcn_s_memtime();
     const int q0 = qstart + it * BQ;
     const int buf = it & 1;
     const char* qt = smem + 2 * KIMG + buf * BUF;
     const char* dot = qt + QT;
     const float* lse_s = reinterpret_cast<const float*>(dot + QT);
     const float* del_s = lse_s + BQ;
-    if (it + 1 < nqt) glds(it + 1, buf ^ 1);
-    flush_ds();
+    const bool late = (prio & 8) != 0;  // (experiment: DMA issue + dS stores after the S/dP MFMAs)
+    const bool spread = (prio & 16) != 0;  // (experiment: one DMA piece / dS store per MFMA step)
+    const bool more = it + 1 < nqt;
+    if (!late && !spread) {
+      if (it + 1 < nqt) glds(it + 1, buf ^ 1);
+      flush_ds();
+    }
+    mark(0);
     const bool need_mask = (q0 + BQ > S) || (k0 + BN > Sk) || (CAUSAL && (k0 + 32 * kg + 31 > q0 + 32 * m + off));
     f32x16 sa, dp;
 #pragma unroll
@@ -557,8 +596,15 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         for (int y = 0; y < 4; ++y) pin(x[y]);
         sa = mfma32b(x[0], x[1], sa);
         dp = mfma32b(x[2], x[3], dp);
+        if (spread && (st & 1) == 0 && more) glds_piece(it + 1, buf ^ 1, st >> 1);
+        if (spread && st == KS - 1 && more) glds_piece(it + 1, buf ^ 1, 4);
       }
     }
+    if (late) {
+      if (it + 1 < nqt) glds(it + 1, buf ^ 1);
+      flush_ds();
+    }
+    mark(1);
     // rows of sa/dp: q = q0 + 32m + (j&3) + 8(j>>2) + 4hh ; column = key (lane)
     if (need_mask) {  // wave-uniform: two straight-line bodies, branch-free selects
 #pragma unroll
@@ -600,6 +646,8 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         pb[s2][j] = f2bf(sa[8 * s2 + j]);
         sb[s2][j] = f2bf(dp[8 * s2 + j]);
       }
+    if constexpr (PROF) asm volatile("" ::"v"(pb[1]), "v"(sb[1]));
+    mark(2);
     const uint32_t tbase = tile_base + buf * BUF;
     const uint32_t ta = tbase + trA, tb = tbase + trB;
     u16x4 tr[2][4];
@@ -622,13 +670,30 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
       const int s2 = i / DB, db = i % DB;
       dv[db] = mfma32b(u16x8{t[0][0], t[0][1], t[0][2], t[0][3], t[1][0], t[1][1], t[1][2], t[1][3]}, pb[s2], dv[db]);
       dk[db] = mfma32b(u16x8{t[2][0], t[2][1], t[2][2], t[2][3], t[3][0], t[3][1], t[3][2], t[3][3]}, sb[s2], dk[db]);
+      if (spread && (i & 1) == 0) flush_ds_piece(i >> 1);
     }
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq)
       dsv[gq] = u16x4{f2bf(dp[4 * gq]), f2bf(dp[4 * gq + 1]), f2bf(dp[4 * gq + 2]), f2bf(dp[4 * gq + 3])};
     ds_q0 = q0;
+    mark(3);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next tile landed
     __syncthreads();                     // ... and every wave's; this tile's buffers consumed
+    mark(4);
+  }
+  if constexpr (PROF) {
+    if (lane < 5) {
+      uint32_t v = ph[0];
+#pragma unroll
+      for (int k = 1; k < 5; ++k) v = lane == k ? ph[k] : v;
+      prof[((size_t)blockIdx.x * 8 + w) * 16 + lane] = v;
+    }
+    if (lane == 5) prof[((size_t)blockIdx.x * 8 + w) * 16 + 5] = (uint32_t)nqt;
+    const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memtime() - t_beg);
+    const uint32_t drt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - rt_beg);
+    if (lane == 6) prof[((size_t)blockIdx.x * 8 + w) * 16 + 6] = dt;
+    if (lane == 7) prof[((size_t)blockIdx.x * 8 + w) * 16 + 7] = drt;
+    if (lane == 8) prof[((size_t)blockIdx.x * 8 + w) * 16 + 8] = (uint32_t)(t_beg - t_entry);
   }
   flush_ds();
   // sum the two halves' partials: m = 1 waves park theirs in LDS ([kg][value][lane], conflict-free)
@@ -665,6 +730,10 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         *reinterpret_cast<f32x4*>(dvq + d) = f32x4{dv[db][4 * gq], dv[db][4 * gq + 1], dv[db][4 * gq + 2],
                                                   dv[db][4 * gq + 3]};
       }
+  }
+  if constexpr (PROF) {
+    const uint64_t t_end = __builtin_amdgcn_s_memtime();
+    if (lane == 9) prof[((size_t)blockIdx.x * 8 + w) * 16 + 9] = (uint32_t)(t_end - t_beg);
   }
 }
 
@@ -721,7 +790,7 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
 
   const int nqb = (S + BQ * QB - 1) / (BQ * QB);
   const int BH = B * Hq;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
   const int qb = nqb - 1 - bid / BH;  // causal: last q blocks see the most keys -> first
   const int bh = bid % BH;
   const int b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
@@ -934,7 +1003,44 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_BWD8_PRIO");
     return e && *e ? atoi(e) : 1;
   }();
-  if (dq_mode == 3 && D == 128 && bwd8) {
+  static const bool bwd8_prof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report of the 8-wave kernel (stderr)
+    const char* e = getenv("MXLLM_ATTN_PROF");
+    return e && e[0] == '1';
+  }();
+  if (dq_mode == 3 && D == 128 && bwd8 && bwd8_prof) {
+    uint16_t* dst = reinterpret_cast<uint16_t*>(work);
+    uint32_t* pbuf = nullptr;
+    const size_t n = (size_t)grid * 128;
+    if (hipMalloc(&pbuf, n * 4) != hipSuccess) return -1;
+    (void)hipMemsetAsync(pbuf, 0, n * 4, stream);
+    if (causal)
+      attn_bwd8_kernel<true, true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
+                                                             off, sl, scale, S_pad, bwd8_prio, pbuf);
+    else
+      attn_bwd8_kernel<false, true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S,
+                                                              Sk, off, sl, scale, S_pad, bwd8_prio, pbuf);
+    std::vector<uint32_t> h(n);
+    (void)hipMemcpyAsync(h.data(), pbuf, n * 4, hipMemcpyDeviceToHost, stream);
+    (void)hipStreamSynchronize(stream);
+    (void)hipFree(pbuf);
+    double sum[2][5] = {}, tiles[2] = {}, tt = 0, rt = 0, pro = 0, epi = 0;
+    for (size_t wv = 0; wv < (size_t)grid * 8; ++wv) {
+      const int half = (int)(wv % 8) >> 2;
+      for (int kk = 0; kk < 5; ++kk) sum[half][kk] += h[wv * 16 + kk];
+      tiles[half] += h[wv * 16 + 5];
+      tt += h[wv * 16 + 6];
+      rt += h[wv * 16 + 7];
+      pro += h[wv * 16 + 8];
+      epi += (double)h[wv * 16 + 9] - h[wv * 16 + 6];
+    }
+    const double nwv = (double)grid * 8;
+    fprintf(stderr, "[attn_bwd8 prof] s_memtime rate %.0f MHz; per wave: prologue %.0f, loop %.0f, epilogue %.0f cycles\n",
+            rt > 0 ? 100.0 * tt / rt : 0.0, pro / nwv, tt / nwv, epi / nwv);
+    for (int half = 0; half < 2; ++half)
+      fprintf(stderr, "[attn_bwd8 prof] waves %d-%d cycles/tile: issue %.0f  S,dP %.0f  softmax %.0f  dV,dK %.0f  barrier %.0f\n",
+              4 * half, 4 * half + 3, sum[half][0] / tiles[half], sum[half][1] / tiles[half], sum[half][2] / tiles[half],
+              sum[half][3] / tiles[half], sum[half][4] / tiles[half]);
+  } else if (dq_mode == 3 && D == 128 && bwd8) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     if (causal)
       attn_bwd8_kernel<true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk, off,

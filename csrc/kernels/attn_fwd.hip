@@ -65,7 +65,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 
   const int nqb = (S + BM - 1) / BM;
   const int BH = B * Hq;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
   const int qb = nqb - 1 - bid / BH;
   const int bh = bid % BH;
   const int b = bh / Hq, h = bh % Hq;
@@ -312,7 +312,7 @@ attn_fwd_p_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K
 
   const int nqb = (S + BM - 1) / BM;
   const int BH = B * Hq;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
   const int qb = nqb - 1 - bid / BH;
   const int bh = bid % BH;
   const int b = bh / Hq, h = bh % Hq;

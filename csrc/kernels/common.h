@@ -82,6 +82,24 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// Bijective remap for grids of (outer, bh) work items, bid = outer * BH + bh, whose cost
+// varies with `outer` (causal attention: heaviest outer index first).  Workgroups are dealt
+// round-robin over the 8 XCDs (MI355X_MICROARCH "Workgroup dispatch"): blocks b, b + 8, ...
+// share one.  xcd_remap above gives each XCD a CONTIGUOUS bid range, i.e. a narrow band of
+// outer indices, so one XCD ran all the heavy blocks while another idled (causal attention
+// at B2 Hq64: 644 µs where the per-CU work is ~410).  Here XCD x takes the KV groups (G
+// consecutive q-heads sharing one K/V head) {x, x + 8, ...} -> K / V stay in one L2 -- and
+// walks them through every outer index in dispatch order, so every XCD sees the same
+// heavy-to-light mix.  Falls back to identity (round-robin already balances) when BH is not
+// a multiple of 8 G.
+__device__ __forceinline__ int xcd_balance(int orig, int nwg, int BH, int G) {
+  if ((nwg & 7) || G <= 0 || BH % (8 * G) || nwg % BH) return orig;
+  const int x = orig & 7, j = orig >> 3, per = BH >> 3;
+  const int outer = j / per, lb = j % per;
+  const int bh = ((lb / G) * 8 + x) * G + lb % G;
+  return outer * BH + bh;
+}
+
 // ---- LDS-DMA-friendly transposed reads (used by the attention kernels) ----
 // ds_read_b64_tr_b16 as inline asm with an immediate offset: invisible to hipcc's
 // waitcnt pass, which otherwise drains every in-flight LDS-DMA (vmcnt(0)) before a
