@@ -564,10 +564,13 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     const char* dot = qt + QT;
     const float* lse_s = reinterpret_cast<const float*>(dot + QT);
     const float* del_s = lse_s + BQ;
-    const bool late = (prio & 8) != 0;  // (experiment: DMA issue + dS stores after the S/dP MFMAs)
-    const bool spread = (prio & 16) != 0;  // (experiment: one DMA piece / dS store per MFMA step)
+    // spread (prio & 16, default): the next tile's DMA pieces go out one per S/dP k step and the
+    // previous tile's dS stores one per dV/dK step -- issued in one burst at the loop top, the 8
+    // waves' vector-memory instructions queued behind each other and the low-priority half
+    // stalled there ~2000 cycles per tile (phase profile, profiles/r2z_bwd8_phase_cycles.txt)
+    const bool spread = (prio & 16) != 0;
     const bool more = it + 1 < nqt;
-    if (!late && !spread) {
+    if (!spread) {
       if (it + 1 < nqt) glds(it + 1, buf ^ 1);
       flush_ds();
     }
@@ -599,10 +602,6 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         if (spread && (st & 1) == 0 && more) glds_piece(it + 1, buf ^ 1, st >> 1);
         if (spread && st == KS - 1 && more) glds_piece(it + 1, buf ^ 1, 4);
       }
-    }
-    if (late) {
-      if (it + 1 < nqt) glds(it + 1, buf ^ 1);
-      flush_ds();
     }
     mark(1);
     // rows of sa/dp: q = q0 + 32m + (j&3) + 8(j>>2) + 4hh ; column = key (lane)
@@ -999,9 +998,12 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_BWD8");
     return !(e && e[0] == '0');
   }();
-  static const int bwd8_prio = [] {  // MXLLM_ATTN_BWD8_PRIO=1: s_setprio 1 for waves 4-7 (experiment)
+  // MXLLM_ATTN_BWD8_PRIO (bit flags, default 17): 1 = s_setprio 1 for waves 4-7, 16 = spread the
+  // DMA / dS-store issue over the MFMA steps; 2 = timing ablation (same q tile every step, wrong
+  // results)
+  static const int bwd8_prio = [] {
     const char* e = getenv("MXLLM_ATTN_BWD8_PRIO");
-    return e && *e ? atoi(e) : 1;
+    return e && *e ? atoi(e) : 17;
   }();
   static const bool bwd8_prof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report of the 8-wave kernel (stderr)
     const char* e = getenv("MXLLM_ATTN_PROF");

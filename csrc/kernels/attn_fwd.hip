@@ -24,6 +24,8 @@
 //    (only when a row max grows by > 2^8: guide T13);
 //  * causal blocks scheduled heaviest-first, XCD-aware block remap so the
 //    q-heads sharing one KV head run on the same XCD (shared L2).
+#include <cstdlib>
+
 #include "common.h"
 #include <stdlib.h>
 
@@ -56,7 +58,7 @@ template <int D, bool CAUSAL, int NW>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
-                int causal_off, float sl, int ldo) {
+                int causal_off, float sl, int ldo, int flags) {
   constexpr int BM = 32 * NW, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int TILE = BN * ROWB;
   constexpr int LPT = BN * CH / (64 * NW);
@@ -111,17 +113,21 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     const int row = byte / ROWB, slot = (byte % ROWB) / 16;
     voff[i] = row * ROWB + 16 * (slot ^ swz<CH>(row));  // logical chunk stored in this slot
   }
-  auto glds = [&](int kt, int buf) {
+  auto glds_piece = [&](int kt, int buf, int i) {
     char* kb = smem + buf * 2 * TILE;
     char* vb = kb + TILE;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int seg = w * LPT + i;
-      const int off = voff[i] + kt * TILE;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kb + seg * 1024), 16, off, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vb + seg * 1024), 16, off, 0, 0, 0);
-    }
+    const int seg = w * LPT + i;
+    const int off = voff[i] + kt * TILE;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kb + seg * 1024), 16, off, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vb + seg * 1024), 16, off, 0, 0, 0);
   };
+  auto glds = [&](int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) glds_piece(kt, buf, i);
+  };
+  // flags & 1: spread the next tile's DMA over the QK^T k steps (one K + V piece per step pair)
+  // instead of one burst at the tile top
+  const bool spread = (flags & 1) != 0;
 
   f32x16 o[DB];
 #pragma unroll
@@ -158,9 +164,10 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   // One 64-key tile out of ring buffer CUR (compile-time).
   auto tile = [&](auto cur_c, int kt) {
     constexpr int CUR = decltype(cur_c)::value;
-    if (kt + 1 < ntiles) glds(kt + 1, CUR ^ 1);  // prefetch next tile into the other buffer
+    const bool more = kt + 1 < ntiles;
     const char* kb = smem + CUR * 2 * TILE;
     const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
+    if (more && (!spread || !active)) glds(kt + 1, CUR ^ 1);  // prefetch next tile into the other buffer
     if (active) {
       f32x16 sacc[2];
 #pragma unroll
@@ -172,6 +179,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         for (int s = 0; s < KS; ++s) {
           const u16x8 a = *reinterpret_cast<const u16x8*>(kb + krow * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(krow)));
           sacc[n] = mfma32(a, qf[s], sacc[n]);
+          if (spread && more && n == 0 && (s % (KS / LPT)) == 0) glds_piece(kt + 1, CUR ^ 1, s / (KS / LPT));
         }
       }
       // row max of the RAW scores (the scale is folded into the exp2 argument below)
@@ -659,9 +667,13 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_FWD_WAVES");
     return (e && e[0] == '8') ? 8 : 4;
   }();
+  static const int fflags = [] {  // MXLLM_ATTN_FWD_FLAGS (default 1): bit 0 = spread the K/V DMA issue
+    const char* e = getenv("MXLLM_ATTN_FWD_FLAGS");   // (B2 0.192 -> 0.186 ms, B16 1.372 -> 1.357 ms)
+    return e && *e ? atoi(e) : 1;
+  }();
 #define FWD(DD, C, NWV)                                                                                  \
   attn_fwd_kernel<DD, C, NWV><<<((S + 32 * NWV - 1) / (32 * NWV)) * B * Hq, 64 * NWV, 0, stream>>>(     \
-      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo)
+      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
   if (D == 128) {
     if (nw128 == 8) { if (causal) FWD(128, true, 8); else FWD(128, false, 8); }
     else { if (causal) FWD(128, true, 4); else FWD(128, false, 4); }
