@@ -24,7 +24,9 @@
 //    (only when a row max grows by > 2^8: guide T13);
 //  * causal blocks scheduled heaviest-first, XCD-aware block remap so the
 //    q-heads sharing one KV head run on the same XCD (shared L2).
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "common.h"
 #include <stdlib.h>
@@ -54,16 +56,27 @@ __device__ __forceinline__ u16x4 tr_read(const char* p) {
 // NW waves per workgroup = 32 NW query rows sharing every streamed K/V tile (2 waves per SIMD
 // either way).  4 by default; 8 halves the K/V tile traffic per FLOP but measured the same
 // (0.259 vs 0.257 ms at B2 S2048 Hq64 Hkv8 D128 causal: the stream is not the limiter)
-template <int D, bool CAUSAL, int NW>
+template <int D, bool CAUSAL, int NW, bool PROF = false>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
-                int causal_off, float sl, int ldo, int flags) {
+                int causal_off, float sl, int ldo, int flags, uint32_t* __restrict__ prof = nullptr) {
+  // PROF (diagnostic build, MXLLM_ATTN_PROF=1): per-wave s_memtime cycle sums of the tile phases
+  uint32_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t tp0 = 0, t_entry = 0, t_loop = 0;
+  auto mark = [&](int k) {
+    if constexpr (PROF) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph[k] += (uint32_t)(t - tp0);
+      tp0 = t;
+    }
+  };
+  if constexpr (PROF) t_entry = __builtin_amdgcn_s_memtime();
   constexpr int BM = 32 * NW, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int TILE = BN * ROWB;
   constexpr int LPT = BN * CH / (64 * NW);
   static_assert(LPT >= 1 && BN * CH % (64 * NW) == 0, "K/V tile must split evenly over the waves");
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE];  // (XOR addressing: 256-B aligned)
 
   const int nqb = (S + BM - 1) / BM;
   const int BH = B * Hq;
@@ -153,6 +166,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     va_base[db][1] = lds0 + TILE + rB * ROWB + 16 * (chunk ^ swz<CH>(rB)) + 8 * (tp & 1);
   }
 
+  const uint32_t kq_base = lds0 + r * ROWB + 16 * (hh ^ swz<CH>(r));  // K row r, k step 0 (D = 128 path)
   if (ntiles > 0) glds(0, 0);
   // Retire the prologue's Q loads and tile-0 DMA with a wait the compiler's
   // waitcnt pass can see (otherwise it treats them as possibly pending at the
@@ -162,8 +176,10 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   const int wq_hi = q0 + 32 * w + 31;
 
   // One 64-key tile out of ring buffer CUR (compile-time).
+  if constexpr (PROF) t_loop = __builtin_amdgcn_s_memtime();
   auto tile = [&](auto cur_c, int kt) {
     constexpr int CUR = decltype(cur_c)::value;
+    if constexpr (PROF) tp0 = __builtin_amdgcn_s_memtime();
     const bool more = kt + 1 < ntiles;
     const char* kb = smem + CUR * 2 * TILE;
     const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
@@ -171,20 +187,49 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     if (active) {
       f32x16 sacc[2];
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
+      for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int j = 0; j < 16; ++j) sacc[n][j] = 0.f;
-        const int krow = n * 32 + r;
+      if constexpr (D == 128) {
+        // both 32-key chains interleaved; K rows by asm reads one k step ahead (counted waits).
+        // Key rows 32n + r share row & 15 with r, hence the swizzle: k step s is base ^ (32 s),
+        // the buffer and the 32-row block n are immediates
+        u16x8 kf2[2][2];
+        auto ld = [&](int st, u16x8 (&x)[2]) {
+          const uint32_t a = kq_base ^ (uint32_t)(32 * st);
+          x[0] = rd128_off(a, CUR * 2 * TILE);
+          x[1] = rd128_off(a, CUR * 2 * TILE + 32 * ROWB);
+        };
+        ld(0, kf2[0]);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const u16x8 a = *reinterpret_cast<const u16x8*>(kb + krow * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(krow)));
-          sacc[n] = mfma32(a, qf[s], sacc[n]);
-          if (spread && more && n == 0 && (s % (KS / LPT)) == 0) glds_piece(kt + 1, CUR ^ 1, s / (KS / LPT));
+        for (int st = 0; st < KS; ++st) {
+          if (st + 1 < KS) ld(st + 1, kf2[(st + 1) & 1]);
+          lds_wait_le(st + 1 < KS ? 2 : 0);
+          u16x8(&x)[2] = kf2[st & 1];
+          pin(x[0]);
+          pin(x[1]);
+          sacc[0] = mfma32(x[0], qf[st], sacc[0]);
+          sacc[1] = mfma32(x[1], qf[st], sacc[1]);
+          if (spread && more && (st % (KS / LPT)) == 0) glds_piece(kt + 1, CUR ^ 1, st / (KS / LPT));
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int krow = n * 32 + r;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const u16x8 a = *reinterpret_cast<const u16x8*>(kb + krow * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(krow)));
+            sacc[n] = mfma32(a, qf[s], sacc[n]);
+            if (spread && more && n == 0 && (s % (KS / LPT)) == 0) glds_piece(kt + 1, CUR ^ 1, s / (KS / LPT));
+          }
         }
       }
+      mark(0);
       // row max of the RAW scores (the scale is folded into the exp2 argument below)
       float mx = -INFINITY;
       const bool need_mask = (kt * BN + BN > Sk) || (CAUSAL && (kt * BN + BN - 1 > q0 + 32 * w + causal_off));
+      // 4 independent partial maxima (a 32-long dependent fmax chain otherwise)
+      float mp[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       if (need_mask) {  // wave-uniform: diagonal / tail tiles only; branch-free select per element
 #pragma unroll
         for (int n = 0; n < 2; ++n)
@@ -194,14 +239,15 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
             const bool dead = (key >= Sk) | (CAUSAL & (key > qrow + causal_off));
             const float x = dead ? -INFINITY : sacc[n][j];
             sacc[n][j] = x;
-            mx = fmaxf(mx, x);
+            mp[j & 3] = fmaxf(mp[j & 3], x);
           }
       } else {
 #pragma unroll
         for (int n = 0; n < 2; ++n)
 #pragma unroll
-          for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sacc[n][j]);
+          for (int j = 0; j < 16; ++j) mp[j & 3] = fmaxf(mp[j & 3], sacc[n][j]);
       }
+      mx = fmaxf(fmaxf(mp[0], mp[1]), fmaxf(mp[2], mp[3]));
       {  // max with the other half-wave (same query column): one permlane32 swap
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
         mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
@@ -221,16 +267,18 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         for (int d = 0; d < DB; ++d) o[d] *= alpha;
       }
       const float nm = -m_i;
-      float ls = 0.f;
+      float lp[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent partial sums
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][j], sl, nm));
           sacc[n][j] = p;
-          ls += p;
+          lp[j & 3] += p;
         }
-      l_i += ls;
+      l_i += (lp[0] + lp[1]) + (lp[2] + lp[3]);
+      if constexpr (PROF) asm volatile("" ::"v"(l_i));
+      mark(1);
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -256,9 +304,14 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
             o[db] = mfma32(a, pb, o[db]);
           }
         }
+      mark(2);
+    } else {
+      mark(5);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for tile kt+1 landed
     __syncthreads();                     // ... and every other wave's; buffer CUR free again
+    mark(3);
+    if constexpr (PROF) ph[4] += 1;
   };
   for (int kt = 0; kt < ntiles; kt += 2) {
     tile(std::integral_constant<int, 0>{}, kt);
@@ -283,6 +336,18 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         *reinterpret_cast<u16x4*>(op + d) = v4;
       }
     if (hh == 0) LSE[(size_t)(b * Hq + h) * S + qrow] = m_i + __log2f(l_tot);
+  }
+  if constexpr (PROF) {
+    const uint64_t t_end = __builtin_amdgcn_s_memtime();
+    uint32_t* pw = prof + ((size_t)blockIdx.x * NW + w) * 16;
+    if (lane < 6) {
+      uint32_t v = ph[0];
+#pragma unroll
+      for (int k = 1; k < 6; ++k) v = lane == k ? ph[k] : v;
+      pw[lane] = v;
+    }
+    if (lane == 6) pw[6] = (uint32_t)(t_loop - t_entry);
+    if (lane == 7) pw[7] = (uint32_t)(t_end - t_loop);
   }
 }
 
@@ -674,6 +739,32 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
 #define FWD(DD, C, NWV)                                                                                  \
   attn_fwd_kernel<DD, C, NWV><<<((S + 32 * NWV - 1) / (32 * NWV)) * B * Hq, 64 * NWV, 0, stream>>>(     \
       q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
+  static const bool fprof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report (D = 128, 4 waves; stderr)
+    const char* e = getenv("MXLLM_ATTN_PROF");
+    return e && e[0] == '1';
+  }();
+  if (D == 128 && nw128 == 4 && causal && fprof) {
+    const unsigned grid = ((S + 127) / 128) * B * Hq;
+    const size_t n = (size_t)grid * 4 * 16;
+    uint32_t* pbuf = nullptr;
+    if (hipMalloc(&pbuf, n * 4) != hipSuccess) return -1;
+    (void)hipMemsetAsync(pbuf, 0, n * 4, stream);
+    attn_fwd_kernel<128, true, 4, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo,
+                                                                  fflags, pbuf);
+    std::vector<uint32_t> h(n);
+    (void)hipMemcpyAsync(h.data(), pbuf, n * 4, hipMemcpyDeviceToHost, stream);
+    (void)hipStreamSynchronize(stream);
+    (void)hipFree(pbuf);
+    double sm[8] = {};
+    for (size_t wv = 0; wv < (size_t)grid * 4; ++wv)
+      for (int kk = 0; kk < 8; ++kk) sm[kk] += h[wv * 16 + kk];
+    const double nt = sm[4] > 0 ? sm[4] : 1, nwv = (double)grid * 4;
+    fprintf(stderr,
+            "[attn_fwd prof] cycles/tile: QK^T %.0f  softmax %.0f  PV %.0f  barrier %.0f  (skipped-tile %.0f); per wave: "
+            "prologue %.0f, loop+epilogue %.0f, tiles %.1f\n",
+            sm[0] / nt, sm[1] / nt, sm[2] / nt, sm[3] / nt, sm[5] / nt, sm[6] / nwv, sm[7] / nwv, nt / nwv);
+    return (int)hipGetLastError();
+  }
   if (D == 128) {
     if (nw128 == 8) { if (causal) FWD(128, true, 8); else FWD(128, false, 8); }
     else { if (causal) FWD(128, true, 4); else FWD(128, false, 4); }
