@@ -573,6 +573,8 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     if (!spread) {
       if (it + 1 < nqt) glds(it + 1, buf ^ 1);
       flush_ds();
+    } else if (prio & 64) {
+      flush_ds();
     }
     mark(0);
     const bool need_mask = (q0 + BQ > S) || (k0 + BN > Sk) || (CAUSAL && (k0 + 32 * kg + 31 > q0 + 32 * m + off));
@@ -669,7 +671,9 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
       const int s2 = i / DB, db = i % DB;
       dv[db] = mfma32b(u16x8{t[0][0], t[0][1], t[0][2], t[0][3], t[1][0], t[1][1], t[1][2], t[1][3]}, pb[s2], dv[db]);
       dk[db] = mfma32b(u16x8{t[2][0], t[2][1], t[2][2], t[2][3], t[3][0], t[3][1], t[3][2], t[3][3]}, sb[s2], dk[db]);
-      if (spread && (i & 1) == 0) flush_ds_piece(i >> 1);
+      // dS stores here, not among the S/dP steps: next to the in-flight LDS-DMA they stalled
+      // issue (B16 5.13 -> 6.09 ms); (prio & 64: at the loop top instead, A/B)
+      if (spread && (i & 1) == 0 && (prio & 64) == 0) flush_ds_piece(i >> 1);
     }
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq)
