@@ -375,8 +375,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
   DevGuard g(q.device());
   const int64_t S_pad = (S + 63) / 64 * 64;
   const int64_t nkb = (Sk + 127) / 128;
-  auto dkp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
-  auto dvp = at::empty({B, Hq, Sk, D}, q.options().dtype(at::kFloat));
+  // dK / dV partials: [B, P, Sk, D] f32, P partial heads (Hq, or fewer when a workgroup of the
+  // 8-wave kernel sums several q-heads of a KV group); a KV head's partials are consecutive
+  const int64_t P = (causal >= 0 && dq_mode == 3)
+                        ? mx_attn_bwd_partial_heads((int)B, (int)Hq, (int)Hkv, (int)S, (int)Sk, (int)D, (int)dq_mode)
+                        : Hq;
+  auto dkp = at::empty({B, P, Sk, D}, q.options().dtype(at::kFloat));
+  auto dvp = at::empty({B, P, Sk, D}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   if (causal >= 0 && dq_mode != 1) {
     at::Tensor work = dq_mode == 2 ? at::empty({nkb, B, Hq, S_pad, D}, q.options().dtype(at::kFloat))

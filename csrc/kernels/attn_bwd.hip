@@ -399,7 +399,7 @@ __global__ void __launch_bounds__(512, 1)
 attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                  const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                  uint16_t* __restrict__ dST, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq,
-                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad, int prio,
+                 int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad, int prio, int hpw,
                  uint32_t* __restrict__ prof = nullptr) {
   constexpr int D = 128, BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
   constexpr int KIMG = BN * ROWB;     // K (or V) image [128][D]
@@ -417,20 +417,24 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   uint64_t t_entry = 0;
   if constexpr (PROF) t_entry = __builtin_amdgcn_s_memtime();
   const int nkb = (Sk + BN - 1) / BN;
-  const int BH = B * Hq;
-  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
-  const int kb = bid / BH;
-  const int bh = bid % BH;
+  // a workgroup = one key block x `hpw` q-heads of one KV group, looped over in turn: the K / V
+  // images load once and dK / dV accumulate over the heads in registers; it writes partial
+  // b * (Hq / hpw) + hp of dKp / dVp (the merge kernel sums the Hq / hpw / Hkv partials per KV head)
+  const int HP = Hq / hpw;  // partials per batch row
+  const int BHP = B * HP;
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BHP, (Hq / Hkv) / hpw);
+  const int kb = bid / BHP;
+  const int bhp = bid % BHP;
   if (kb >= nkb) return;
-  const int b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
-  const uint16_t* Qp = Q + (size_t)(b * Hq + h) * S * D;
+  const int b = bhp / HP, hp = bhp % HP, h0 = hp * hpw, hk = h0 / (Hq / Hkv);
   const uint16_t* Kp = K + (size_t)(b * Hkv + hk) * Sk * D;
   const uint16_t* Vp = V + (size_t)(b * Hkv + hk) * Sk * D;
   const size_t dstride = (size_t)Hq * D;
-  const uint16_t* dOp = dO + (size_t)b * S * dstride + (size_t)h * D;
-  const float* lsep = LSE + (size_t)(b * Hq + h) * S;
-  const float* delp = DELTA + (size_t)(b * Hq + h) * S;
-  uint16_t* dstp = dST + (size_t)(b * Hq + h) * (nkb * BN) * S_pad;
+  auto Qp = [&](int h) { return Q + (size_t)(b * Hq + h) * S * D; };
+  auto dOp = [&](int h) { return dO + (size_t)b * S * dstride + (size_t)h * D; };
+  auto lsep = [&](int h) { return LSE + (size_t)(b * Hq + h) * S; };
+  auto delp = [&](int h) { return DELTA + (size_t)(b * Hq + h) * S; };
+  auto dstp = [&](int h) { return dST + (size_t)(b * Hq + h) * (nkb * BN) * S_pad; };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -462,6 +466,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   int qstart = 0;
   if (CAUSAL) qstart = max(0, (k0 - off) / BQ * BQ);
   const int nqt = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
+  const int nit = nqt * hpw;  // flattened (head, q tile) iterations
 
   // Q / dO tile pieces: 2 per wave (one Q, one dO), range-checked buffer loads
   const int orec = (int)(((size_t)(S - 1) * dstride + D) * 2);
@@ -478,38 +483,40 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   }
   // piece k of the DMA of q tile `it` into buffer `buf`: 0..3 = Q / dO rows, 4 = lse + delta
   // (wave 0); glds = all of them
-  auto glds_piece = [&](int it, int buf, int k) {
+  // (hj, it): head h0 + hj, q tile it
+  auto glds_piece = [&](int hj, int it, int buf, int k) {
     char* qt = smem + 2 * KIMG + buf * BUF;
     char* dot = qt + QT;
     char* ld = dot + QT;
+    const int h = h0 + hj;
     const int q0 = (prio & 2) ? qstart : qstart + it * BQ;  // (prio & 2: timing ablation, same tile)
     if (k < 4) {
       const int i = k >> 1;
       if ((k & 1) == 0) {
-        const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp, 0, S * ROWB, 0x00020000);
+        const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp(h), 0, S * ROWB, 0x00020000);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(qt + (pseg + i) * 1024), 16, qoff[i] + q0 * ROWB, 0,
                                                  0, 0);
       } else {
-        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp, 0, orec, 0x00020000);
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp(h), 0, orec, 0x00020000);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (lptr_t)(dot + (pseg + i) * 1024), 16,
                                                  ooff[i] + (int)(q0 * dstride * 2), 0, 0, 0);
       }
     } else if (w == 0) {
       const int q = min(q0 + lane, S - 1);
-      __builtin_amdgcn_global_load_lds((gptr_t)(lsep + q), (lptr_t)(ld), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((gptr_t)(delp + q), (lptr_t)(ld + BQ * 4), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(lsep(h) + q), (lptr_t)(ld), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(delp(h) + q), (lptr_t)(ld + BQ * 4), 4, 0, 0);
     }
   };
-  auto glds = [&](int it, int buf) {
+  auto glds = [&](int hj, int it, int buf) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) glds_piece(it, buf, k);
+    for (int k = 0; k < 5; ++k) glds_piece(hj, it, buf, k);
   };
 
   u16x4 dsv[4];
-  int ds_q0 = -1;
+  int ds_q0 = -1, ds_h = h0;
   auto flush_ds_piece = [&](int gq) {
     if (ds_q0 < 0) return;
-    uint16_t* rowp = dstp + ((size_t)(ds_q0 / BQ) * (nkb * BN) + key) * BQ + 32 * m;
+    uint16_t* rowp = dstp(ds_h) + ((size_t)(ds_q0 / BQ) * (nkb * BN) + key) * BQ + 32 * m;
     *reinterpret_cast<u16x4*>(rowp + 8 * gq + 4 * hh) = dsv[gq];
   };
   auto flush_ds = [&]() {
@@ -537,7 +544,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   const uint32_t qrowb = (32 * m + r) * ROWB + 16 * (hh ^ swz);
   const uint32_t krowb = lds_addr(kimg) + (32 * kg + r) * ROWB + 16 * (hh ^ swz);
   if ((prio & 1) && m == 1) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (waves 4-7)
-  if (nqt > 0) glds(0, 0);
+  if (nit > 0) glds(0, 0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
   // PROF: per-wave cycle sums of the loop phases (s_memtime at phase boundaries; diagnostic
@@ -556,10 +563,12 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     t_beg = __builtin_amdgcn_s_memtime();
     rt_beg = __builtin_amdgcn_s_memrealtime();
   }
-  for (int it = 0; it < nqt; ++it) {
+  int hj = 0, it = 0;  // head / q tile of flattened iteration L
+  for (int L = 0; L < nit; ++L) {
     if constexpr (PROF) tp0 = __builtin_amdgcn_s_memtime();
     const int q0 = qstart + it * BQ;
-    const int buf = it & 1;
+    const int buf = L & 1;
+    const int nx_it = it + 1 < nqt ? it + 1 : 0, nx_hj = it + 1 < nqt ? hj : hj + 1;  // next iteration
     const char* qt = smem + 2 * KIMG + buf * BUF;
     const char* dot = qt + QT;
     const float* lse_s = reinterpret_cast<const float*>(dot + QT);
@@ -569,9 +578,9 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     // waves' vector-memory instructions queued behind each other and the low-priority half
     // stalled there ~2000 cycles per tile (phase profile, profiles/r2z_bwd8_phase_cycles.txt)
     const bool spread = (prio & 16) != 0;
-    const bool more = it + 1 < nqt;
+    const bool more = L + 1 < nit;
     if (!spread) {
-      if (it + 1 < nqt) glds(it + 1, buf ^ 1);
+      if (more) glds(nx_hj, nx_it, buf ^ 1);
       flush_ds();
     } else if (prio & 64) {
       flush_ds();
@@ -601,8 +610,8 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         for (int y = 0; y < 4; ++y) pin(x[y]);
         sa = mfma32b(x[0], x[1], sa);
         dp = mfma32b(x[2], x[3], dp);
-        if (spread && (st & 1) == 0 && more) glds_piece(it + 1, buf ^ 1, st >> 1);
-        if (spread && st == KS - 1 && more) glds_piece(it + 1, buf ^ 1, 4);
+        if (spread && (st & 1) == 0 && more) glds_piece(nx_hj, nx_it, buf ^ 1, st >> 1);
+        if (spread && st == KS - 1 && more) glds_piece(nx_hj, nx_it, buf ^ 1, 4);
       }
     }
     mark(1);
@@ -679,10 +688,13 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     for (int gq = 0; gq < 4; ++gq)
       dsv[gq] = u16x4{f2bf(dp[4 * gq]), f2bf(dp[4 * gq + 1]), f2bf(dp[4 * gq + 2]), f2bf(dp[4 * gq + 3])};
     ds_q0 = q0;
+    ds_h = h0 + hj;
     mark(3);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next tile landed
     __syncthreads();                     // ... and every wave's; this tile's buffers consumed
     mark(4);
+    it = nx_it;
+    hj = nx_hj;
   }
   if constexpr (PROF) {
     if (lane < 5) {
@@ -691,7 +703,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
       for (int k = 1; k < 5; ++k) v = lane == k ? ph[k] : v;
       prof[((size_t)blockIdx.x * 8 + w) * 16 + lane] = v;
     }
-    if (lane == 5) prof[((size_t)blockIdx.x * 8 + w) * 16 + 5] = (uint32_t)nqt;
+    if (lane == 5) prof[((size_t)blockIdx.x * 8 + w) * 16 + 5] = (uint32_t)nit;
     const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memtime() - t_beg);
     const uint32_t drt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - rt_beg);
     if (lane == 6) prof[((size_t)blockIdx.x * 8 + w) * 16 + 6] = dt;
@@ -720,8 +732,8 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         dk[db][j] += red[((db * 16) + j) * 64];
         dv[db][j] += red[((DB * 16) + db * 16 + j) * 64];
       }
-    float* dkq = dKp + ((size_t)(b * Hq + h) * Sk + key) * D;
-    float* dvq = dVp + ((size_t)(b * Hq + h) * Sk + key) * D;
+    float* dkq = dKp + ((size_t)bhp * Sk + key) * D;
+    float* dvq = dVp + ((size_t)bhp * Sk + key) * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -973,6 +985,34 @@ using namespace mx;
 // dq_mode 3 (split, default): work = B*Hq * ceil(Sk/128)*128 * ceil(S/64)*64 bf16 (dS^T,
 //   no zeroing); dq receives [B,Hq,S,D] from attn_bwd_dq_kernel.  Deterministic.
 // delta: workspace [B,Hq,S].
+// q-heads per workgroup of the 8-wave backward (split mode, D = 128): the largest of 4 / 2 / 1
+// that divides the GQA group and still leaves >= 2 workgroups per CU (512) for the causal
+// heavy-to-light balance; MXLLM_ATTN_BWD8_HPW forces a value.  1 on every other path.
+static bool attn_bwd8_on() {
+  static const bool on = [] {  // MXLLM_ATTN_BWD8=0: the one-wave-per-SIMD split kernel (A/B)
+    const char* e = getenv("MXLLM_ATTN_BWD8");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static int attn_bwd8_hpw(int B, int Hq, int Hkv, int S, int Sk, int D, int dq_mode) {
+  (void)S;
+  if (dq_mode != 3 || D != 128 || !attn_bwd8_on() || Hkv <= 0 || Hq % Hkv) return 1;
+  const char* fe = getenv("MXLLM_ATTN_BWD8_HPW");  // read per call (tests sweep it)
+  const int forced = fe && *fe ? atoi(fe) : 0;
+  const int G = Hq / Hkv, nkb = (Sk + 127) / 128;
+  if (forced > 0) return G % forced == 0 ? forced : 1;
+  for (int hpw = 4; hpw > 1; hpw >>= 1)
+    if (G % hpw == 0 && (int64_t)nkb * B * (Hq / hpw) >= 512) return hpw;
+  return 1;
+}
+
+// dK / dV partial heads mx_attn_bwd writes per batch row (dKp / dVp are [B, this, Sk, D] f32;
+// each KV head's partials are consecutive: sum them to get dK / dV)
+extern "C" int mx_attn_bwd_partial_heads(int B, int Hq, int Hkv, int S, int Sk, int D, int dq_mode) {
+  return Hq / attn_bwd8_hpw(B, Hq, Hkv, S, Sk, D, dq_mode);
+}
+
 extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
                            const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
                            int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, int dq_mode,
@@ -998,10 +1038,7 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     return (int)hipGetLastError();
   }
   float* dqk = dq_mode == 1 ? dq : reinterpret_cast<float*>(work);
-  static const bool bwd8 = [] {  // MXLLM_ATTN_BWD8=0: the one-wave-per-SIMD split kernel (A/B)
-    const char* e = getenv("MXLLM_ATTN_BWD8");
-    return !(e && e[0] == '0');
-  }();
+  const bool bwd8 = attn_bwd8_on();
   // MXLLM_ATTN_BWD8_PRIO (bit flags, default 17): 1 = s_setprio 1 for waves 4-7, 16 = spread the
   // DMA / dS-store issue over the MFMA steps; 2 = timing ablation (same q tile every step, wrong
   // results)
@@ -1013,24 +1050,26 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_PROF");
     return e && e[0] == '1';
   }();
+  const int hpw = attn_bwd8_hpw(B, Hq, Hkv, S, Sk, D, dq_mode);
+  const int grid8 = nkb * B * (Hq / hpw);
   if (dq_mode == 3 && D == 128 && bwd8 && bwd8_prof) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     uint32_t* pbuf = nullptr;
-    const size_t n = (size_t)grid * 128;
+    const size_t n = (size_t)grid8 * 128;
     if (hipMalloc(&pbuf, n * 4) != hipSuccess) return -1;
     (void)hipMemsetAsync(pbuf, 0, n * 4, stream);
     if (causal)
-      attn_bwd8_kernel<true, true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
-                                                             off, sl, scale, S_pad, bwd8_prio, pbuf);
+      attn_bwd8_kernel<true, true><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S,
+                                                              Sk, off, sl, scale, S_pad, bwd8_prio, hpw, pbuf);
     else
-      attn_bwd8_kernel<false, true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S,
-                                                              Sk, off, sl, scale, S_pad, bwd8_prio, pbuf);
+      attn_bwd8_kernel<false, true><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S,
+                                                               Sk, off, sl, scale, S_pad, bwd8_prio, hpw, pbuf);
     std::vector<uint32_t> h(n);
     (void)hipMemcpyAsync(h.data(), pbuf, n * 4, hipMemcpyDeviceToHost, stream);
     (void)hipStreamSynchronize(stream);
     (void)hipFree(pbuf);
     double sum[2][5] = {}, tiles[2] = {}, tt = 0, rt = 0, pro = 0, epi = 0;
-    for (size_t wv = 0; wv < (size_t)grid * 8; ++wv) {
+    for (size_t wv = 0; wv < (size_t)grid8 * 8; ++wv) {
       const int half = (int)(wv % 8) >> 2;
       for (int kk = 0; kk < 5; ++kk) sum[half][kk] += h[wv * 16 + kk];
       tiles[half] += h[wv * 16 + 5];
@@ -1039,7 +1078,7 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
       pro += h[wv * 16 + 8];
       epi += (double)h[wv * 16 + 9] - h[wv * 16 + 6];
     }
-    const double nwv = (double)grid * 8;
+    const double nwv = (double)grid8 * 8;
     fprintf(stderr, "[attn_bwd8 prof] s_memtime rate %.0f MHz; per wave: prologue %.0f, loop %.0f, epilogue %.0f cycles\n",
             rt > 0 ? 100.0 * tt / rt : 0.0, pro / nwv, tt / nwv, epi / nwv);
     for (int half = 0; half < 2; ++half)
@@ -1049,11 +1088,11 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   } else if (dq_mode == 3 && D == 128 && bwd8) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     if (causal)
-      attn_bwd8_kernel<true><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk, off,
-                                                       sl, scale, S_pad, bwd8_prio);
+      attn_bwd8_kernel<true><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
+                                                        off, sl, scale, S_pad, bwd8_prio, hpw);
     else
-      attn_bwd8_kernel<false><<<grid, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
-                                                        off, sl, scale, S_pad, bwd8_prio);
+      attn_bwd8_kernel<false><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
+                                                         off, sl, scale, S_pad, bwd8_prio, hpw);
   } else {
 #define BWD(DD, C)                                                                                                  \
   do {                                                                                                              \

@@ -202,8 +202,8 @@ class _RingAttnFn(torch.autograd.Function):
         kv = torch.stack([k, v])
         dkv = torch.zeros(2, B, Hkv, S, D, dtype=torch.float32, device=q.device)  # travels with kv
 
-        def gsum(t):  # per-q-head partials -> per-kv-head sums
-            return t.view(B, Hkv, rep, t.shape[2], D).sum(2)
+        def gsum(t):  # dK / dV partials (per q-head, or per group of q-heads) -> per-kv-head sums
+            return t.view(B, Hkv, -1, t.shape[2], D).sum(2)
 
         cur, dcur = kv, dkv
         for step in range(P):
@@ -235,9 +235,8 @@ class _RingAttnFn(torch.autograd.Function):
                 _Ring.wait(dworks)
         dk, dv = dcur[0], dcur[1]  # this rank's own block, complete
         if use_native(q):
-            dkp = (dk / rep).repeat_interleave(rep, 1).contiguous()  # rope_merge sums the GQA group back
-            dvp = (dv / rep).repeat_interleave(rep, 1).contiguous()
-            dqkv = native().rope_merge_bwd(dq, dkp, dvp, cos_l, sin_l, B, S, Hq, Hkv, D, 0)
+            # already one sum per KV head: the merge takes them as Hkv "partials"
+            dqkv = native().rope_merge_bwd(dq, dk.contiguous(), dv.contiguous(), cos_l, sin_l, B, S, Hq, Hkv, D, 0)
         else:
             dqr = ref.apply_rope(dq.transpose(1, 2), cos_l, -sin_l)
             dkr = ref.apply_rope(dk.transpose(1, 2), cos_l, -sin_l)

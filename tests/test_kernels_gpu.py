@@ -184,8 +184,8 @@ def test_attention_fwd_bwd(gpu, B, Hq, Hkv, S, Sk, D, causal):
     orf.backward(do.float())
     dq, dkp, dvp = _ops().attn_bwd(do.view(B, S, Hq * D), q, k, v, o, lse, causal, scale)
     rep = Hq // Hkv
-    dk = dkp.view(B, Hkv, rep, Sk, D).sum(2)
-    dv = dvp.view(B, Hkv, rep, Sk, D).sum(2)
+    dk = dkp.view(B, Hkv, -1, Sk, D).sum(2)  # partials: per q-head or per q-head group
+    dv = dvp.view(B, Hkv, -1, Sk, D).sum(2)
     assert rel_err(dq, qf.grad) < 3e-2
     assert rel_err(dk, kf.grad) < 3e-2
     assert rel_err(dv, vf.grad) < 3e-2
@@ -247,9 +247,11 @@ def test_attention_bwd_deterministic(gpu, causal, S):
         torch.testing.assert_close(r1[0], ra[0], rtol=1e-3, atol=1e-3)
         if mode == 2:  # same key-block kernel: dK / dV summed in the same order
             assert torch.equal(r1[1], ra[1]) and torch.equal(r1[2], ra[2])
-        else:  # D=128 split mode: the 8-wave kernel sums its two q halves at the end
-            torch.testing.assert_close(r1[1], ra[1], rtol=1e-4, atol=1e-5)
-            torch.testing.assert_close(r1[2], ra[2], rtol=1e-4, atol=1e-5)
+        else:  # D=128 split mode: the 8-wave kernel sums its q halves (and q-heads) in its own order
+            def g(t):
+                return t.view(B, Hkv, -1, S, D).sum(2)
+            torch.testing.assert_close(g(r1[1]), g(ra[1]), rtol=1e-4, atol=1e-4)
+            torch.testing.assert_close(g(r1[2]), g(ra[2]), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("mode", [3, 1])
@@ -268,8 +270,8 @@ def test_attention_training_shape_vs_fp32(gpu, mode):
     do = torch.randn(B, S, Hq, D, device=gpu, dtype=torch.bfloat16)
     dq, dkp, dvp = _ops().attn_bwd(do.view(B, S, Hq * D), q, k, v, o, lse, True, sc, mode)
     rep = Hq // Hkv
-    dk = dkp.view(B, Hkv, rep, S, D).sum(2)
-    dv = dvp.view(B, Hkv, rep, S, D).sum(2)
+    dk = dkp.view(B, Hkv, -1, S, D).sum(2)
+    dv = dvp.view(B, Hkv, -1, S, D).sum(2)
     qf, kf, vf = [t.float().requires_grad_(True) for t in (q, k, v)]
     orf = ref.attention(qf.transpose(1, 2), kf.transpose(1, 2), vf.transpose(1, 2), causal=True)
     assert rel_err(o.view(B, S, Hq, D), orf) < 2e-2
@@ -277,6 +279,32 @@ def test_attention_training_shape_vs_fp32(gpu, mode):
     assert rel_err(dq, qf.grad) < 3e-2
     assert rel_err(dk, kf.grad) < 3e-2
     assert rel_err(dv, vf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("hpw", [2, 4, 8])
+def test_attention_bwd_heads_per_workgroup(gpu, hpw, monkeypatch):
+    """The 8-wave backward with `hpw` q-heads of one KV group per workgroup (dK / dV summed over
+    them in registers): [B, Hq / hpw, Sk, D] partials whose per-KV-head sums equal the one-head-
+    per-workgroup result, and the same dQ (it does not depend on the grouping)."""
+    torch.manual_seed(9)
+    B, Hq, Hkv, S, D = 1, 16, 2, 640, 128
+    q = torch.randn(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    sc = 1.0 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, True, sc)
+    do = torch.randn(B, S, Hq * D, device=gpu, dtype=torch.bfloat16)
+    monkeypatch.setenv("MXLLM_ATTN_BWD8_HPW", "1")
+    dq1, dk1, dv1 = _ops().attn_bwd(do, q, k, v, o, lse, True, sc, 3)
+    monkeypatch.setenv("MXLLM_ATTN_BWD8_HPW", str(hpw))
+    dq, dkp, dvp = _ops().attn_bwd(do, q, k, v, o, lse, True, sc, 3)
+    assert dkp.shape == (B, Hq // hpw, S, D) and dk1.shape == (B, Hq, S, D)
+    assert torch.equal(dq, dq1)
+
+    def g(t):
+        return t.view(B, Hkv, -1, S, D).sum(2)
+    torch.testing.assert_close(g(dkp), g(dk1), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(g(dvp), g(dv1), rtol=1e-4, atol=1e-4)
 
 
 def test_attention_block_autograd(gpu):
