@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--act-ckpt", action="store_true", help="activation checkpointing per layer")
+    ap.add_argument("--act-ckpt-layers", type=int, default=None,
+                    help="with --act-ckpt: checkpoint only the first N layers (the rest keep activations)")
     ap.add_argument("--sp", type=int, default=1,
                     help="sequence-parallel degree (Ulysses all-to-all around attention; long-context runs)")
     ap.add_argument("--cp", type=int, default=1,
@@ -80,6 +82,11 @@ def parse(argv=None):
                     help="also measure BASELINE config 4 (70B full fine-tune, ZeRO-3) after the headline; "
                          "auto = when the headline runs on 8 GPUs")
     ap.add_argument("--config4-micro-batch", type=int, default=4)
+    # selective checkpointing: the last 24 of 80 layers keep their activations.  Emulated world-8
+    # step (profiles/r2s3_emul8_ck*.json): all 80 checkpointed 3,559 ms / 191 GB peak; first 56
+    # 3,321 ms / 239 GB; first 48 3,247 ms / 255 GB.  56 leaves ~65 GB for RCCL buffers and the
+    # in-flight gather / reduce-scatter units of the real 8-rank job.
+    ap.add_argument("--config4-act-ckpt-layers", type=int, default=56)
     ap.add_argument("--config4-model", default="llama3.1-70b", help=argparse.SUPPRESS)  # tests: tiny models
     ap.add_argument("--config4-steps", type=int, default=3)
     ap.add_argument("--config4-warmup", type=int, default=2)
@@ -198,6 +205,7 @@ def run_config4(a, world: int) -> dict:
     os.close(fd)
     argv = ["--gpus", str(world), "--model", a.config4_model, "--finetune", "full", "--parallel", "zero3",
             "--act-ckpt", "--micro-batch", str(a.config4_micro_batch), "--seq-len", str(a.seq_len),
+            "--act-ckpt-layers", str(a.config4_act_ckpt_layers),
             "--steps", str(a.config4_steps), "--warmup", str(a.config4_warmup), "--config4", "off",
             "--json-out", path] + (["--device", a.device] if a.device else [])
     keep = {k: v for k, v in os.environ.items()
@@ -248,6 +256,7 @@ def run(a, env) -> dict:
     t0 = time.perf_counter()
     opt = OptimConfig(lr=1e-4, weight_decay=0.0, grad_clip=1.0)
     emulated = 0
+    ckpt = a.act_ckpt if (not a.act_ckpt or a.act_ckpt_layers is None) else a.act_ckpt_layers
     if a.parallel == "zero3":
         if a.finetune != "full":
             raise SystemExit("--parallel zero3 requires --finetune full")
@@ -257,12 +266,12 @@ def run(a, env) -> dict:
             if env.world_size > 1:
                 raise SystemExit("--emulate-world is a single-process proxy")
             emulated = a.emulate_world
-        trainer = Zero3Trainer(cfg, env, opt, seed=1234, activation_checkpointing=a.act_ckpt,
+        trainer = Zero3Trainer(cfg, env, opt, seed=1234, activation_checkpointing=ckpt,
                                emulate_world=emulated)
         model = trainer.model
     else:
         model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
-                      activation_checkpointing=a.act_ckpt)
+                      activation_checkpointing=ckpt)
         trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb, shard_optimizer=a.parallel == "zero1")
     sp_group, data_rank, shard_fn = None, env.rank, None
     if a.sp > 1 and a.cp > 1:
@@ -356,7 +365,8 @@ def run(a, env) -> dict:
                          if a.finetune == "lora" else "full (bf16 params+grads, fp32 master/Adam)"),
             "micro_batch": a.micro_batch,
             "grad_accum": a.grad_accum,
-            "activation_checkpointing": a.act_ckpt,
+            "activation_checkpointing": (a.act_ckpt if a.act_ckpt_layers is None or not a.act_ckpt
+                                         else f"first {a.act_ckpt_layers} of {cfg.n_layers} layers"),
             "optimizer": "fused AdamW (HIP), grad clip 1.0",
             "gemm": "hipBLASLt/rocBLAS" + (" (tuned solution table)" if tuned else ""),
         },

@@ -67,6 +67,7 @@ class RunConfig:
     grad_accum: int = 1
     bucket_mb: float = 128.0
     activation_checkpointing: bool = False
+    ckpt_layers: int = -1  # with activation_checkpointing: -1 = every layer, N = only the first N (selective)
     ckpt_dir: str = ""
     save_every: int = 0
     save_hf: str = ""  # at the end: write the model as a Hugging Face Llama directory (LoRA merged)

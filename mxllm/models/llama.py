@@ -170,9 +170,19 @@ class LlamaLayer(nn.Module):
         self.wd = FusedLinear(cfg.ffn, [h], dx_image="d" in DX_IMAGE, transposed="d" in LORA_T, **kw)
 
 
+def ckpt_layer(setting: bool | int | None, i: int) -> bool:
+    """Whether layer ``i`` is activation-checkpointed: ``True`` = every layer, an int
+    ``n`` = the first ``n`` layers (selective checkpointing: the rest keep their
+    activations, trading HBM for the recompute), ``False``/``0``/``None`` = none."""
+    if isinstance(setting, bool) or setting is None:
+        return bool(setting)
+    return i < int(setting)
+
+
 class Llama(nn.Module):
     def __init__(self, cfg: LlamaConfig, *, device=None, dtype=torch.bfloat16, lora_r: int = 0,
-                 lora_alpha: float = 16.0, seed: int = 0, init: bool = True, activation_checkpointing: bool = False):
+                 lora_alpha: float = 16.0, seed: int = 0, init: bool = True,
+                 activation_checkpointing: bool | int = False):
         super().__init__()
         device = torch.device(device) if device is not None else torch.device("cpu")
         self.cfg = cfg
@@ -272,7 +282,7 @@ class Llama(nn.Module):
         for i in range(len(self.layers)):
             if wait is not None:
                 wait(groups[i + 1])
-            if self.activation_checkpointing and self.training and torch.is_grad_enabled():
+            if ckpt_layer(self.activation_checkpointing, i) and self.training and torch.is_grad_enabled():
                 x, h = ckpt.checkpoint(self._layer, i, x, h, B, S, use_reentrant=False)
             else:
                 x, h = self._layer(i, x, h, B, S)

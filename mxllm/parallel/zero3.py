@@ -328,7 +328,7 @@ class _CkptLayer(torch.autograd.Function):
 class Zero3Trainer:
     """Same ``train_step`` contract as :class:`mxllm.train.trainer.Trainer`."""
 
-    def __init__(self, cfg, env: DistEnv, optim=None, *, seed: int = 0, activation_checkpointing: bool = False,
+    def __init__(self, cfg, env: DistEnv, optim=None, *, seed: int = 0, activation_checkpointing: bool | int = False,
                  process_group=None, emulate_world: int = 0, max_inflight: int | None = None,
                  init_from: str | None = None):
         from ..models.llama import Llama
@@ -512,6 +512,8 @@ class Zero3Trainer:
 
     # ---------------------------------------------------------------- step
     def _forward(self, ids, labels):
+        from ..models.llama import ckpt_layer
+
         m = self.model
         cfg = m.cfg
         B, S = ids.shape
@@ -530,7 +532,7 @@ class Zero3Trainer:
                 u = self._units_by_layer[i]
                 nxt = self._units_by_layer.get(i + 1, self._head)
                 self._use(u, nxt)
-                if self.act_ckpt:
+                if ckpt_layer(self.act_ckpt, i):
                     x, h = _CkptLayer.apply(self, i, x, h)
                 else:
                     x, h = m._layer(i, x, h, B, S)

@@ -49,6 +49,13 @@ def cleanup():
     runtime.cleanup()
 
 
+def _ckpt_setting(run):
+    """bool (every layer / none) or the number of leading layers checkpointed."""
+    if run.activation_checkpointing and run.ckpt_layers >= 0:
+        return int(run.ckpt_layers)
+    return bool(run.activation_checkpointing)
+
+
 def build_trainer(run, env):
     """``run.model``: a preset (random init) or a Hugging Face Llama directory (its
     weights; ZeRO-3 reads them unit by unit, so no rank holds the whole model)."""
@@ -62,10 +69,10 @@ def build_trainer(run, env):
     if run.parallel == "zero3":
         from mxllm.parallel.zero3 import Zero3Trainer
 
-        return Zero3Trainer(cfg, env, opt, seed=run.seed, activation_checkpointing=run.activation_checkpointing,
+        return Zero3Trainer(cfg, env, opt, seed=run.seed, activation_checkpointing=_ckpt_setting(run),
                             init_from=run.model if is_hf_dir(run.model) else None)
     model = build_model(run.model, device=env.device, lora_r=lora_r, lora_alpha=run.lora_alpha, seed=run.seed,
-                        activation_checkpointing=run.activation_checkpointing)
+                        activation_checkpointing=_ckpt_setting(run))
     return Trainer(model, env, opt, bucket_mb=run.bucket_mb, shard_optimizer=run.parallel == "zero1")
 
 
