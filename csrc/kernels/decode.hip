@@ -388,40 +388,85 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
-// logits [B, V] (bf16 or f32); temperature <= 0 -> greedy.  out ids [B] int64
+// logits [B, V] (bf16 or f32); temperature <= 0 -> greedy.  out ids [B] int64.
+//
+// Split over the vocabulary: grid (nchunks, B), each workgroup reduces `chunk`
+// logits of one row to (max, smallest index), the last workgroup of the row to
+// arrive (agent-scope counter, no spinning) combines the partials in chunk
+// order.  One workgroup per row left a batch-1 decode step with ONE CU
+// streaming 256 KB of logits: 176 us of a 4.1 ms 8B step; split over ~63
+// workgroups it is a few microseconds.  The result (and the Gumbel noise of
+// each (seed, row, step, index)) is the same as a single-pass argmax.
+constexpr int kSampMaxRows = 1024;   // rows per launch (more rows: several launches)
+constexpr int kSampMaxChunks = 64;   // partials per row (= one wave in the final pass)
+__device__ float g_samp_val[kSampMaxRows * kSampMaxChunks];
+__device__ int g_samp_idx[kSampMaxRows * kSampMaxChunks];
+__device__ unsigned int g_samp_cnt[kSampMaxRows];  // zero at load, reset by the last arriver
+
+__device__ __forceinline__ void samp_pick(float& best, int& bi, float ov, int oi) {
+  if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logits, int64_t* __restrict__ out, int V,
-                                                     float inv_temp, uint32_t seed, uint32_t step) {
+                                                     int chunk, float inv_temp, uint32_t seed, uint32_t step,
+                                                     int row0) {
   __shared__ float sv[4];
   __shared__ int si[4];
-  const int64_t row = blockIdx.x;
+  __shared__ int s_last;
+  const int lrow = blockIdx.y, nch = gridDim.x;
+  const int64_t row = (int64_t)row0 + lrow;
   const T* x = logits + row * V;
+  const int c0 = blockIdx.x * chunk, c1 = min(V, c0 + chunk);
   float best = -INFINITY;
-  int bi = 0;
-  for (int c = threadIdx.x; c < V; c += 256) {
-    float v;
-    if constexpr (sizeof(T) == 2) v = bf2f(reinterpret_cast<const uint16_t*>(x)[c]);
-    else v = reinterpret_cast<const float*>(x)[c];
-    if (inv_temp > 0.f) {
-      const uint32_t h = hash3(seed + (uint32_t)row * 7919u, step, (uint32_t)c);
-      const float u = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
-      v = v * inv_temp - __logf(-__logf(u));  // Gumbel-max
+  int bi = c0 < V ? c0 : 0;
+  for (int cb = c0 + (int)threadIdx.x; cb < c1; cb += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // 8 independent loads in flight per thread
+      const int c = cb + 256 * u;
+      if constexpr (sizeof(T) == 2) v[u] = c < c1 ? bf2f(reinterpret_cast<const uint16_t*>(x)[c]) : -INFINITY;
+      else v[u] = c < c1 ? reinterpret_cast<const float*>(x)[c] : -INFINITY;
     }
-    if (v > best) { best = v; bi = c; }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = cb + 256 * u;
+      if (c >= c1) break;
+      float w = v[u];
+      if (inv_temp > 0.f) {
+        const uint32_t h = hash3(seed + (uint32_t)row * 7919u, step, (uint32_t)c);
+        const float uu = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+        w = w * inv_temp - __logf(-__logf(uu));  // Gumbel-max
+      }
+      if (w > best) { best = w; bi = c; }
+    }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-  }
+  for (int o = 32; o > 0; o >>= 1) samp_pick(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
   if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = best; si[threadIdx.x >> 6] = bi; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w)
-      if (sv[w] > best || (sv[w] == best && si[w] < bi)) { best = sv[w]; bi = si[w]; }
-    out[row] = bi;
+    for (int w = 1; w < 4; ++w) samp_pick(best, bi, sv[w], si[w]);
+    g_samp_val[lrow * kSampMaxChunks + blockIdx.x] = best;
+    g_samp_idx[lrow * kSampMaxChunks + blockIdx.x] = bi;
+    __threadfence();
+    const unsigned prev = atomicAdd(&g_samp_cnt[lrow], 1u);
+    s_last = prev == (unsigned)(nch - 1);
+    if (s_last) g_samp_cnt[lrow] = 0u;
   }
+  __syncthreads();
+  if (!s_last || threadIdx.x >= 64) return;
+  __threadfence();  // acquire: the other workgroups' partials
+  const int l = threadIdx.x;
+  best = -INFINITY;
+  bi = 0x7fffffff;
+  if (l < nch) {
+    best = g_samp_val[lrow * kSampMaxChunks + l];
+    bi = g_samp_idx[lrow * kSampMaxChunks + l];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) samp_pick(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
+  if (l == 0) out[row] = bi == 0x7fffffff ? 0 : bi;
 }
 
 }  // namespace mx
@@ -465,10 +510,19 @@ extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint1
 extern "C" int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
                          uint32_t seed, uint32_t step, hipStream_t stream) {
   if (B <= 0) return 0;
+  if (V <= 0) return -1;
   const float it = temperature > 0.f ? 1.f / temperature : 0.f;
-  if (is_bf16)
-    sample_kernel<uint16_t><<<B, 256, 0, stream>>>((const uint16_t*)logits, out, V, it, seed, step);
-  else
-    sample_kernel<float><<<B, 256, 0, stream>>>((const float*)logits, out, V, it, seed, step);
+  int chunk = 2048, nch = (V + chunk - 1) / chunk;
+  if (nch > kSampMaxChunks) {
+    chunk = ((V + kSampMaxChunks - 1) / kSampMaxChunks + 255) / 256 * 256;
+    nch = (V + chunk - 1) / chunk;
+  }
+  for (int r0 = 0; r0 < B; r0 += kSampMaxRows) {
+    const dim3 grid(nch, std::min(kSampMaxRows, B - r0));
+    if (is_bf16)
+      sample_kernel<uint16_t><<<grid, 256, 0, stream>>>((const uint16_t*)logits, out, V, chunk, it, seed, step, r0);
+    else
+      sample_kernel<float><<<grid, 256, 0, stream>>>((const float*)logits, out, V, chunk, it, seed, step, r0);
+  }
   return (int)hipGetLastError();
 }

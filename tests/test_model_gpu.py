@@ -91,6 +91,12 @@ def test_sampler(gpu):
 
     logits = torch.randn(5, 128256, device=gpu)
     assert torch.equal(native().sample(logits, 0.0, 0, 0), logits.argmax(-1))
+    # split-vocabulary kernel: odd vocabularies (partial chunks, > 64 chunks), bf16 ties -> smallest index
+    for V in (7, 1000, 70001, 200003):
+        x = torch.randn(3, V, device=gpu).to(torch.bfloat16)
+        x[1, V // 3] = x[1, (2 * V) // 3] = 9.0  # tie across chunks
+        assert torch.equal(native().sample(x, 0.0, 0, 0), x.float().argmax(-1)), V
+        assert int(native().sample(x, 0.0, 0, 0)[1]) == V // 3
     # temperature sampling follows the softmax distribution (chi-square-ish sanity)
     small = torch.tensor([[0.0, 1.0, 2.0, -1.0]], device=gpu).repeat(4000, 1).contiguous()
     draws = native().sample(small, 1.0, 123, 0).cpu()
