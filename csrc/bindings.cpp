@@ -509,6 +509,21 @@ at::Tensor skinny_linear(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+// y[M, F] = swiglu(x[M, K] . w[2F, K]^T) for M <= 32 tokens, w = [gate; up] rows: the decode
+// MLP's first projection with SwiGLU in the GEMM epilogue (csrc/kernels/skinny_gemm.hip).
+at::Tensor skinny_linear_swiglu(const at::Tensor& x, const at::Tensor& w) {
+  MX_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "x: bf16 [M, K] rows");
+  MX_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1, "w: bf16 [2F, K] rows");
+  const int64_t M = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  MX_CHECK(w.size(1) == K && w.size(0) == 2 * F && M >= 1 && M <= 32 && F % 8 == 0 && K % 512 == 0 &&
+               x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "skinny_linear_swiglu shape contract");
+  DevGuard g(x.device());
+  auto y = at::empty({M, F}, x.options());
+  MX_OK(mx_skinny_gemm_swiglu(bf(x), x.stride(0), bf(w), w.stride(0), bfm(y), F, (int)M, (int)F, (int)K,
+                              cur_stream()));
+  return y;
+}
+
 // ---------------------------------------------------------------- fp8 weights (serving)
 // y[M, N] = x[M, K] . (scale[:, None] * q[N, K])^T ; q: e4m3 codes (uint8), scale f32 [N].
 // M <= 32: the fused weight-streaming kernel; otherwise dequantise to bf16 and run the
@@ -634,6 +649,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("sample_rows(Tensor logits, Tensor temps, Tensor top_p, Tensor top_k, Tensor seeds, Tensor steps) -> Tensor");
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
+  m.def("skinny_linear_swiglu(Tensor x, Tensor w) -> Tensor");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
   m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha) -> ()");
@@ -666,6 +682,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("sample_rows", &sample_rows);
   m.impl("w8_linear", &w8_linear);
   m.impl("skinny_linear", &skinny_linear);
+  m.impl("skinny_linear_swiglu", &skinny_linear_swiglu);
   m.impl("w8_dequant", &w8_dequant);
   m.impl("quant_rows_e4m3", &quant_rows_e4m3);
   m.impl("lora_xwt", &lora_xwt);

@@ -72,6 +72,8 @@ extern "C" {
 // fp8_gemm.hip
 int mx_skinny_gemm(const uint16_t* x, int64_t ldx, const uint16_t* w, int64_t ldw, uint16_t* y, int64_t ldy,
                    int M, int N, int K, hipStream_t stream);
+int mx_skinny_gemm_swiglu(const uint16_t* x, int64_t ldx, const uint16_t* w, int64_t ldw, uint16_t* y,
+                          int64_t ldy, int M, int F, int K, hipStream_t stream);
 int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, const float* scale, uint16_t* y, int64_t ldy,
                   int M, int N, int K, hipStream_t stream);
 int mx_w8_dequant(const uint8_t* q, const float* scale, uint16_t* w, int64_t N, int K, hipStream_t stream);

@@ -12,6 +12,11 @@
 //    and the X fragments use the same k permutation;
 //  * 8 chunks' loads are issued before the first is used: 256 B of weights per lane in
 //    flight, 128 KB per workgroup.
+//  * SWO (SwiGLU output, the decode MLP's gate|up projection, W = [gate; up] [2F, K]): a
+//    workgroup's 16 channels are 8 gate rows n..n+7 and the matching 8 up rows F+n..F+n+7, so
+//    the epilogue holds both halves of its 8 outputs and writes silu(g) * u [M, F] directly
+//    (g, u rounded to bf16 first, as the separate GEMM + SwiGLU kernels round them: same bits).
+//    Same weight stream as the plain kernel; one launch and the [M, 2F] round trip less.
 #include <cstdlib>
 
 #include "common.h"
@@ -28,10 +33,14 @@ __device__ __forceinline__ f32x4 mfma16_sk(const u16x8& a, const u16x8& b, const
 // MB: 16-token blocks (1 or 2); X rows >= M are clamped to M-1 and discarded.
 // NC: 16-channel groups per workgroup: each X fragment then feeds NC MFMAs, so X traffic per
 // streamed weight byte drops NC-fold (it equals the weight traffic at 16 tokens with NC = 1).
-template <int MB, int NC>
+__device__ __forceinline__ float silu_sk(float x) { return x / (1.f + __expf(-x)); }
+
+template <int MB, int NC, bool SWO = false>
 __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx,
                                                           const uint16_t* __restrict__ W, int64_t ldw,
-                                                          uint16_t* __restrict__ Y, int64_t ldy, int M, int K) {
+                                                          uint16_t* __restrict__ Y, int64_t ldy, int M, int K,
+                                                          int F = 0) {
+  static_assert(!SWO || NC == 1, "SwiGLU epilogue: one channel group");
   constexpr int NW = 8, UNR = NC == 1 ? 8 : 4;
   __shared__ f32x4 red[NW][NC][MB][64];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -41,7 +50,11 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
   const int kq = K / NW;  // this wave's K part
   const uint16_t* wrow[NC];
 #pragma unroll
-  for (int j = 0; j < NC; ++j) wrow[j] = W + (int64_t)(n0 + 16 * j + c) * ldw + (int64_t)w * kq + 16 * g;
+  for (int j = 0; j < NC; ++j) {
+    // SWO: channel c < 8 -> gate row blockIdx.x * 8 + c, c >= 8 -> the matching up row
+    const int64_t wr = SWO ? (int64_t)blockIdx.x * 8 + (c & 7) + (c >= 8 ? F : 0) : (int64_t)(n0 + 16 * j + c);
+    wrow[j] = W + wr * ldw + (int64_t)w * kq + 16 * g;
+  }
   const uint16_t* xr[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) xr[mb] = X + (int64_t)min(mb * 16 + c, M - 1) * ldx + (int64_t)w * kq + 16 * g;
@@ -101,7 +114,19 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
 #pragma unroll
         for (int ww = 1; ww < NW; ++ww) s += red[ww][j][mb][lane];
         const int m = mb * 16 + c;
-        if (m < M) {
+        if constexpr (SWO) {
+          // lane (c, g) holds channels 4g..4g+3: gate outputs for g < 2, the up outputs of the
+          // same columns in lane (c, g + 2) = lane ^ 32
+          f32x4 up;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32, 64);
+          if (g < 2 && m < M) {
+            u16x4 o;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = f2bf(silu_sk(bf2f(f2bf(s[i]))) * bf2f(f2bf(up[i])));
+            *reinterpret_cast<u16x4*>(Y + (int64_t)m * ldy + (int64_t)blockIdx.x * 8 + 4 * g) = o;
+          }
+        } else if (m < M) {
           u16x4 o;
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = f2bf(s[i]);
@@ -137,5 +162,19 @@ extern "C" int mx_skinny_gemm(const uint16_t* x, int64_t ldx, const uint16_t* w,
     if (nc >= 4) SKG(2, 4); else if (nc == 2) SKG(2, 2); else SKG(2, 1);
   }
 #undef SKG
+  return (int)hipGetLastError();
+}
+
+// y[M, F] = silu(g) * u with [g | u] = x[M, K] . W[2F, K]^T, W = [gate; up] rows: the decode
+// MLP's gate|up projection with the SwiGLU in its epilogue.  Same contract as mx_skinny_gemm
+// with N = 2F, plus F % 8 == 0.
+extern "C" int mx_skinny_gemm_swiglu(const uint16_t* x, int64_t ldx, const uint16_t* w, int64_t ldw, uint16_t* y,
+                                     int64_t ldy, int M, int F, int K, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 32 || F % 8 || K % 512 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K || ldy < F) return -1;
+  if (M <= 16)
+    skinny_gemm_kernel<1, 1, true><<<F / 8, 512, 0, stream>>>(x, ldx, w, ldw, y, ldy, M, K, F);
+  else
+    skinny_gemm_kernel<2, 1, true><<<F / 8, 512, 0, stream>>>(x, ldx, w, ldw, y, ldy, M, K, F);
   return (int)hipGetLastError();
 }

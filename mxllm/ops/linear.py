@@ -332,6 +332,20 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return F.linear(x, w)
 
 
+def linear_swiglu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
+    """Inference: ``swiglu(linear(x, w))`` for decode-sized row counts as ONE launch, with
+    ``w = [gate; up]`` [2F, K] (csrc/kernels/skinny_gemm.hip SWO variant: the SwiGLU in
+    the GEMM epilogue, bit-identical to the GEMM + SwiGLU kernels).  None when the fused
+    kernel does not take the call (the caller then runs the two ops)."""
+    if SKINNY_M <= 0 or x.dim() != 2 or (w.requires_grad and torch.is_grad_enabled()):
+        return None
+    if x.shape[1] != w.shape[1] or w.shape[0] % 16 or not 0 < x.shape[0] <= SKINNY_M:
+        return None
+    if not _skinny_ok(x, w):
+        return None
+    return native().skinny_linear_swiglu(x, w)
+
+
 def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, b: torch.Tensor, splits: Sequence[int],
                 scaling: float) -> torch.Tensor:
     """y = x W^T + scaling * (x A^T) Bbd^T with block-diagonal Bbd (see module doc)."""

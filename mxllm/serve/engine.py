@@ -36,8 +36,10 @@ from dataclasses import dataclass, field
 import torch
 
 from .. import ops
+from ..models.llama import FusedLinear
 from ..ops import decode as dops
 
+_SWIGLU_FUSED = os.environ.get("MXLLM_SWIGLU_FUSED", "1") != "0"  # A/B switch (bench/serve_bench.py)
 log = logging.getLogger("mxllm.engine")
 
 
@@ -145,7 +147,12 @@ class Engine:
             if self.tp is not None:  # row-parallel Wo: sum the heads' partial outputs
                 self.tp.all_reduce_(a)
             xn, h = ops.add_rms_norm(a, h, layer.mlp_norm, c.norm_eps)
-            d = layer.wd(ops.swiglu(layer.wgu(xn)))
+            mid = None
+            if _SWIGLU_FUSED and type(layer.wgu) is FusedLinear and layer.wgu.lora_r == 0 and xn.dim() == 2:
+                mid = ops.linear_swiglu(xn, layer.wgu.weight)  # decode rows: SwiGLU in the GEMM epilogue
+            if mid is None:
+                mid = ops.swiglu(layer.wgu(xn))
+            d = layer.wd(mid)
             if self.tp is not None:  # row-parallel Wdown
                 self.tp.all_reduce_(d)
             nxt = m.layers[i + 1].attn_norm if i + 1 < len(m.layers) else m.final_norm

@@ -504,3 +504,27 @@ def test_skinny_linear_vs_fp32(gpu, M, N, K):
     y = _ops().skinny_linear(x, w)
     ref = x.float() @ w.float().t()
     assert y.shape == (M, N) and rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,F,K", [(1, 14336, 4096), (5, 520, 512), (8, 1024, 1536), (17, 256, 1024),
+                                   (32, 512, 2048)])
+def test_skinny_linear_swiglu(gpu, M, F, K):
+    """Decode gate|up projection with SwiGLU in the epilogue: bit-identical to the decode
+    GEMM + SwiGLU kernel, and close to fp32 silu(x Wg^T) * (x Wu^T).  x is row-strided."""
+    import sys
+
+    from mxllm import ops
+
+    torch.manual_seed(M * 7 + K)
+    xb = torch.randn(M, K + 64, device=gpu, dtype=torch.bfloat16)
+    x = xb[:, :K]
+    w = torch.randn(2 * F, K, device=gpu, dtype=torch.bfloat16) * 0.05
+    y = _ops().skinny_linear_swiglu(x, w)
+    two = ops.swiglu(_ops().skinny_linear(x, w))
+    assert y.shape == (M, F) and torch.equal(y, two)
+    gu = x.float() @ w.float().t()
+    ref = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    assert rel_err(y, ref) < 1e-2
+    if M <= sys.modules["mxllm.ops.linear"].SKINNY_M:  # the routed entry point takes it
+        assert torch.equal(ops.linear_swiglu(x, w), y)
