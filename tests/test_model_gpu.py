@@ -66,6 +66,9 @@ def test_decode_kernels(gpu, D, Hq, Hkv):
     kc_ref, vc_ref = kc.clone(), vc.clone()
     q = native().rope_append(qkv, cos, sin, pos, slots, kc, vc, Hq, Hkv, D)
     out = native().decode_attn(q, kc, vc, pos, slots, max(lens) + 1, 1.0 / math.sqrt(D), 1)
+    # the split merge runs in the attention kernel (last-arriving split): its arrival counters
+    # must be back at zero for the next call -> identical output
+    assert torch.equal(native().decode_attn(q, kc, vc, pos, slots, max(lens) + 1, 1.0 / math.sqrt(D), 1), out)
     x = qkv.float().view(B, Hq + 2 * Hkv, D)
     for i in range(B):
         p, s = lens[i], int(slots[i])
