@@ -469,6 +469,27 @@ at::Tensor sample(const at::Tensor& logits, double temperature, int64_t seed, in
   return out;
 }
 
+// per-row temperature / seed / step without top-k / top-p (the split-vocabulary kernel of
+// decode.hip; same draws as sample_rows for such rows)
+at::Tensor sample_temp_rows(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor& seeds,
+                            const at::Tensor& steps) {
+  MX_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "logits [B, V] contiguous GPU");
+  MX_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16/f32");
+  const int64_t B = logits.size(0);
+  auto chk = [&](const at::Tensor& t, at::ScalarType st, const char* name) {
+    MX_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == st && t.numel() == B, name);
+  };
+  chk(temps, at::kFloat, "temps f32 [B]");
+  chk(seeds, at::kLong, "seeds i64 [B]");
+  chk(steps, at::kInt, "steps i32 [B]");
+  DevGuard g(logits.device());
+  auto out = at::empty({B}, logits.options().dtype(at::kLong));
+  MX_OK(mx_sample_temp_rows(logits.data_ptr(), logits.scalar_type() == at::kBFloat16 ? 1 : 0,
+                            out.data_ptr<int64_t>(), (int)B, (int)logits.size(1), temps.data_ptr<float>(),
+                            seeds.data_ptr<int64_t>(), steps.data_ptr<int32_t>(), cur_stream()));
+  return out;
+}
+
 at::Tensor sample_rows(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor& top_p,
                        const at::Tensor& top_k, const at::Tensor& seeds, const at::Tensor& steps) {
   MX_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "logits [B, V] contiguous GPU");
@@ -647,6 +668,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("sample_rows(Tensor logits, Tensor temps, Tensor top_p, Tensor top_k, Tensor seeds, Tensor steps) -> Tensor");
+  m.def("sample_temp_rows(Tensor logits, Tensor temps, Tensor seeds, Tensor steps) -> Tensor");
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_linear_swiglu(Tensor x, Tensor w) -> Tensor");
@@ -680,6 +702,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("decode_attn", &decode_attn);
   m.impl("sample", &sample);
   m.impl("sample_rows", &sample_rows);
+  m.impl("sample_temp_rows", &sample_temp_rows);
   m.impl("w8_linear", &w8_linear);
   m.impl("skinny_linear", &skinny_linear);
   m.impl("skinny_linear_swiglu", &skinny_linear_swiglu);

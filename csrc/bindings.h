@@ -62,6 +62,8 @@ int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, co
                    int max_seq, int nsplit, float scale, hipStream_t stream);
 int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature, uint32_t seed,
               uint32_t step, hipStream_t stream);
+int mx_sample_temp_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, const float* temps,
+                        const int64_t* seeds, const int32_t* steps, hipStream_t stream);
 // sampling.hip
 int mx_sample_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, const float* temps,
                    const float* top_ps, const int32_t* top_ks, const int64_t* seeds, const int32_t* steps,

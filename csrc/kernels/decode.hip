@@ -410,7 +410,9 @@ __device__ __forceinline__ void samp_pick(float& best, int& bi, float ov, int oi
 template <typename T>
 __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logits, int64_t* __restrict__ out, int V,
                                                      int chunk, float inv_temp, uint32_t seed, uint32_t step,
-                                                     int row0) {
+                                                     int row0, const float* __restrict__ temps,
+                                                     const int64_t* __restrict__ seeds,
+                                                     const int32_t* __restrict__ steps) {
   __shared__ float sv[4];
   __shared__ int si[4];
   __shared__ int s_last;
@@ -418,6 +420,13 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
   const int64_t row = (int64_t)row0 + lrow;
   const T* x = logits + row * V;
   const int c0 = blockIdx.x * chunk, c1 = min(V, c0 + chunk);
+  uint32_t nseed = seed + (uint32_t)row * 7919u;
+  if (temps) {  // per-row parameters (sample_rows without top-k / top-p): noise of sampling.hip
+    const float t = temps[row];
+    inv_temp = t > 0.f ? 1.f / t : 0.f;
+    nseed = (uint32_t)seeds[row];
+    step = (uint32_t)steps[row];
+  }
   float best = -INFINITY;
   int bi = c0 < V ? c0 : 0;
   for (int cb = c0 + (int)threadIdx.x; cb < c1; cb += 256 * 8) {
@@ -434,7 +443,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
       if (c >= c1) break;
       float w = v[u];
       if (inv_temp > 0.f) {
-        const uint32_t h = hash3(seed + (uint32_t)row * 7919u, step, (uint32_t)c);
+        const uint32_t h = hash3(nseed, step, (uint32_t)c);
         const float uu = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
         w = w * inv_temp - __logf(-__logf(uu));  // Gumbel-max
       }
@@ -507,8 +516,9 @@ extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint1
   return (int)hipGetLastError();
 }
 
-extern "C" int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
-                         uint32_t seed, uint32_t step, hipStream_t stream) {
+static int sample_launch(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
+                         uint32_t seed, uint32_t step, const float* temps, const int64_t* seeds,
+                         const int32_t* steps, hipStream_t stream) {
   if (B <= 0) return 0;
   if (V <= 0) return -1;
   const float it = temperature > 0.f ? 1.f / temperature : 0.f;
@@ -520,9 +530,23 @@ extern "C" int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, i
   for (int r0 = 0; r0 < B; r0 += kSampMaxRows) {
     const dim3 grid(nch, std::min(kSampMaxRows, B - r0));
     if (is_bf16)
-      sample_kernel<uint16_t><<<grid, 256, 0, stream>>>((const uint16_t*)logits, out, V, chunk, it, seed, step, r0);
+      sample_kernel<uint16_t><<<grid, 256, 0, stream>>>((const uint16_t*)logits, out, V, chunk, it, seed, step, r0,
+                                                         temps, seeds, steps);
     else
-      sample_kernel<float><<<grid, 256, 0, stream>>>((const float*)logits, out, V, chunk, it, seed, step, r0);
+      sample_kernel<float><<<grid, 256, 0, stream>>>((const float*)logits, out, V, chunk, it, seed, step, r0, temps,
+                                                      seeds, steps);
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
+                         uint32_t seed, uint32_t step, hipStream_t stream) {
+  return sample_launch(logits, is_bf16, out, B, V, temperature, seed, step, nullptr, nullptr, nullptr, stream);
+}
+
+// per-row temperature (<= 0: greedy), seed and step, no top-k / top-p: the draws of
+// sampling.hip's sample_topkp_kernel for such rows (same noise), split over the vocabulary
+extern "C" int mx_sample_temp_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, const float* temps,
+                                   const int64_t* seeds, const int32_t* steps, hipStream_t stream) {
+  return sample_launch(logits, is_bf16, out, B, V, 0.f, 0u, 0u, temps, seeds, steps, stream);
 }

@@ -93,6 +93,9 @@ def sample_rows(logits: torch.Tensor, temps, top_ps, top_ks, seeds, steps) -> to
                            dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
         st = torch.tensor([[int(sd), int(sp)] for sd, sp in zip(seeds, steps)], dtype=torch.int64).pin_memory()
         st = st.to(dev, non_blocking=True)
+        if all(p >= 1.0 for p in top_ps) and all(k <= 0 for k in top_ks):
+            # temperature / greedy rows only: the vocabulary-split kernel (same draws)
+            return ops.sample_temp_rows(x, prm[:, 0].contiguous(), st[:, 0].contiguous(), st[:, 1].int().contiguous())
         return ops.sample_rows(x, prm[:, 0].contiguous(), prm[:, 1].contiguous(), prm[:, 2].int().contiguous(),
                                st[:, 0].contiguous(), st[:, 1].int().contiguous())
     out = torch.empty(B, dtype=torch.long)

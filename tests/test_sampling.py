@@ -60,3 +60,27 @@ def test_gpu_sampler_mixed_batch_and_vocab_128k(gpu):
     assert ids[1] == one[0]
     assert dops.filter_probs(x[2].float().cpu(), 0.9, 0, 0.9)[ids[2]] > 0
     assert dops.filter_probs(x[3].float().cpu(), 1.0, 40, 0.5)[ids[3]] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,V", [(torch.bfloat16, 128256), (torch.float32, 50001)])
+def test_gpu_temperature_rows_split_kernel_matches_topkp_kernel(gpu, dtype, V):
+    """Rows without top-k / top-p go to the vocabulary-split kernel (decode.hip); its draws
+    equal the radix-select kernel's (sampling.hip) for the same (seed, step) noise."""
+    from mxllm.ops import native
+
+    B = 6
+    x = torch.randn(B, V, device=gpu).to(dtype)
+    temps = torch.tensor([0.0, 0.7, 1.0, 1.3, 0.0, 0.2], device=gpu)
+    seeds = torch.tensor([1, 2, 3, 4, 5, 123456789], device=gpu, dtype=torch.int64)
+    steps = torch.tensor([0, 9, 17, 3, 1, 1000], device=gpu, dtype=torch.int32)
+    ones = torch.ones(B, device=gpu)
+    zeros = torch.zeros(B, device=gpu, dtype=torch.int32)
+    for _ in range(3):
+        a = native().sample_temp_rows(x, temps, seeds, steps)
+        b = native().sample_rows(x, temps, ones, zeros, seeds, steps)
+        assert torch.equal(a, b)
+        steps += 1
+    # routed entry point
+    ids = dops.sample_rows(x, temps.tolist(), [1.0] * B, [0] * B, seeds.tolist(), steps.tolist())
+    assert torch.equal(ids, native().sample_rows(x, temps, ones, zeros, seeds, steps))
