@@ -545,6 +545,39 @@ at::Tensor skinny_linear_swiglu(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+// Decode rows (M <= 4): y = rmsnorm(h + delta) . w^T with the RMSNorm (and residual add) in the
+// GEMM prologue (csrc/kernels/skinny_gemm.hip NORM); swiglu: w = [gate; up], y = silu(g) * u.
+// Returns (y, h + delta) — the new residual is h itself when delta is absent.
+std::tuple<at::Tensor, at::Tensor> skinny_norm_linear(const at::Tensor& h, const c10::optional<at::Tensor>& delta,
+                                                      const at::Tensor& gamma, double eps, const at::Tensor& w,
+                                                      bool swiglu) {
+  MX_CHECK(h.is_cuda() && h.scalar_type() == at::kBFloat16 && h.dim() == 2 && h.stride(1) == 1, "h: bf16 [M, K] rows");
+  MX_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1, "w: bf16 [N, K] rows");
+  const int64_t M = h.size(0), K = h.size(1), N = w.size(0);
+  MX_CHECK(gamma.is_cuda() && gamma.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && gamma.numel() == K,
+           "gamma: bf16 [K]");
+  MX_CHECK(w.size(1) == K && M >= 1 && M <= 4 && M * K <= 32768 && N % 16 == 0 && K % 512 == 0 &&
+               h.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (!swiglu || N % 16 == 0),
+           "skinny_norm_linear shape contract");
+  const uint16_t* dp = nullptr;
+  int64_t ldd = 0;
+  at::Tensor h_out = h;
+  if (delta.has_value() && delta->defined()) {
+    const at::Tensor& d = *delta;
+    MX_CHECK(d.is_cuda() && d.scalar_type() == at::kBFloat16 && d.dim() == 2 && d.size(0) == M && d.size(1) == K &&
+                 d.stride(1) == 1 && d.stride(0) % 8 == 0, "delta: bf16 [M, K] rows");
+    dp = bf(d);
+    ldd = d.stride(0);
+    h_out = at::empty({M, K}, h.options());
+  }
+  DevGuard g(h.device());
+  const int64_t Ny = swiglu ? N / 2 : N;
+  auto y = at::empty({M, Ny}, h.options());
+  MX_OK(mx_skinny_norm_gemm(bf(h), h.stride(0), dp, ldd, bf(gamma), (float)eps, dp ? bfm(h_out) : nullptr, bf(w),
+                            w.stride(0), bfm(y), Ny, (int)M, (int)N, (int)K, swiglu ? 1 : 0, cur_stream()));
+  return {y, h_out};
+}
+
 // ---------------------------------------------------------------- fp8 weights (serving)
 // y[M, N] = x[M, K] . (scale[:, None] * q[N, K])^T ; q: e4m3 codes (uint8), scale f32 [N].
 // M <= 32: the fused weight-streaming kernel; otherwise dequantise to bf16 and run the
@@ -672,6 +705,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_linear_swiglu(Tensor x, Tensor w) -> Tensor");
+  m.def("skinny_norm_linear(Tensor h, Tensor? delta, Tensor gamma, float eps, Tensor w, bool swiglu) -> (Tensor, Tensor)");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
   m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha) -> ()");
@@ -706,6 +740,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("w8_linear", &w8_linear);
   m.impl("skinny_linear", &skinny_linear);
   m.impl("skinny_linear_swiglu", &skinny_linear_swiglu);
+  m.impl("skinny_norm_linear", &skinny_norm_linear);
   m.impl("w8_dequant", &w8_dequant);
   m.impl("quant_rows_e4m3", &quant_rows_e4m3);
   m.impl("lora_xwt", &lora_xwt);

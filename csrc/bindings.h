@@ -76,6 +76,9 @@ int mx_skinny_gemm(const uint16_t* x, int64_t ldx, const uint16_t* w, int64_t ld
                    int M, int N, int K, hipStream_t stream);
 int mx_skinny_gemm_swiglu(const uint16_t* x, int64_t ldx, const uint16_t* w, int64_t ldw, uint16_t* y,
                           int64_t ldy, int M, int F, int K, hipStream_t stream);
+int mx_skinny_norm_gemm(const uint16_t* h, int64_t ldh, const uint16_t* delta, int64_t ldd, const uint16_t* gamma,
+                        float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw, uint16_t* y, int64_t ldy, int M,
+                        int N, int K, int swiglu, hipStream_t stream);
 int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, const float* scale, uint16_t* y, int64_t ldy,
                   int M, int N, int K, hipStream_t stream);
 int mx_w8_dequant(const uint8_t* q, const float* scale, uint16_t* w, int64_t N, int K, hipStream_t stream);

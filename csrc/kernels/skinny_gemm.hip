@@ -17,6 +17,11 @@
 //    the epilogue holds both halves of its 8 outputs and writes silu(g) * u [M, F] directly
 //    (g, u rounded to bf16 first, as the separate GEMM + SwiGLU kernels round them: same bits).
 //    Same weight stream as the plain kernel; one launch and the [M, 2F] round trip less.
+//  * NORM (decode, M <= 4 rows): the RMSNorm (with the residual add) that produces X runs in
+//    the prologue: every workgroup rebuilds the normalised rows in LDS from the residual h
+//    (and the sub-block output `delta`), with the thread mapping, summation order and
+//    rounding of rmsnorm.hip's forward kernel (same bits); workgroup 0 stores h + delta.
+//    The X fragments then come from LDS.  Saves the two RMSNorm launches of every layer.
 #include <cstdlib>
 
 #include "common.h"
@@ -35,12 +40,21 @@ __device__ __forceinline__ f32x4 mfma16_sk(const u16x8& a, const u16x8& b, const
 // streamed weight byte drops NC-fold (it equals the weight traffic at 16 tokens with NC = 1).
 __device__ __forceinline__ float silu_sk(float x) { return x / (1.f + __expf(-x)); }
 
-template <int MB, int NC, bool SWO = false>
+struct SkNorm {
+  const uint16_t* delta;  // [M, K] sub-block output added to the residual (nullptr: plain RMSNorm)
+  int64_t ldd;
+  const uint16_t* gamma;  // [K]
+  uint16_t* h_out;        // [M, K] (row stride K): h + delta, written by workgroup 0
+  float eps;
+};
+
+template <int MB, int NC, bool SWO = false, bool NORM = false>
 __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx,
                                                           const uint16_t* __restrict__ W, int64_t ldw,
                                                           uint16_t* __restrict__ Y, int64_t ldy, int M, int K,
-                                                          int F = 0) {
+                                                          int F = 0, SkNorm na = {}) {
   static_assert(!SWO || NC == 1, "SwiGLU epilogue: one channel group");
+  static_assert(!NORM || (MB == 1 && NC == 1), "fused RMSNorm: <= 16 rows, one channel group");
   constexpr int NW = 8, UNR = NC == 1 ? 8 : 4;
   __shared__ f32x4 red[NW][NC][MB][64];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -56,8 +70,82 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
     wrow[j] = W + wr * ldw + (int64_t)w * kq + 16 * g;
   }
   const uint16_t* xr[MB];
+  const int nit = kq / 64;
+  // NORM: the first UNR chunks' weight loads go out before the prologue, so the weight stream's
+  // latency overlaps the RMSNorm instead of following it
+  u16x8 apre[UNR][NC][2];
+  if constexpr (NORM) {
+    if (nit >= UNR) {
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) xr[mb] = X + (int64_t)min(mb * 16 + c, M - 1) * ldx + (int64_t)w * kq + 16 * g;
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          apre[u][j][0] = *reinterpret_cast<const u16x8*>(wrow[j] + u * 64);
+          apre[u][j][1] = *reinterpret_cast<const u16x8*>(wrow[j] + u * 64 + 8);
+        }
+    }
+  }
+  if constexpr (NORM) {
+    // rows m = q, q + 2, ... by wave group q (4 waves = rmsnorm.hip's 256-thread row mapping)
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [M, K] normalised rows
+    __shared__ float nscr[2][4];
+    __shared__ float nrs[4];
+    const int q = w >> 2, tq = tid & 255;
+    for (int m0 = 0; m0 < M; m0 += 2) {
+      const int m = m0 + q;
+      float ss = 0.f;
+      if (m < M) {
+        for (int cc = tq * 8; cc < K; cc += 2048) {
+          const u16x8 hv = *reinterpret_cast<const u16x8*>(X + (int64_t)m * ldx + cc);
+          u16x8 hb = hv;
+          if (na.delta) {
+            const u16x8 dv = *reinterpret_cast<const u16x8*>(na.delta + (int64_t)m * na.ldd + cc);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hb[j] = f2bf(bf2f(dv[j]) + bf2f(hv[j]));
+            if (blockIdx.x == 0) *reinterpret_cast<u16x8*>(na.h_out + (int64_t)m * K + cc) = hb;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float v = bf2f(hb[j]);
+            ss += v * v;
+          }
+          *reinterpret_cast<u16x8*>(xs + (int64_t)m * K + cc) = hb;
+        }
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) nscr[q][w & 3] = ss;
+      __syncthreads();
+      if (m < M && tq == 0) {
+        float r = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r += nscr[q][i];
+        nrs[m] = rsqrtf(r / (float)K + na.eps);
+      }
+      __syncthreads();
+    }
+    // normalise in place (each thread rewrites the chunks it stored)
+    for (int m0 = 0; m0 < M; m0 += 2) {
+      const int m = m0 + q;
+      if (m < M) {
+        const float rs = nrs[m];
+        for (int cc = tq * 8; cc < K; cc += 2048) {
+          u16x8* px = reinterpret_cast<u16x8*>(xs + (int64_t)m * K + cc);
+          const u16x8 hb = *px;
+          const u16x8 gw = *reinterpret_cast<const u16x8*>(na.gamma + cc);
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(hb[j]) * rs * bf2f(gw[j]));
+          *px = o;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) xr[mb] = xs + (int64_t)min(mb * 16 + c, M - 1) * K + (int64_t)w * kq + 16 * g;
+  } else {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) xr[mb] = X + (int64_t)min(mb * 16 + c, M - 1) * ldx + (int64_t)w * kq + 16 * g;
+  }
 
   f32x4 acc[NC][MB];
 #pragma unroll
@@ -85,8 +173,22 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
         acc[j][mb] = mfma16_sk(a[j][1], b[mb][1], acc[j][mb]);
       }
   };
-  const int nit = kq / 64;
   int it = 0;
+  if constexpr (NORM) {
+    if (nit >= UNR) {  // first block: weights prefetched above, X fragments from LDS
+      u16x8 b[UNR][MB][2];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          b[u][mb][0] = *reinterpret_cast<const u16x8*>(xr[mb] + u * 64);
+          b[u][mb][1] = *reinterpret_cast<const u16x8*>(xr[mb] + u * 64 + 8);
+        }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) step(apre[u], b[u]);
+      it = UNR;
+    }
+  }
   for (; it + UNR <= nit; it += UNR) {
     u16x8 a[UNR][NC][2], b[UNR][MB][2];
 #pragma unroll
@@ -139,6 +241,31 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
 }  // namespace mx
 
 using namespace mx;
+
+// y = rmsnorm(h [+ delta]) . W^T (or with the SwiGLU epilogue: W = [gate; up], y [M, N/2]) for
+// M <= 4 decode rows: the RMSNorm in the GEMM prologue (see NORM above).  h [M, K] (row stride
+// ldh), delta [M, K] (row stride ldd) or nullptr, gamma [K]; h_out [M, K] (row stride K) gets
+// h + delta when delta is given.  Requires M * K <= 32768 (64 KiB of LDS), K % 512 == 0.
+extern "C" int mx_skinny_norm_gemm(const uint16_t* h, int64_t ldh, const uint16_t* delta, int64_t ldd,
+                                   const uint16_t* gamma, float eps, uint16_t* h_out, const uint16_t* w,
+                                   int64_t ldw, uint16_t* y, int64_t ldy, int M, int N, int K, int swiglu,
+                                   hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 4 || (int64_t)M * K > 32768 || N % 16 || K % 512 || ldh % 8 || ldd % 8 || ldw % 8 || ldy % 4 ||
+      ldh < K || ldw < K || (delta && (ldd < K || !h_out)))
+    return -1;
+  const SkNorm na{delta, ldd, gamma, h_out, eps};
+  const size_t lds = (size_t)M * K * 2;
+  if (swiglu) {
+    const int Fh = N / 2;
+    if (Fh % 8 || ldy < Fh) return -1;
+    skinny_gemm_kernel<1, 1, true, true><<<Fh / 8, 512, lds, stream>>>(h, ldh, w, ldw, y, ldy, M, K, Fh, na);
+  } else {
+    if (ldy < N) return -1;
+    skinny_gemm_kernel<1, 1, false, true><<<N / 16, 512, lds, stream>>>(h, ldh, w, ldw, y, ldy, M, K, 0, na);
+  }
+  return (int)hipGetLastError();
+}
 
 // X [M, K] bf16 (row stride ldx), W [N, K] bf16 (row stride ldw), Y [M, N] bf16 (row stride
 // ldy).  Requires M in 1..32, N % 16 == 0, K % 512 == 0, ldx / ldw multiples of 8, ldy of 4.

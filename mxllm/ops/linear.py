@@ -346,6 +346,32 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
     return native().skinny_linear_swiglu(x, w)
 
 
+# rows up to which the RMSNorm runs in the decode GEMM's prologue (every workgroup recomputes the
+# rows): measured same box, 8B decode batch 1 3.607 -> 3.479 ms and 70B 26.22 -> 24.98 ms, but batch 4
+# 3.83 -> 4.04 ms (profiles/r2s3_decode_ab/); the kernel takes up to 4
+NORM_M = int(os.environ.get("MXLLM_NORM_FUSED_M", "2"))
+
+
+def norm_linear(delta: torch.Tensor | None, h: torch.Tensor, gamma: torch.Tensor, eps: float, w: torch.Tensor,
+                swiglu: bool = False):
+    """Inference, decode rows: ``(linear(rmsnorm(h + delta) * gamma, w), h + delta)`` as ONE
+    launch (csrc/kernels/skinny_gemm.hip NORM: the RMSNorm in the GEMM prologue, same bits as
+    the RMSNorm kernel + decode GEMM); with ``swiglu`` w = [gate; up] and the first output is
+    silu(g) * u.  ``delta`` None: plain RMSNorm, the residual is ``h``.  None when the fused
+    kernel does not take the call."""
+    if SKINNY_M <= 0 or h.dim() != 2 or (w.requires_grad and torch.is_grad_enabled()):
+        return None
+    M, K = h.shape
+    if not 0 < M <= min(NORM_M, SKINNY_M) or M * K > 32768 or h.stride(1) != 1 or w.shape[1] != K or w.shape[0] % 16:
+        return None
+    if gamma.dtype != torch.bfloat16 or not gamma.is_contiguous() or not _skinny_ok(h, w):
+        return None
+    if delta is not None and (delta.shape != h.shape or delta.dtype != h.dtype or delta.stride(1) != 1
+                              or delta.stride(0) % 8):
+        return None
+    return native().skinny_norm_linear(h, delta, gamma, float(eps), w, bool(swiglu))
+
+
 def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, b: torch.Tensor, splits: Sequence[int],
                 scaling: float) -> torch.Tensor:
     """y = x W^T + scaling * (x A^T) Bbd^T with block-diagonal Bbd (see module doc)."""

@@ -40,6 +40,7 @@ from ..models.llama import FusedLinear
 from ..ops import decode as dops
 
 _SWIGLU_FUSED = os.environ.get("MXLLM_SWIGLU_FUSED", "1") != "0"  # A/B switch (bench/serve_bench.py)
+_NORM_FUSED = os.environ.get("MXLLM_NORM_FUSED", "1") != "0"  # A/B switch: RMSNorm in the decode GEMM prologue
 log = logging.getLogger("mxllm.engine")
 
 
@@ -135,28 +136,48 @@ class Engine:
         self.finished = 0
 
     # ------------------------------------------------------------------ model pieces
+    def _norm_proj(self, delta, h, gamma, lin, swiglu: bool):
+        """(proj(rmsnorm(h + delta) * gamma), h + delta); ``swiglu``: proj = swiglu(lin(.)).
+        Decode rows of a plain bf16 projection run as ONE launch (RMSNorm in the GEMM
+        prologue, SwiGLU in its epilogue: csrc/kernels/skinny_gemm.hip)."""
+        eps = self.cfg.norm_eps
+        plain = type(lin) is FusedLinear and lin.lora_r == 0
+        if _NORM_FUSED and plain:
+            r = ops.norm_linear(delta, h, gamma, eps, lin.weight, swiglu)
+            if r is not None:
+                return r
+        if delta is None:
+            xn = ops.rms_norm(h, gamma, eps)
+        else:
+            xn, h = ops.add_rms_norm(delta, h, gamma, eps)
+        if not swiglu:
+            return lin(xn), h
+        mid = None
+        if _SWIGLU_FUSED and plain and xn.dim() == 2:
+            mid = ops.linear_swiglu(xn, lin.weight)  # decode rows: SwiGLU in the GEMM epilogue
+        if mid is None:
+            mid = ops.swiglu(lin(xn))
+        return mid, h
+
     @torch.no_grad()
     def _layers(self, x: torch.Tensor, attn_fn) -> torch.Tensor:
         m, c = self.model, self.cfg
         h = x
-        xn = ops.rms_norm(h, m.layers[0].attn_norm, c.norm_eps)
+        delta, gamma = None, m.layers[0].attn_norm  # sub-block output not yet added to h, next norm
         for i, layer in enumerate(m.layers):
-            qkv = layer.wqkv(xn)
+            qkv, h = self._norm_proj(delta, h, gamma, layer.wqkv, False)
             o = attn_fn(i, qkv)
             a = layer.wo(o)
             if self.tp is not None:  # row-parallel Wo: sum the heads' partial outputs
                 self.tp.all_reduce_(a)
-            xn, h = ops.add_rms_norm(a, h, layer.mlp_norm, c.norm_eps)
-            mid = None
-            if _SWIGLU_FUSED and type(layer.wgu) is FusedLinear and layer.wgu.lora_r == 0 and xn.dim() == 2:
-                mid = ops.linear_swiglu(xn, layer.wgu.weight)  # decode rows: SwiGLU in the GEMM epilogue
-            if mid is None:
-                mid = ops.swiglu(layer.wgu(xn))
+            mid, h = self._norm_proj(a, h, layer.mlp_norm, layer.wgu, True)
             d = layer.wd(mid)
             if self.tp is not None:  # row-parallel Wdown
                 self.tp.all_reduce_(d)
-            nxt = m.layers[i + 1].attn_norm if i + 1 < len(m.layers) else m.final_norm
-            xn, h = ops.add_rms_norm(d, h, nxt, c.norm_eps)
+            delta, gamma = d, (m.layers[i + 1].attn_norm if i + 1 < len(m.layers) else m.final_norm)
+        if delta is None:
+            return ops.rms_norm(h, gamma, c.norm_eps)
+        xn, h = ops.add_rms_norm(delta, h, gamma, c.norm_eps)
         return xn
 
     @torch.no_grad()

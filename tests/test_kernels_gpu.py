@@ -528,3 +528,36 @@ def test_skinny_linear_swiglu(gpu, M, F, K):
     assert rel_err(y, ref) < 1e-2
     if M <= sys.modules["mxllm.ops.linear"].SKINNY_M:  # the routed entry point takes it
         assert torch.equal(ops.linear_swiglu(x, w), y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,resid,swiglu", [(1, 6144, 4096, False, False), (1, 1024, 4096, True, False),
+                                                (3, 512, 8192, True, False), (4, 2048, 4096, True, True),
+                                                (1, 28672 // 8, 8192, True, True), (2, 1040, 1536, False, True)])
+def test_skinny_norm_linear(gpu, M, N, K, resid, swiglu):
+    """Decode projection with the (residual-add +) RMSNorm in the GEMM prologue: bit-identical to
+    the RMSNorm kernel followed by the decode GEMM (or the SwiGLU-epilogue GEMM), same new
+    residual, and close to the fp32 reference."""
+    from mxllm import ops
+
+    torch.manual_seed(M + N + K)
+    h = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    d = torch.randn(M, K, device=gpu, dtype=torch.bfloat16) if resid else None
+    gamma = (1.0 + 0.1 * torch.randn(K, device=gpu)).to(torch.bfloat16)
+    w = torch.randn(N, K, device=gpu, dtype=torch.bfloat16) * 0.05
+    y, h2 = _ops().skinny_norm_linear(h, d, gamma, 1e-5, w, swiglu)
+    if resid:
+        xn, hn = ops.add_rms_norm(d, h, gamma, 1e-5)
+        assert torch.equal(h2, hn)
+    else:
+        xn, hn = ops.rms_norm(h, gamma, 1e-5), h
+        assert h2.data_ptr() == h.data_ptr()
+    two = _ops().skinny_linear_swiglu(xn, w) if swiglu else _ops().skinny_linear(xn, w)
+    assert torch.equal(y, two)
+    hf = hn.float()
+    xr = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma.float()
+    gu = xr @ w.float().t()
+    ref = torch.nn.functional.silu(gu[:, :N // 2]) * gu[:, N // 2:] if swiglu else gu
+    assert rel_err(y, ref) < 2e-2
+    got = ops.norm_linear(d, h, gamma, 1e-5, w, swiglu)
+    assert got is not None and torch.equal(got[0], y)
