@@ -559,5 +559,8 @@ def test_skinny_norm_linear(gpu, M, N, K, resid, swiglu):
     gu = xr @ w.float().t()
     ref = torch.nn.functional.silu(gu[:, :N // 2]) * gu[:, N // 2:] if swiglu else gu
     assert rel_err(y, ref) < 2e-2
-    got = ops.norm_linear(d, h, gamma, 1e-5, w, swiglu)
-    assert got is not None and torch.equal(got[0], y)
+    import sys
+
+    if M <= sys.modules["mxllm.ops.linear"].NORM_M:  # the routed entry point takes it
+        got = ops.norm_linear(d, h, gamma, 1e-5, w, swiglu)
+        assert got is not None and torch.equal(got[0], y)
