@@ -578,6 +578,55 @@ std::tuple<at::Tensor, at::Tensor> skinny_norm_linear(const at::Tensor& h, const
   return {y, h_out};
 }
 
+// Decode QKV projection with the RoPE / KV-cache append in the GEMM epilogue and, when gamma is
+// given, the (residual-add +) RMSNorm in its prologue (csrc/kernels/skinny_gemm.hip ROPE / NORM).
+// Returns (q [M, Hq, 128] rotated, new residual); K/V rows land in the caches at (slot, pos).
+std::tuple<at::Tensor, at::Tensor> skinny_qkv_rope(const at::Tensor& h, const c10::optional<at::Tensor>& delta,
+                                                   const c10::optional<at::Tensor>& gamma, double eps,
+                                                   const at::Tensor& w, const at::Tensor& cosb, const at::Tensor& sinb,
+                                                   const at::Tensor& pos, const c10::optional<at::Tensor>& slots,
+                                                   at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv) {
+  MX_CHECK(h.is_cuda() && h.scalar_type() == at::kBFloat16 && h.dim() == 2 && h.stride(1) == 1, "h: bf16 [M, K] rows");
+  MX_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1, "w: bf16 [N, K] rows");
+  const int64_t M = h.size(0), K = h.size(1);
+  const bool norm = gamma.has_value() && gamma->defined();
+  MX_CHECK(w.size(0) == (Hq + 2 * Hkv) * 128 && w.size(1) == K && M >= 1 && M <= (norm ? 4 : 16) && K % 512 == 0 &&
+               (!norm || M * K <= 32768) && h.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
+           "skinny_qkv_rope shape contract");
+  MX_CHECK(cosb.scalar_type() == at::kFloat && sinb.scalar_type() == at::kFloat && cosb.is_contiguous() &&
+               sinb.is_contiguous() && cosb.size(-1) == 64, "cos/sin f32 [max_pos, 64]");
+  MX_CHECK(pos.scalar_type() == at::kInt && pos.numel() == M, "pos int32 [M]");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  MX_CHECK(k_cache.size(1) == Hkv && k_cache.size(3) == 128 && k_cache.is_contiguous() && v_cache.is_contiguous(),
+           "caches [slots, Hkv, max_seq, 128]");
+  const int32_t* sl = nullptr;
+  if (slots.has_value() && slots->defined()) {
+    MX_CHECK(slots->scalar_type() == at::kInt && slots->numel() == M, "slots int32 [M]");
+    sl = slots->data_ptr<int32_t>();
+  }
+  const uint16_t* dp = nullptr;
+  int64_t ldd = 0;
+  at::Tensor h_out = h;
+  if (norm && delta.has_value() && delta->defined()) {
+    const at::Tensor& d = *delta;
+    MX_CHECK(d.is_cuda() && d.scalar_type() == at::kBFloat16 && d.dim() == 2 && d.size(0) == M && d.size(1) == K &&
+                 d.stride(1) == 1 && d.stride(0) % 8 == 0, "delta: bf16 [M, K] rows");
+    dp = bf(d);
+    ldd = d.stride(0);
+    h_out = at::empty({M, K}, h.options());
+  }
+  if (norm)
+    MX_CHECK(gamma->scalar_type() == at::kBFloat16 && gamma->is_contiguous() && gamma->numel() == K, "gamma bf16 [K]");
+  DevGuard g(h.device());
+  auto q = at::empty({M, Hq, 128}, h.options());
+  MX_OK(mx_skinny_rope_gemm(bf(h), h.stride(0), norm ? 1 : 0, dp, ldd, norm ? bf(*gamma) : nullptr, (float)eps,
+                            dp ? bfm(h_out) : nullptr, bf(w), w.stride(0), cosb.data_ptr<float>(),
+                            sinb.data_ptr<float>(), pos.data_ptr<int32_t>(), sl, bfm(q), bfm(k_cache),
+                            bfm(v_cache), (int)Hq, (int)Hkv, (int)k_cache.size(2), (int)M, (int)K, cur_stream()));
+  return {q, h_out};
+}
+
 // ---------------------------------------------------------------- fp8 weights (serving)
 // y[M, N] = x[M, K] . (scale[:, None] * q[N, K])^T ; q: e4m3 codes (uint8), scale f32 [N].
 // M <= 32: the fused weight-streaming kernel; otherwise dequantise to bf16 and run the
@@ -705,6 +754,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_linear_swiglu(Tensor x, Tensor w) -> Tensor");
+  m.def("skinny_qkv_rope(Tensor h, Tensor? delta, Tensor? gamma, float eps, Tensor w, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv) -> (Tensor, Tensor)");
   m.def("skinny_norm_linear(Tensor h, Tensor? delta, Tensor gamma, float eps, Tensor w, bool swiglu) -> (Tensor, Tensor)");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
@@ -740,6 +790,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("w8_linear", &w8_linear);
   m.impl("skinny_linear", &skinny_linear);
   m.impl("skinny_linear_swiglu", &skinny_linear_swiglu);
+  m.impl("skinny_qkv_rope", &skinny_qkv_rope);
   m.impl("skinny_norm_linear", &skinny_norm_linear);
   m.impl("w8_dequant", &w8_dequant);
   m.impl("quant_rows_e4m3", &quant_rows_e4m3);

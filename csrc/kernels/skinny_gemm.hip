@@ -22,6 +22,11 @@
 //    (and the sub-block output `delta`), with the thread mapping, summation order and
 //    rounding of rmsnorm.hip's forward kernel (same bits); workgroup 0 stores h + delta.
 //    The X fragments then come from LDS.  Saves the two RMSNorm launches of every layer.
+//  * ROPE (decode QKV projection, head_dim 128): a workgroup's 16 channels are 8 first-half
+//    channels i..i+7 of one head and the matching second-half channels 64+i..64+i+7, so the
+//    epilogue holds both halves of each rotation pair and does decode.hip rope_append's work:
+//    rotated q rows -> q, rotated k and plain v rows -> the KV cache at (slot, pos).  Saves the
+//    rope_append launch of every layer.
 #include <cstdlib>
 
 #include "common.h"
@@ -48,12 +53,24 @@ struct SkNorm {
   float eps;
 };
 
-template <int MB, int NC, bool SWO = false, bool NORM = false>
+struct SkRope {
+  const float* cosb;  // [max_pos, 64]
+  const float* sinb;
+  const int32_t* pos;    // [M] position of the new token
+  const int32_t* slots;  // [M] cache slot (nullptr: row index)
+  uint16_t* q;           // [M, Hq, 128]
+  uint16_t* kc;          // [slots, Hkv, max_seq, 128]
+  uint16_t* vc;
+  int Hq, Hkv, max_seq;
+};
+
+template <int MB, int NC, bool SWO = false, bool NORM = false, bool ROPE = false>
 __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx,
                                                           const uint16_t* __restrict__ W, int64_t ldw,
                                                           uint16_t* __restrict__ Y, int64_t ldy, int M, int K,
-                                                          int F = 0, SkNorm na = {}) {
+                                                          int F = 0, SkNorm na = {}, SkRope rp = {}) {
   static_assert(!SWO || NC == 1, "SwiGLU epilogue: one channel group");
+  static_assert(!ROPE || (NC == 1 && !SWO), "RoPE epilogue: one channel group");
   static_assert(!NORM || (MB == 1 && NC == 1), "fused RMSNorm: <= 16 rows, one channel group");
   constexpr int NW = 8, UNR = NC == 1 ? 8 : 4;
   __shared__ f32x4 red[NW][NC][MB][64];
@@ -66,7 +83,10 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
     // SWO: channel c < 8 -> gate row blockIdx.x * 8 + c, c >= 8 -> the matching up row
-    const int64_t wr = SWO ? (int64_t)blockIdx.x * 8 + (c & 7) + (c >= 8 ? F : 0) : (int64_t)(n0 + 16 * j + c);
+    // ROPE: head blockIdx.x / 8, pair base 8 (blockIdx.x % 8); c >= 8 -> the second-half row
+    const int64_t wr = SWO    ? (int64_t)blockIdx.x * 8 + (c & 7) + (c >= 8 ? F : 0)
+                       : ROPE ? (int64_t)(blockIdx.x >> 3) * 128 + (blockIdx.x & 7) * 8 + (c & 7) + (c >= 8 ? 64 : 0)
+                              : (int64_t)(n0 + 16 * j + c);
     wrow[j] = W + wr * ldw + (int64_t)w * kq + 16 * g;
   }
   const uint16_t* xr[MB];
@@ -216,7 +236,37 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
 #pragma unroll
         for (int ww = 1; ww < NW; ++ww) s += red[ww][j][mb][lane];
         const int m = mb * 16 + c;
-        if constexpr (SWO) {
+        if constexpr (ROPE) {
+          // lane (c, g < 2): first-half pair indices i0 + 4g .. +3; lane ^ 32: their second halves
+          f32x4 hi;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hi[i] = __shfl_xor(s[i], 32, 64);
+          if (g < 2 && m < M) {
+            const int head = blockIdx.x >> 3, i0 = (blockIdx.x & 7) * 8 + 4 * g;
+            const int p = rp.pos[m];
+            const int slot = rp.slots ? rp.slots[m] : m;
+            u16x4 y1, y2;
+            uint16_t* dst;
+            if (head >= rp.Hq + rp.Hkv) {  // v: no rotation
+#pragma unroll
+              for (int i = 0; i < 4; ++i) y1[i] = f2bf(s[i]), y2[i] = f2bf(hi[i]);
+              dst = rp.vc + (((int64_t)slot * rp.Hkv + (head - rp.Hq - rp.Hkv)) * rp.max_seq + p) * 128;
+            } else {
+              const float* cp = rp.cosb + (int64_t)p * 64 + i0;
+              const float* sp = rp.sinb + (int64_t)p * 64 + i0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {  // rope_append's arithmetic on the bf16-rounded projection
+                const float a = bf2f(f2bf(s[i])), bb = bf2f(f2bf(hi[i]));
+                y1[i] = f2bf(a * cp[i] - bb * sp[i]);
+                y2[i] = f2bf(bb * cp[i] + a * sp[i]);
+              }
+              dst = head < rp.Hq ? rp.q + ((int64_t)m * rp.Hq + head) * 128
+                                 : rp.kc + (((int64_t)slot * rp.Hkv + (head - rp.Hq)) * rp.max_seq + p) * 128;
+            }
+            *reinterpret_cast<u16x4*>(dst + i0) = y1;
+            *reinterpret_cast<u16x4*>(dst + 64 + i0) = y2;
+          }
+        } else if constexpr (SWO) {
           // lane (c, g) holds channels 4g..4g+3: gate outputs for g < 2, the up outputs of the
           // same columns in lane (c, g + 2) = lane ^ 32
           f32x4 up;
@@ -246,6 +296,31 @@ using namespace mx;
 // M <= 4 decode rows: the RMSNorm in the GEMM prologue (see NORM above).  h [M, K] (row stride
 // ldh), delta [M, K] (row stride ldd) or nullptr, gamma [K]; h_out [M, K] (row stride K) gets
 // h + delta when delta is given.  Requires M * K <= 32768 (64 KiB of LDS), K % 512 == 0.
+// Decode QKV projection with the RoPE / KV-cache append in the epilogue (see ROPE above), and
+// optionally the RMSNorm in the prologue (h, delta, gamma as mx_skinny_norm_gemm; norm = 0: X = h
+// as is, any M <= 16).  w [(Hq + 2 Hkv) * 128, K]; q out [M, Hq, 128].
+extern "C" int mx_skinny_rope_gemm(const uint16_t* h, int64_t ldh, int norm, const uint16_t* delta, int64_t ldd,
+                                   const uint16_t* gamma, float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw,
+                                   const float* cosb, const float* sinb, const int32_t* pos, const int32_t* slots,
+                                   uint16_t* q, uint16_t* kc, uint16_t* vc, int Hq, int Hkv, int max_seq, int M,
+                                   int K, hipStream_t stream) {
+  if (M <= 0) return 0;
+  const int N = (Hq + 2 * Hkv) * 128;
+  if (M > (norm ? 4 : 16) || (norm && (int64_t)M * K > 32768) || K % 512 || ldh % 8 || ldd % 8 || ldw % 8 ||
+      ldh < K || ldw < K || (norm && delta && (ldd < K || !h_out)))
+    return -1;
+  const SkRope rp{cosb, sinb, pos, slots, q, kc, vc, Hq, Hkv, max_seq};
+  if (norm) {
+    const SkNorm na{delta, ldd, gamma, h_out, eps};
+    skinny_gemm_kernel<1, 1, false, true, true><<<N / 16, 512, (size_t)M * K * 2, stream>>>(
+        h, ldh, w, ldw, nullptr, 0, M, K, 0, na, rp);
+  } else {
+    skinny_gemm_kernel<1, 1, false, false, true><<<N / 16, 512, 0, stream>>>(h, ldh, w, ldw, nullptr, 0, M, K, 0,
+                                                                               SkNorm{}, rp);
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int mx_skinny_norm_gemm(const uint16_t* h, int64_t ldh, const uint16_t* delta, int64_t ldd,
                                    const uint16_t* gamma, float eps, uint16_t* h_out, const uint16_t* w,
                                    int64_t ldw, uint16_t* y, int64_t ldy, int M, int N, int K, int swiglu,

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+import math
 import os
 import threading
 import time
@@ -41,6 +42,7 @@ from ..ops import decode as dops
 
 _SWIGLU_FUSED = os.environ.get("MXLLM_SWIGLU_FUSED", "1") != "0"  # A/B switch (bench/serve_bench.py)
 _NORM_FUSED = os.environ.get("MXLLM_NORM_FUSED", "1") != "0"  # A/B switch: RMSNorm in the decode GEMM prologue
+_ROPE_FUSED = os.environ.get("MXLLM_ROPE_FUSED", "1") != "0"  # A/B switch: RoPE + cache append in the QKV epilogue
 log = logging.getLogger("mxllm.engine")
 
 
@@ -160,13 +162,20 @@ class Engine:
         return mid, h
 
     @torch.no_grad()
-    def _layers(self, x: torch.Tensor, attn_fn) -> torch.Tensor:
+    def _layers(self, x: torch.Tensor, attn_fn, qkv_fn=None) -> torch.Tensor:
+        """``qkv_fn(i, delta, h, gamma, layer)`` (decode): the fused norm + QKV + RoPE/cache-append
+        projection returning (rotated q, new residual) or None; ``attn_fn(i, qkv, q=None)``."""
         m, c = self.model, self.cfg
         h = x
         delta, gamma = None, m.layers[0].attn_norm  # sub-block output not yet added to h, next norm
         for i, layer in enumerate(m.layers):
-            qkv, h = self._norm_proj(delta, h, gamma, layer.wqkv, False)
-            o = attn_fn(i, qkv)
+            r = qkv_fn(i, delta, h, gamma, layer) if qkv_fn is not None else None
+            if r is not None:
+                q, h = r
+                o = attn_fn(i, None, q)
+            else:
+                qkv, h = self._norm_proj(delta, h, gamma, layer.wqkv, False)
+                o = attn_fn(i, qkv)
             a = layer.wo(o)
             if self.tp is not None:  # row-parallel Wo: sum the heads' partial outputs
                 self.tp.all_reduce_(a)
@@ -256,11 +265,22 @@ class Engine:
         sl = inp[2].to(torch.int32)
         x = ops.embedding(inp[0], m.tok_emb)
 
-        def attn(i, qkv):
+        def attn(i, qkv, q=None):
+            if q is not None:  # RoPE and the cache append already done by the QKV GEMM
+                return ops.native().decode_attn(q, self.k_cache[i], self.v_cache[i], pos, sl, max_len,
+                                                1.0 / math.sqrt(c.head_dim), 1)
             return dops.decode_attention(qkv, m.rope_cos, m.rope_sin, self.k_cache[i], self.v_cache[i], pos, sl,
                                          c.n_heads, c.n_kv_heads, c.head_dim, max_len)
 
-        xn = self._layers(x, attn)
+        def qkv_fn(i, delta, h, gamma, layer):
+            # 1-2 rows: RMSNorm prologue + QKV GEMM + RoPE/cache-append epilogue in one launch
+            if not (_ROPE_FUSED and _NORM_FUSED and self.tp is None and c.head_dim == 128
+                    and type(layer.wqkv) is FusedLinear and layer.wqkv.lora_r == 0):
+                return None
+            return ops.qkv_rope_linear(delta, h, gamma, c.norm_eps, layer.wqkv.weight, m.rope_cos, m.rope_sin, pos,
+                                       sl, self.k_cache[i], self.v_cache[i], c.n_heads, c.n_kv_heads)
+
+        xn = self._layers(x, attn, qkv_fn)
         return self._logits(xn)
 
     def _buckets(self, B: int, max_len: int) -> tuple[int, int]:

@@ -564,3 +564,39 @@ def test_skinny_norm_linear(gpu, M, N, K, resid, swiglu):
     if M <= sys.modules["mxllm.ops.linear"].NORM_M:  # the routed entry point takes it
         got = ops.norm_linear(d, h, gamma, 1e-5, w, swiglu)
         assert got is not None and torch.equal(got[0], y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,Hq,Hkv,K,norm,resid", [(1, 32, 8, 4096, True, True), (2, 8, 2, 1024, True, False),
+                                                   (2, 64, 8, 8192, True, True), (5, 16, 4, 2048, False, False)])
+def test_skinny_qkv_rope(gpu, M, Hq, Hkv, K, norm, resid):
+    """Decode QKV projection with RoPE + KV-cache append in the GEMM epilogue (and the RMSNorm
+    in its prologue): the same q, cache rows and residual as RMSNorm + decode GEMM + rope_append."""
+    from mxllm import ops
+
+    torch.manual_seed(M * 3 + Hq)
+    D, max_seq, nslots = 128, 300, M + 2
+    N = (Hq + 2 * Hkv) * D
+    h = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    d = torch.randn(M, K, device=gpu, dtype=torch.bfloat16) if resid else None
+    gamma = (1.0 + 0.1 * torch.randn(K, device=gpu)).to(torch.bfloat16) if norm else None
+    w = torch.randn(N, K, device=gpu, dtype=torch.bfloat16) * 0.05
+    cos, sin = ref.rope_tables(1024, D, 500000.0, None, gpu)
+    pos = torch.tensor([17, 299, 0, 5, 123][:M], dtype=torch.int32, device=gpu)
+    slots = torch.tensor([3, 0, 2, 1, 4][:M], dtype=torch.int32, device=gpu) % nslots
+    kc = torch.randn(nslots, Hkv, max_seq, D, device=gpu, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q, h2 = _ops().skinny_qkv_rope(h, d, gamma, 1e-5, w, cos, sin, pos, slots, kc, vc, Hq, Hkv)
+    if norm:
+        if resid:
+            xn, hn = ops.add_rms_norm(d, h, gamma, 1e-5)
+        else:
+            xn, hn = ops.rms_norm(h, gamma, 1e-5), h
+        assert torch.equal(h2, hn)
+    else:
+        xn = h
+    qkv = _ops().skinny_linear(xn, w)
+    q_ref = _ops().rope_append(qkv, cos, sin, pos, slots, kc2, vc2, Hq, Hkv, D)
+    assert torch.equal(q.view(M, -1), q_ref.reshape(M, -1))
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
