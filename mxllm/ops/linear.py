@@ -352,23 +352,29 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
 NORM_M = int(os.environ.get("MXLLM_NORM_FUSED_M", "2"))
 
 
+def qkv_rope_ok(h: torch.Tensor, w: torch.Tensor, cos, sin, k_cache, v_cache, Hq: int, Hkv: int,
+                norm: bool) -> bool:
+    """Whether :func:`qkv_rope_linear` takes these shapes (``norm``: with the RMSNorm prologue)."""
+    if SKINNY_M <= 0 or h.dim() != 2 or (w.requires_grad and torch.is_grad_enabled()):
+        return False
+    M, K = h.shape
+    if not 0 < M <= (min(NORM_M, SKINNY_M) if norm else SKINNY_M) or (norm and M * K > 32768):
+        return False
+    if w.shape != ((Hq + 2 * Hkv) * 128, K) or k_cache.shape[-1] != 128 or k_cache.dtype != torch.bfloat16:
+        return False
+    return bool(_skinny_ok(h, w) and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+                and k_cache.is_contiguous() and v_cache.is_contiguous())
+
+
 def qkv_rope_linear(delta, h: torch.Tensor, gamma, eps: float, w: torch.Tensor, cos, sin, pos, slots, k_cache,
                     v_cache, Hq: int, Hkv: int):
     """Inference, decode rows: the QKV projection with RoPE and the KV-cache append in the GEMM
     epilogue (csrc/kernels/skinny_gemm.hip ROPE) and, for 1-NORM_M rows, the (residual-add +)
     RMSNorm in its prologue; ``gamma`` None: ``h`` is already normalised.  Returns
     (q [M, Hq, 128] rotated, new residual) or None when the fused kernel does not take the call."""
-    if SKINNY_M <= 0 or h.dim() != 2 or (w.requires_grad and torch.is_grad_enabled()):
+    if not qkv_rope_ok(h, w, cos, sin, k_cache, v_cache, Hq, Hkv, gamma is not None):
         return None
-    M, K = h.shape
     norm = gamma is not None
-    if not 0 < M <= (min(NORM_M, SKINNY_M) if norm else SKINNY_M) or (norm and M * K > 32768):
-        return None
-    if w.shape != ((Hq + 2 * Hkv) * 128, K) or k_cache.shape[-1] != 128 or k_cache.dtype != torch.bfloat16:
-        return None
-    if not (_skinny_ok(h, w) and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
-            and k_cache.is_contiguous() and v_cache.is_contiguous()):
-        return None
     if norm and (gamma.dtype != torch.bfloat16 or not gamma.is_contiguous()):
         return None
     if delta is not None and (not norm or delta.shape != h.shape or delta.stride(1) != 1 or delta.stride(0) % 8):

@@ -273,12 +273,25 @@ class Engine:
                                          c.n_heads, c.n_kv_heads, c.head_dim, max_len)
 
         def qkv_fn(i, delta, h, gamma, layer):
-            # 1-2 rows: RMSNorm prologue + QKV GEMM + RoPE/cache-append epilogue in one launch
-            if not (_ROPE_FUSED and _NORM_FUSED and self.tp is None and c.head_dim == 128
+            # QKV GEMM with the RoPE/cache-append epilogue; 1-2 rows also with the RMSNorm prologue
+            # (one launch), more rows after the RMSNorm kernel
+            if not (_ROPE_FUSED and self.tp is None and c.head_dim == 128
                     and type(layer.wqkv) is FusedLinear and layer.wqkv.lora_r == 0):
                 return None
-            return ops.qkv_rope_linear(delta, h, gamma, c.norm_eps, layer.wqkv.weight, m.rope_cos, m.rope_sin, pos,
-                                       sl, self.k_cache[i], self.v_cache[i], c.n_heads, c.n_kv_heads)
+            rope = (layer.wqkv.weight, m.rope_cos, m.rope_sin, pos, sl, self.k_cache[i], self.v_cache[i],
+                    c.n_heads, c.n_kv_heads)
+            if _NORM_FUSED:
+                r = ops.qkv_rope_linear(delta, h, gamma, c.norm_eps, *rope)
+                if r is not None:
+                    return r
+            if not ops.qkv_rope_ok(h, rope[0], rope[1], rope[2], rope[5], rope[6], rope[7], rope[8], False):
+                return None
+            if delta is None:
+                xn = ops.rms_norm(h, gamma, c.norm_eps)
+            else:
+                xn, h = ops.add_rms_norm(delta, h, gamma, c.norm_eps)
+            q, _ = ops.qkv_rope_linear(None, xn, None, c.norm_eps, *rope)
+            return q, h
 
         xn = self._layers(x, attn, qkv_fn)
         return self._logits(xn)
