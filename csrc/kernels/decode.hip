@@ -391,17 +391,17 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 // logits [B, V] (bf16 or f32); temperature <= 0 -> greedy.  out ids [B] int64.
 //
 // Split over the vocabulary: grid (nchunks, B), each workgroup reduces `chunk`
-// logits of one row to (max, smallest index), the last workgroup of the row to
-// arrive (agent-scope counter, no spinning) combines the partials in chunk
-// order.  One workgroup per row left a batch-1 decode step with ONE CU
-// streaming 256 KB of logits: 176 us of a 4.1 ms 8B step; split over ~63
-// workgroups it is a few microseconds.  The result (and the Gumbel noise of
-// each (seed, row, step, index)) is the same as a single-pass argmax.
+// logits of one row to (max, smallest index); a second one-wave-per-row kernel
+// combines the partials in chunk order.  One workgroup per row left a batch-1
+// decode step with ONE CU streaming 256 KB of logits: 176 us of a 4.1 ms 8B
+// step; split over ~63 workgroups it is a few microseconds.  (A last-arriver
+// merge in the same kernel needed an agent-scope release fence per workgroup:
+// 94 us at batch 64.)  The result (and the Gumbel noise of each (seed, row,
+// step, index)) is the same as a single-pass argmax.
 constexpr int kSampMaxRows = 1024;   // rows per launch (more rows: several launches)
 constexpr int kSampMaxChunks = 64;   // partials per row (= one wave in the final pass)
 __device__ float g_samp_val[kSampMaxRows * kSampMaxChunks];
 __device__ int g_samp_idx[kSampMaxRows * kSampMaxChunks];
-__device__ unsigned int g_samp_cnt[kSampMaxRows];  // zero at load, reset by the last arriver
 
 __device__ __forceinline__ void samp_pick(float& best, int& bi, float ov, int oi) {
   if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
@@ -415,8 +415,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
                                                      const int32_t* __restrict__ steps) {
   __shared__ float sv[4];
   __shared__ int si[4];
-  __shared__ int s_last;
-  const int lrow = blockIdx.y, nch = gridDim.x;
+  const int lrow = blockIdx.y;
   const int64_t row = (int64_t)row0 + lrow;
   const T* x = logits + row * V;
   const int c0 = blockIdx.x * chunk, c1 = min(V, c0 + chunk);
@@ -458,24 +457,21 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
     for (int w = 1; w < 4; ++w) samp_pick(best, bi, sv[w], si[w]);
     g_samp_val[lrow * kSampMaxChunks + blockIdx.x] = best;
     g_samp_idx[lrow * kSampMaxChunks + blockIdx.x] = bi;
-    __threadfence();
-    const unsigned prev = atomicAdd(&g_samp_cnt[lrow], 1u);
-    s_last = prev == (unsigned)(nch - 1);
-    if (s_last) g_samp_cnt[lrow] = 0u;
   }
-  __syncthreads();
-  if (!s_last || threadIdx.x >= 64) return;
-  __threadfence();  // acquire: the other workgroups' partials
-  const int l = threadIdx.x;
-  best = -INFINITY;
-  bi = 0x7fffffff;
+}
+
+// partials of one row (chunk order) -> out[row]; grid rows, one wave
+__global__ void __launch_bounds__(64) sample_final_kernel(int64_t* __restrict__ out, int nch, int row0) {
+  const int lrow = blockIdx.x, l = threadIdx.x;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
   if (l < nch) {
     best = g_samp_val[lrow * kSampMaxChunks + l];
     bi = g_samp_idx[lrow * kSampMaxChunks + l];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) samp_pick(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
-  if (l == 0) out[row] = bi == 0x7fffffff ? 0 : bi;
+  if (l == 0) out[(int64_t)row0 + lrow] = bi == 0x7fffffff ? 0 : bi;
 }
 
 }  // namespace mx
@@ -535,6 +531,7 @@ static int sample_launch(const void* logits, int is_bf16, int64_t* out, int B, i
     else
       sample_kernel<float><<<grid, 256, 0, stream>>>((const float*)logits, out, V, chunk, it, seed, step, r0, temps,
                                                       seeds, steps);
+    sample_final_kernel<<<grid.y, 64, 0, stream>>>(out, nch, r0);
   }
   return (int)hipGetLastError();
 }
