@@ -368,10 +368,35 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restri
                                                            uint16_t* __restrict__ out, int nsplit) {
   const int64_t bh = blockIdx.x;
   const float* ml = part_ml + bh * nsplit * 2;
+  const int d = threadIdx.x;
+  if (nsplit <= 8) {
+    // every partial load issued at once (one memory round trip instead of two: the outputs'
+    // loads do not wait for the maxima); same arithmetic order as the loop below
+    float mv[8], lv[8], ov[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const bool on = s < nsplit;
+      mv[s] = on ? ml[2 * s] : -INFINITY;
+      lv[s] = on ? ml[2 * s + 1] : 0.f;
+      ov[s] = on ? part_o[(bh * nsplit + s) * D + d] : 0.f;
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) M = fmaxf(M, mv[s]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (mv[s] == -INFINITY) continue;
+      const float wgt = __builtin_amdgcn_exp2f(mv[s] - M);
+      L += wgt * lv[s];
+      acc += wgt * ov[s];
+    }
+    out[bh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+    return;
+  }
   float M = -INFINITY;
   for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
   float L = 0.f, acc = 0.f;
-  const int d = threadIdx.x;
   for (int s = 0; s < nsplit; ++s) {
     const float m = ml[2 * s];
     if (m == -INFINITY) continue;
