@@ -30,6 +30,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "decode_fuse.h"
 
 namespace mx {
 
@@ -43,27 +44,6 @@ __device__ __forceinline__ f32x4 mfma16_sk(const u16x8& a, const u16x8& b, const
 // MB: 16-token blocks (1 or 2); X rows >= M are clamped to M-1 and discarded.
 // NC: 16-channel groups per workgroup: each X fragment then feeds NC MFMAs, so X traffic per
 // streamed weight byte drops NC-fold (it equals the weight traffic at 16 tokens with NC = 1).
-__device__ __forceinline__ float silu_sk(float x) { return x / (1.f + __expf(-x)); }
-
-struct SkNorm {
-  const uint16_t* delta;  // [M, K] sub-block output added to the residual (nullptr: plain RMSNorm)
-  int64_t ldd;
-  const uint16_t* gamma;  // [K]
-  uint16_t* h_out;        // [M, K] (row stride K): h + delta, written by workgroup 0
-  float eps;
-};
-
-struct SkRope {
-  const float* cosb;  // [max_pos, 64]
-  const float* sinb;
-  const int32_t* pos;    // [M] position of the new token
-  const int32_t* slots;  // [M] cache slot (nullptr: row index)
-  uint16_t* q;           // [M, Hq, 128]
-  uint16_t* kc;          // [slots, Hkv, max_seq, 128]
-  uint16_t* vc;
-  int Hq, Hkv, max_seq;
-};
-
 template <int MB, int NC, bool SWO = false, bool NORM = false, bool ROPE = false>
 __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx,
                                                           const uint16_t* __restrict__ W, int64_t ldw,
@@ -84,9 +64,7 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
   for (int j = 0; j < NC; ++j) {
     // SWO: channel c < 8 -> gate row blockIdx.x * 8 + c, c >= 8 -> the matching up row
     // ROPE: head blockIdx.x / 8, pair base 8 (blockIdx.x % 8); c >= 8 -> the second-half row
-    const int64_t wr = SWO    ? (int64_t)blockIdx.x * 8 + (c & 7) + (c >= 8 ? F : 0)
-                       : ROPE ? (int64_t)(blockIdx.x >> 3) * 128 + (blockIdx.x & 7) * 8 + (c & 7) + (c >= 8 ? 64 : 0)
-                              : (int64_t)(n0 + 16 * j + c);
+    const int64_t wr = (SWO || ROPE) ? dfuse_row<SWO>(blockIdx.x, c, F) : (int64_t)(n0 + 16 * j + c);
     wrow[j] = W + wr * ldw + (int64_t)w * kq + 16 * g;
   }
   const uint16_t* xr[MB];
@@ -106,60 +84,10 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
     }
   }
   if constexpr (NORM) {
-    // rows m = q, q + 2, ... by wave group q (4 waves = rmsnorm.hip's 256-thread row mapping)
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [M, K] normalised rows
     __shared__ float nscr[2][4];
     __shared__ float nrs[4];
-    const int q = w >> 2, tq = tid & 255;
-    for (int m0 = 0; m0 < M; m0 += 2) {
-      const int m = m0 + q;
-      float ss = 0.f;
-      if (m < M) {
-        for (int cc = tq * 8; cc < K; cc += 2048) {
-          const u16x8 hv = *reinterpret_cast<const u16x8*>(X + (int64_t)m * ldx + cc);
-          u16x8 hb = hv;
-          if (na.delta) {
-            const u16x8 dv = *reinterpret_cast<const u16x8*>(na.delta + (int64_t)m * na.ldd + cc);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) hb[j] = f2bf(bf2f(dv[j]) + bf2f(hv[j]));
-            if (blockIdx.x == 0) *reinterpret_cast<u16x8*>(na.h_out + (int64_t)m * K + cc) = hb;
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float v = bf2f(hb[j]);
-            ss += v * v;
-          }
-          *reinterpret_cast<u16x8*>(xs + (int64_t)m * K + cc) = hb;
-        }
-      }
-      ss = wave_sum(ss);
-      if (lane == 0) nscr[q][w & 3] = ss;
-      __syncthreads();
-      if (m < M && tq == 0) {
-        float r = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r += nscr[q][i];
-        nrs[m] = rsqrtf(r / (float)K + na.eps);
-      }
-      __syncthreads();
-    }
-    // normalise in place (each thread rewrites the chunks it stored)
-    for (int m0 = 0; m0 < M; m0 += 2) {
-      const int m = m0 + q;
-      if (m < M) {
-        const float rs = nrs[m];
-        for (int cc = tq * 8; cc < K; cc += 2048) {
-          u16x8* px = reinterpret_cast<u16x8*>(xs + (int64_t)m * K + cc);
-          const u16x8 hb = *px;
-          const u16x8 gw = *reinterpret_cast<const u16x8*>(na.gamma + cc);
-          u16x8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(hb[j]) * rs * bf2f(gw[j]));
-          *px = o;
-        }
-      }
-    }
-    __syncthreads();
+    dfuse_norm_rows(X, ldx, M, K, na, xs, nscr, nrs);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) xr[mb] = xs + (int64_t)min(mb * 16 + c, M - 1) * K + (int64_t)w * kq + 16 * g;
   } else {
@@ -237,47 +165,9 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
         for (int ww = 1; ww < NW; ++ww) s += red[ww][j][mb][lane];
         const int m = mb * 16 + c;
         if constexpr (ROPE) {
-          // lane (c, g < 2): first-half pair indices i0 + 4g .. +3; lane ^ 32: their second halves
-          f32x4 hi;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) hi[i] = __shfl_xor(s[i], 32, 64);
-          if (g < 2 && m < M) {
-            const int head = blockIdx.x >> 3, i0 = (blockIdx.x & 7) * 8 + 4 * g;
-            const int p = rp.pos[m];
-            const int slot = rp.slots ? rp.slots[m] : m;
-            u16x4 y1, y2;
-            uint16_t* dst;
-            if (head >= rp.Hq + rp.Hkv) {  // v: no rotation
-#pragma unroll
-              for (int i = 0; i < 4; ++i) y1[i] = f2bf(s[i]), y2[i] = f2bf(hi[i]);
-              dst = rp.vc + (((int64_t)slot * rp.Hkv + (head - rp.Hq - rp.Hkv)) * rp.max_seq + p) * 128;
-            } else {
-              const float* cp = rp.cosb + (int64_t)p * 64 + i0;
-              const float* sp = rp.sinb + (int64_t)p * 64 + i0;
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {  // rope_append's arithmetic on the bf16-rounded projection
-                const float a = bf2f(f2bf(s[i])), bb = bf2f(f2bf(hi[i]));
-                y1[i] = f2bf(a * cp[i] - bb * sp[i]);
-                y2[i] = f2bf(bb * cp[i] + a * sp[i]);
-              }
-              dst = head < rp.Hq ? rp.q + ((int64_t)m * rp.Hq + head) * 128
-                                 : rp.kc + (((int64_t)slot * rp.Hkv + (head - rp.Hq)) * rp.max_seq + p) * 128;
-            }
-            *reinterpret_cast<u16x4*>(dst + i0) = y1;
-            *reinterpret_cast<u16x4*>(dst + 64 + i0) = y2;
-          }
+          dfuse_rope_store(s, g, m, M, blockIdx.x, rp);
         } else if constexpr (SWO) {
-          // lane (c, g) holds channels 4g..4g+3: gate outputs for g < 2, the up outputs of the
-          // same columns in lane (c, g + 2) = lane ^ 32
-          f32x4 up;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32, 64);
-          if (g < 2 && m < M) {
-            u16x4 o;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] = f2bf(silu_sk(bf2f(f2bf(s[i]))) * bf2f(f2bf(up[i])));
-            *reinterpret_cast<u16x4*>(Y + (int64_t)m * ldy + (int64_t)blockIdx.x * 8 + 4 * g) = o;
-          }
+          dfuse_swiglu_store(s, g, m, M, Y, ldy, blockIdx.x);
         } else if (m < M) {
           u16x4 o;
 #pragma unroll
