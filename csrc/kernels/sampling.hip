@@ -7,7 +7,8 @@
 // (the token that crosses top_p is kept); one token is drawn from the
 // renormalised candidates.  T <= 0 is greedy argmax.
 //
-// One 1024-thread workgroup per row, no sort:
+// (Rows without top-k / top-p take decode.hip's vocabulary-split kernel instead, same draws;
+// mxllm/ops/decode.py sample_rows routes them.)  Here: one 1024-thread workgroup per row, no sort:
 //  * logits map to order-preserving 32-bit keys (bf16 -> its exact f32);
 //  * the k-th largest key and then the top-p boundary key are found by a
 //    radix select, 11 + 11 + 10 bits, over LDS histograms: counts for top-k,
