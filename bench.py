@@ -92,6 +92,20 @@ def parse(argv=None):
     ap.add_argument("--config4-warmup", type=int, default=2)
     ap.add_argument("--config4-timeout", type=float, default=360.0,
                     help="hard limit for the config-4 child job; the headline line is printed either way")
+    # per-rank HBM the config-4 child needs: the emulated world-8 peak with the first 56 of 80 layers
+    # checkpointed (239 GB reserved, profiles/r2s3_emul8_ck56.json) + RCCL buffers / in-flight units
+    ap.add_argument("--config4-need-gb", type=float, default=255.0)
+    ap.add_argument("--config2", choices=["auto", "on", "off"], default="auto",
+                    help="also measure BASELINE config 2 (Llama-3.1-8B FULL fine-tune, DDP) in-process after "
+                         "the headline; auto = when the headline runs on 1 GPU")
+    ap.add_argument("--config3", choices=["auto", "on", "off"], default="auto",
+                    help="also measure BASELINE config 3 (Llama-3.1-8B FULL fine-tune, DDP over all N GPUs) "
+                         "in-process after the headline; auto = when the headline runs on 8 GPUs")
+    ap.add_argument("--full-model", default="llama3.1-8b", help=argparse.SUPPRESS)  # tests: tiny models
+    ap.add_argument("--full-steps", type=int, default=10)
+    ap.add_argument("--full-warmup", type=int, default=3)
+    ap.add_argument("--grad-dtype", choices=["auto", "bf16", "fp32"], default="auto",
+                    help="gradient accumulation / reduction dtype; auto = fp32 for zero3, bf16 otherwise")
     return ap.parse_args(argv)
 
 
@@ -164,25 +178,78 @@ def main(argv=None):
     os.environ.setdefault("MXLLM_XGMI", "0")
     env = runtime.init()
     out = run(a, env)
-    c4 = a.config4 == "on" or (a.config4 == "auto" and env.world_size == 8 and a.model == "llama3.1-70b"
-                               and a.finetune == "lora" and a.parallel == "ddp" and env.device.type == "cuda")
+    cuda = env.device.type == "cuda"
+    headline = a.model == "llama3.1-70b" and a.finetune == "lora" and a.parallel == "ddp" and not a.layers
+    c2 = a.config2 == "on" or (a.config2 == "auto" and env.world_size == 1 and headline and cuda)
+    c3 = a.config3 == "on" or (a.config3 == "auto" and env.world_size == 8 and headline and cuda)
+    if (c2 and env.world_size == 1) or (c3 and env.world_size > 1):
+        key = "config2_8b_full" if env.world_size == 1 else f"config3_8b_full_dp{env.world_size}"
+        out[key] = run_full(a, env)
+    c4 = a.config4 == "on" or (a.config4 == "auto" and env.world_size == 8 and headline and cuda)
     if not c4:
         if env.is_main:
             emit(out, a.json_out)
         runtime.cleanup()
         return 0
     # BASELINE config 4 in a fresh job: this job's ranks free the GPUs (non-zero
-    # ranks exit; the launcher waits for rank 0), local rank 0 runs the child
+    # ranks exit; the launcher waits for rank 0), local rank 0 runs the child.
+    # Every rank first reports the HBM it can hand over; too little -> skipped with the reason
+    _free_gpu_memory(env)
+    free_gb = _min_free_gb(env)
     runtime.cleanup()
+    if env.is_main:
+        if free_gb is not None and free_gb < a.config4_need_gb:
+            out["config4_full_zero3"] = {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < "
+                                                    f"{a.config4_need_gb:.0f} GB the config-4 child needs"}
+        else:
+            out["config4_full_zero3"] = run_config4(a, env.world_size)
+        emit(out, a.json_out)
+    return 0
+
+
+def _free_gpu_memory(env):
     import gc
 
     gc.collect()
     if env.device.type == "cuda":
+        torch.cuda.synchronize(env.device)
         torch.cuda.empty_cache()
-    if env.is_main:
-        out["config4_full_zero3"] = run_config4(a, env.world_size)
-        emit(out, a.json_out)
-    return 0
+
+
+def _min_free_gb(env) -> float | None:
+    """Smallest free HBM over the ranks (GB) after this job released its caches."""
+    from mxllm.parallel import runtime
+
+    if env.device.type != "cuda":
+        return None
+    free = torch.cuda.mem_get_info(env.device)[0] / 1e9
+    return runtime.all_reduce_scalars([free], op="min")[0]
+
+
+def run_full(a, env) -> dict:
+    """BASELINE config 2 (1 GPU) / config 3 (N GPUs): Llama-3.1-8B FULL-parameter
+    fine-tune with plain DDP, in this process after the headline (whose model and
+    caches are released first).  Same timing contract as the headline.  A failure
+    is recorded in the returned dict; the headline line is printed either way."""
+    import copy
+
+    _free_gpu_memory(env)
+    b = copy.copy(a)
+    b.model, b.finetune, b.parallel = a.full_model, "full", "ddp"
+    b.steps, b.warmup, b.layers = a.full_steps, a.full_warmup, None
+    b.act_ckpt, b.act_ckpt_layers, b.sp, b.cp, b.emulate_world = False, None, 1, 1, 0
+    b.grad_accum = 1
+    try:
+        res = run(b, env)
+    except Exception as e:  # noqa: BLE001  (e.g. out of memory): report, keep the headline
+        res = {"error": f"{type(e).__name__}: {e}"[:500]}
+    _free_gpu_memory(env)
+    res.pop("vs_baseline", None)
+    cfg = b.model
+    res["metric"] = f"fine-tune tokens/sec (whole node) {PRETTY.get(cfg, cfg)} FULL-parameter DDP"
+    res["label"] = (f"BASELINE config {2 if env.world_size == 1 else 3}: {PRETTY.get(cfg, cfg)} full-parameter "
+                    f"fine-tune, DDP over {env.world_size} GPU(s), measured in-process after the headline")
+    return res
 
 
 def emit(out: dict, json_out: str | None):
@@ -232,7 +299,8 @@ def run_config4(a, world: int) -> dict:
         with contextlib.suppress(OSError):
             os.remove(path)
     res.pop("vs_baseline", None)
-    res["label"] = ("BASELINE config 4: Llama-3.1-70B FULL-parameter fine-tune, ZeRO-3 sharded over "
+    name = PRETTY.get(a.config4_model, a.config4_model)
+    res["label"] = (f"BASELINE config 4: {name} FULL-parameter fine-tune, ZeRO-3 sharded over "
                     f"{world} GPUs, activation checkpointing, measured after the headline in a separate job")
     return res
 
@@ -257,6 +325,8 @@ def run(a, env) -> dict:
     opt = OptimConfig(lr=1e-4, weight_decay=0.0, grad_clip=1.0)
     emulated = 0
     ckpt = a.act_ckpt if (not a.act_ckpt or a.act_ckpt_layers is None) else a.act_ckpt_layers
+    gd = a.grad_dtype if a.grad_dtype != "auto" else ("fp32" if a.parallel == "zero3" else "bf16")
+    gdt = torch.float32 if gd == "fp32" else None
     if a.parallel == "zero3":
         if a.finetune != "full":
             raise SystemExit("--parallel zero3 requires --finetune full")
@@ -267,12 +337,13 @@ def run(a, env) -> dict:
                 raise SystemExit("--emulate-world is a single-process proxy")
             emulated = a.emulate_world
         trainer = Zero3Trainer(cfg, env, opt, seed=1234, activation_checkpointing=ckpt,
-                               emulate_world=emulated)
+                               emulate_world=emulated, grad_dtype=gdt)
         model = trainer.model
     else:
         model = Llama(cfg, device=dev, dtype=torch.bfloat16, lora_r=lora_r, lora_alpha=a.lora_alpha, seed=1234,
                       activation_checkpointing=ckpt)
-        trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb, shard_optimizer=a.parallel == "zero1")
+        trainer = Trainer(model, env, opt, bucket_mb=a.bucket_mb, shard_optimizer=a.parallel == "zero1",
+                          grad_dtype=gdt)
     sp_group, data_rank, shard_fn = None, env.rank, None
     if a.sp > 1 and a.cp > 1:
         raise SystemExit("--sp and --cp are alternatives")
@@ -367,7 +438,10 @@ def run(a, env) -> dict:
             "grad_accum": a.grad_accum,
             "activation_checkpointing": (a.act_ckpt if a.act_ckpt_layers is None or not a.act_ckpt
                                          else f"first {a.act_ckpt_layers} of {cfg.n_layers} layers"),
-            "optimizer": "fused AdamW (HIP), grad clip 1.0",
+            "optimizer": "fused AdamW (HIP), grad clip 1.0" + (
+                ", per-layer updates overlapped with the next forward" if getattr(trainer, "overlap_optimizer", False)
+                else ""),
+            "grad_reduce_dtype": gd,
             "gemm": "hipBLASLt/rocBLAS" + (" (tuned solution table)" if tuned else ""),
         },
         "tokens_per_sec_per_gpu": round(tps / env.world_size, 2),

@@ -33,10 +33,7 @@ def _export_hf(argv) -> int:
     model = build_model(a.base, device="cpu", dtype=torch.bfloat16, lora_r=a.lora_r, lora_alpha=a.lora_alpha,
                         seed=a.seed)
     if a.weights:
-        path = a.weights
-        if os.path.isdir(path) and os.path.exists(os.path.join(path, "model.safetensors")):
-            path = os.path.join(path, "model.safetensors")
-        load_model_weights(model, path)
+        load_model_weights(model, a.weights)  # step dir (DDP / ZeRO-1 / ZeRO-3) or .safetensors
     files = save_hf_llama(model, a.out, max_shard_bytes=int(a.max_shard_gb * (1 << 30)))
     print(json.dumps({"out": a.out, "files": [os.path.basename(f) for f in files]}))
     return 0

@@ -11,7 +11,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from ..parallel.grad_ready import deliver_grad
+from ..parallel.grad_ready import accum_grad, deliver_grad
 from ._ext import native, use_native
 
 
@@ -31,15 +31,18 @@ class _EmbeddingFn(torch.autograd.Function):
         if not ctx.needs_input_grad[1]:
             return None, None
         if ctx.nat:
-            dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab).to(ctx.wdtype)
+            dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab)  # f32 accumulator
         else:
             dy2 = dy.reshape(-1, dy.shape[-1])
             dw = torch.zeros(ctx.vocab, dy2.shape[1], dtype=torch.float32, device=dy.device)
             dw.index_add_(0, ids.reshape(-1), dy2.float())
-            dw = dw.to(ctx.wdtype)
-        if deliver_grad(ctx.wp, dw):
+        # fp32 gradient owners take the f32 sums as they are (no bf16 rounding)
+        if accum_grad(ctx.wp, dw):
             return None, None
-        return None, dw
+        sink32 = getattr(ctx.wp, "_mx_grad_sink_dtype", None) == torch.float32
+        if deliver_grad(ctx.wp, dw if sink32 else dw.to(ctx.wdtype)):
+            return None, None
+        return None, dw.to(ctx.wdtype)
 
 
 def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:

@@ -31,7 +31,7 @@ from typing import Sequence
 import torch
 import torch.nn.functional as F
 
-from ..parallel.grad_ready import direct_grad, mark_ready
+from ..parallel.grad_ready import direct_grad, direct_grad32, mark_ready
 from ._ext import native, use_native
 
 
@@ -248,14 +248,21 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, be
     runs in the reduction-contiguous form the forward uses: dW = dyT @ xT^T,
     12-20 % faster including the transposes
     (bench/dw_layout_probe.py, profiles/r1e_dw_layout_probe.md)."""
+    f32 = out is not None and out.dtype == torch.float32 and dy.dtype != torch.float32
     if _DW_TN and use_native(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
         xt = transpose2d(x)
         dyt = transpose2d(dy)
         if out is None:
             return torch.mm(dyt, xt.t())
+        if f32:  # bf16 operands, fp32 accumulate-into output (hipBLASLt D = C in fp32)
+            return torch.ops.aten.addmm.dtype_out(out, dyt, xt.t(), torch.float32, beta=beta, out=out)
         return out.addmm_(dyt, xt.t(), beta=beta)
     if out is None:
         return torch.mm(dy.t(), x)
+    if f32:
+        if dy.is_cuda:
+            return torch.ops.aten.addmm.dtype_out(out, dy.t(), x, torch.float32, beta=beta, out=out)
+        return out.addmm_(dy.t().float(), x.float(), beta=beta)
     return out.addmm_(dy.t(), x, beta=beta)
 
 
@@ -263,12 +270,15 @@ def param_weight_grad(wp: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor
     """Weight gradient of parameter ``wp`` for a backward pass.
 
     When an owner pre-attached ``wp.grad`` (the trainer's flat grad buffer, or a
-    ZeRO-3 unit's gathered-gradient buffer) the dW GEMM writes straight into it —
+    ZeRO-3 unit's gathered-gradient buffer) — or an fp32 target ``wp._mx_grad32``
+    (fp32 gradient accumulation) — the dW GEMM writes straight into it —
     accumulating (beta 1), or overwriting (beta 0) when the owner flagged the
     buffer ``_mx_grad_fresh`` so it need not be zero-filled first — the owner is
     notified via ``mark_ready`` and None is returned.  Otherwise the dW tensor
     is returned for autograd to accumulate."""
     g = direct_grad(wp) if wp is not None else None
+    if g is None and wp is not None:
+        g = direct_grad32(wp)  # fp32 gradient accumulation: the GEMM writes fp32
     if g is None:
         return weight_grad_(None, dy, x)
     fresh = getattr(wp, "_mx_grad_fresh", False)

@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import reference as ref
+from ..parallel.grad_ready import accum_grad
 from ._ext import native, rows_view, use_native
 
 # ``out_pad`` / ``grad_pad``: the normalised output (forward) or the input
@@ -23,13 +24,25 @@ class _RMSNormFn(torch.autograd.Function):
     def forward(ctx, x, w, eps, out_pad):
         y, rstd, _ = native().rmsnorm_fwd(x, None, w, eps, out_pad)
         ctx.save_for_backward(x, w, rstd)
+        ctx.wp = w if w.is_leaf else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, rstd = ctx.saved_tensors
         dx, dw = native().rmsnorm_bwd(dy.contiguous(), x, w, rstd, None, ctx.needs_input_grad[1])
-        return dx, (dw.to(w.dtype) if ctx.needs_input_grad[1] else None), None, None
+        return dx, _wgrad(ctx, dw, w, 1), None, None
+
+
+def _wgrad(ctx, dw, w, idx: int):
+    """dγ (fp32 from the kernel; ``idx``: w's input position): added straight into
+    an fp32 gradient target when the owner keeps one (no bf16 rounding), else
+    handed to autograd as w.dtype."""
+    if dw is None or not ctx.needs_input_grad[idx]:
+        return None
+    if accum_grad(ctx.wp, dw):
+        return None
+    return dw.to(w.dtype)
 
 
 class _AddRMSNormFn(torch.autograd.Function):
@@ -39,6 +52,7 @@ class _AddRMSNormFn(torch.autograd.Function):
     def forward(ctx, x, res, w, eps, out_pad, grad_pad):
         y, rstd, h = native().rmsnorm_fwd(x, res, w, eps, out_pad)
         ctx.save_for_backward(h, w, rstd)
+        ctx.wp = w if w.is_leaf else None
         ctx.grad_pad = grad_pad
         return y, h
 
@@ -49,7 +63,7 @@ class _AddRMSNormFn(torch.autograd.Function):
             dy = torch.zeros_like(h)
         dres = rows_view(dh) if dh is not None else None
         dx, dw = native().rmsnorm_bwd(dy.contiguous(), h, w, rstd, dres, ctx.needs_input_grad[2], ctx.grad_pad)
-        return dx, dx, (dw.to(w.dtype) if ctx.needs_input_grad[2] else None), None, None, None
+        return dx, dx, _wgrad(ctx, dw, w, 2), None, None, None
 
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5, out_pad: int = 0) -> torch.Tensor:

@@ -34,7 +34,8 @@ class FlatParams:
 
     ``param_dtype``: storage of the live parameters the model computes with.
     ``master``: fp32 copy (created when param_dtype != fp32).
-    ``grad_dtype``: dtype of the flat grad buffer (defaults to param dtype).
+    ``grad_dtype``: dtype of the flat grad buffer (defaults to param dtype);
+    float32 with bf16 parameters = fp32 gradient accumulation and reduction.
     """
 
     def __init__(self, named_params: list[tuple[str, torch.nn.Parameter]], grad_dtype: torch.dtype | None = None,
@@ -65,12 +66,33 @@ class FlatParams:
                 p.data = view
                 self._plist.append(p)
         self.master = self.params if pdt == torch.float32 else self.params.float()
+        # fp32 gradients of low-precision parameters (autograd cannot hold them in
+        # ``.grad``): ops add into ``p._mx_grad32`` (grad_ready.accum_grad / the
+        # fp32-output dW GEMMs), anything autograd accumulates in ``.grad`` is folded
+        # in by a hook that runs before every other post-accumulate hook (DDP's)
+        self.grad32 = self.grad_dtype == torch.float32 and pdt != torch.float32
+        if self.grad32:
+            for p in self._plist:
+                p.register_post_accumulate_grad_hook(self._fold_hook)
         self.attach_grads()
 
+    def _view(self, k: int, buf: torch.Tensor) -> torch.Tensor:
+        s = self.slots[k]
+        return buf[s.offset:s.offset + s.numel].view(s.shape)
+
+    def _fold_hook(self, p):
+        if p.grad is not None:
+            p._mx_grad32.add_(p.grad)
+            p.grad = None
+
     def attach_grads(self):
-        """Point every ``p.grad`` at its slice of the flat grad buffer."""
-        for p, s in zip(self._plist, self.slots):
-            g = self.grads[s.offset:s.offset + s.numel].view(s.shape)
+        """Point every ``p.grad`` (fp32 mode: ``p._mx_grad32``) at its slice of
+        the flat grad buffer."""
+        for k, p in enumerate(self._plist):
+            g = self._view(k, self.grads)
+            if self.grad32:
+                p._mx_grad32 = g
+                continue
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g if self.grad_dtype == p.dtype else None
         return self
@@ -84,10 +106,14 @@ class FlatParams:
         self.attach_grads()
 
     def sync_grads_from_params(self):
-        """If autograd replaced a .grad (dtype mismatch / detached), copy it back."""
+        """If autograd replaced a .grad (dtype mismatch / detached), copy it back
+        (fp32 mode: fold any ``.grad`` left behind into the fp32 buffer)."""
         for p, s in zip(self._plist, self.slots):
             g = p.grad
             if g is None:
+                continue
+            if self.grad32:
+                self._fold_hook(p)
                 continue
             flat = self.grads[s.offset:s.offset + s.numel]
             if g.data_ptr() != flat.data_ptr():
@@ -96,3 +122,26 @@ class FlatParams:
 
     def state_dict(self):
         return {"slots": [(s.name, s.offset, s.numel, list(s.shape)) for s in self.slots], "numel": self.numel}
+
+
+def production_order(model, named: list) -> list:
+    """Trainable parameters in gradient-PRODUCTION order (the flat-buffer layout):
+    the model's forward parameter groups (``Llama._wait_groups``: embedding, each
+    layer + the norm it applies next, head) reversed, each group reversed — the LM
+    head's gradient comes first in backward, the embedding's last.  DDP buckets then
+    fill front to back during backward (the head's 1 GB bucket no longer waits for
+    the embedding), and every forward group is one contiguous range (the
+    per-layer optimizer chunks).  Parameters outside the groups keep registration
+    order (reversed) at the end."""
+    groups_fn = getattr(model, "_wait_groups", None)
+    if groups_fn is None:
+        return list(reversed(named))
+    want = {id(p): (n, p) for n, p in named}
+    taken, chunks = set(), []
+    for g in groups_fn():
+        c = [want[id(p)] for p in g if id(p) in want and id(p) not in taken]
+        taken.update(id(p) for _, p in c)
+        chunks.append(c)
+    out = [e for c in reversed(chunks) for e in reversed(c)]
+    out += [e for e in reversed(named) if id(e[1]) not in taken]
+    return out

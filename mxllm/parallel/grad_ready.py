@@ -22,6 +22,32 @@ def direct_grad(p):
     return None
 
 
+def direct_grad32(p):
+    """The fp32 gradient target of ``p`` when its owner accumulates gradients in
+    fp32 (``FlatParams(grad_dtype=float32)``, ZeRO-3 fp32 units): ops that form a
+    parameter gradient themselves (dW GEMMs with an fp32 output, the RMSNorm dγ and
+    embedding kernels' fp32 partials) add into it without an intermediate bf16
+    rounding.  None otherwise."""
+    if getattr(p, "_mx_no_direct", False):
+        return None
+    return getattr(p, "_mx_grad32", None)
+
+
+def accum_grad(p, g) -> bool:
+    """Add a computed gradient ``g`` (any float dtype) into ``p``'s fp32 target and
+    notify the owner; False when ``p`` has no fp32 target (return ``g`` to autograd)."""
+    t = direct_grad32(p) if p is not None else None
+    if t is None:
+        return False
+    if getattr(p, "_mx_grad_fresh", False):
+        t.copy_(g.reshape(t.shape))
+        p._mx_grad_fresh = False
+    else:
+        t.add_(g.reshape(t.shape))
+    mark_ready(p)
+    return True
+
+
 def deliver_grad(p, g) -> bool:
     """Hand a freshly computed full gradient ``g`` of ``p`` to its owner instead
     of autograd (ZeRO-3 sets ``p._mx_grad_sink`` on parameters whose storage is

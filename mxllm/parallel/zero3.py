@@ -197,10 +197,17 @@ class Unit:
         self.n_trainable = len(self.params)
         self.device = None
         self.dtype = None
+        self.gdt = None  # gradient dtype (reduce-scatter / accumulation): fp32 or bf16
+        # world 1 (not emulated): the shard IS the full unit — no gather copy, and
+        # with fp32 gradients the dW GEMMs write straight into the fp32 grad shard
+        self.local = world == 1 and not comm.emulate
 
     # -------------------------------------------------------------- gather / release
     def gather(self, async_op: bool = True):
         if self.full is not None:
+            return
+        if self.local:
+            self.full = self.shard
             return
         self.full = torch.empty(self.full_numel, dtype=self.dtype, device=self.device)
         self.work = self.comm.all_gather(self.full, self.shard, async_op)
@@ -225,56 +232,88 @@ class Unit:
         self.full = None
 
     # -------------------------------------------------------------- gradients
-    def attach_grads(self):
-        """Point every parameter's .grad at its slice of a fresh gathered-size
-        gradient buffer; the dW GEMMs overwrite it (``_mx_grad_fresh``), so only
-        the alignment pad is zeroed.  Parameters whose gradient comes from
-        autograd (embedding, tied weights) are copied in at reduce time."""
+    @property
+    def grad32(self) -> bool:
+        return self.gdt == torch.float32
+
+    def direct(self) -> bool:
+        """Gradients land in ``grad_shard`` itself: world 1 with fp32 gradients."""
+        return self.local and self.grad32
+
+    def attach_grads(self, first: bool = True):
+        """Point every parameter's gradient target (``.grad``, or ``_mx_grad32``
+        for fp32 gradients) at its slice of a gathered-size gradient buffer.  The
+        dW GEMMs overwrite it (``_mx_grad_fresh``), so only the alignment pad is
+        zeroed.  World 1 with fp32 gradients: the buffer IS the fp32 grad shard
+        (overwritten on the first micro-batch, accumulated on later ones).
+        Parameters whose gradient comes from autograd (embedding, tied weights)
+        are copied in at reduce time.  ``first``: first micro-batch of the step."""
         if self.gbuf is not None:
             return
         # GPU: every projection/head gradient comes from param_weight_grad, which
         # honours the fresh flag; the CPU reference ops accumulate through autograd
         fresh = ops.use_native(self.shard)
-        if fresh:
-            self.gbuf = torch.empty(self.full_numel, dtype=self.dtype, device=self.device)
+        if self.direct():
+            self.gbuf = self.grad_shard  # zero past the parameters (AdamW clears it every step)
+            fresh = fresh and first
+        elif fresh:
+            self.gbuf = torch.empty(self.full_numel, dtype=self.gdt, device=self.device)
             if self.full_numel > self.numel:
                 self.gbuf[self.numel:].zero_()
         else:
-            self.gbuf = torch.zeros(self.full_numel, dtype=self.dtype, device=self.device)
+            self.gbuf = torch.zeros(self.full_numel, dtype=self.gdt, device=self.device)
         for p, o, n, s in zip(self.params, self.offsets, self.numels, self.shapes):
             if getattr(p, "_mx_no_direct", False) or p.shape != s:
                 continue
-            p.grad = self.gbuf[o:o + n].view(s)
+            if self.grad32:
+                p._mx_grad32 = self.gbuf[o:o + n].view(s)
+            else:
+                p.grad = self.gbuf[o:o + n].view(s)
             p._mx_grad_fresh = fresh
 
-    def reduce_async(self):
+    def reduce_async(self, first: bool = True):
         """Launch the reduce-scatter of the unit's gradient buffer; returns
-        (work | None, bf16 shard) to be folded into ``grad_shard`` later."""
+        (work | None, shard | None, fold).  ``fold``: the shard must still be added
+        into ``grad_shard`` (bf16 gradients, or a later micro-batch); fp32 on the
+        first micro-batch reduce-scatters straight into ``grad_shard``, and world 1
+        with fp32 gradients has nothing to reduce (the GEMMs wrote ``grad_shard``)."""
         if self.gbuf is None:
             g0 = self.params[0].grad if len(self.params) == 1 else None
             if (g0 is not None and g0.is_contiguous() and g0.numel() == self.full_numel
-                    and g0.dtype == self.dtype):
+                    and g0.dtype == self.gdt):
                 self.gbuf = g0.view(-1)  # autograd's own gradient tensor, no copy (e.g. the embedding)
+            elif self.direct():
+                self.gbuf = self.grad_shard
             else:
-                self.gbuf = torch.zeros(self.full_numel, dtype=self.dtype, device=self.device)
+                self.gbuf = torch.zeros(self.full_numel, dtype=self.gdt, device=self.device)
+        direct = self.gbuf is self.grad_shard
         for p, o, n in zip(self.params, self.offsets, self.numels):
             g = p.grad
             dst = self.gbuf[o:o + n]
+            fresh = getattr(p, "_mx_grad_fresh", False)
             if g is None:
-                if getattr(p, "_mx_grad_fresh", False):
+                if fresh:
                     dst.zero_()  # attached but never written (parameter unused this step)
             elif g.data_ptr() != dst.data_ptr():
-                dst.copy_(g.reshape(-1))
-            elif getattr(p, "_mx_grad_fresh", False):
+                if direct and not fresh:
+                    dst.add_(g.reshape(-1))  # grad_shard accumulates across micro-batches
+                else:
+                    dst.copy_(g.reshape(-1))
+            elif fresh:
                 dst.zero_()
             p.grad = None
             p._mx_grad_fresh = False
-        out = torch.empty(self.shard_numel, dtype=self.dtype, device=self.device)
-        work = self.comm.reduce_scatter(out, self.gbuf, async_op=True)
-        self.gbuf = None  # RCCL keeps the buffer alive until the collective is done
+            p._mx_grad32 = None
         self.seen.clear()
         self.reduced = True
-        return work, out
+        if direct:
+            self.gbuf = None
+            return None, None, False
+        into = first and self.grad32
+        out = self.grad_shard if into else torch.empty(self.shard_numel, dtype=self.gdt, device=self.device)
+        work = self.comm.reduce_scatter(out, self.gbuf, async_op=True)
+        self.gbuf = None  # RCCL keeps the buffer alive until the collective is done
+        return work, (None if into else out), not into
 
 
 class _PreBackward(torch.autograd.Function):
@@ -330,7 +369,11 @@ class Zero3Trainer:
 
     def __init__(self, cfg, env: DistEnv, optim=None, *, seed: int = 0, activation_checkpointing: bool | int = False,
                  process_group=None, emulate_world: int = 0, max_inflight: int | None = None,
-                 init_from: str | None = None):
+                 init_from: str | None = None, grad_dtype: torch.dtype | None = torch.float32):
+        """``grad_dtype``: dtype the unit gradients are formed, reduce-scattered and
+        accumulated in — fp32 by default (no bf16 rounding at any ring hop; the dW
+        GEMMs write fp32 output), ``torch.bfloat16`` halves the reduce-scatter
+        bytes.  ``None`` = fp32."""
         from ..models.llama import Llama
         from ..train.trainer import OptimConfig
 
@@ -359,8 +402,9 @@ class Zero3Trainer:
         units = unit_layout(model)
         self.units = [Unit(k, ps, self.world, self.rank, comm, res) for k, (_, ps, res) in enumerate(units)]
         self.unit_names = [u[0] for u in units]
+        self.grad_dtype = grad_dtype or torch.float32
         for u in self.units:
-            u.device, u.dtype = dev, torch.bfloat16
+            u.device, u.dtype, u.gdt = dev, torch.bfloat16, self.grad_dtype
         total = sum(u.shard_numel for u in self.units)
         self.shard_params = torch.empty(total, dtype=torch.bfloat16, device=dev)
         self.master = torch.empty(total, dtype=torch.float32, device=dev)
@@ -385,7 +429,9 @@ class Zero3Trainer:
                 p._mx_on_grad_ready = self._grad_hook  # dW written by the GEMM itself (param_weight_grad)
                 if not u.resident and len(u.params) == 1 and not getattr(p, "_mx_no_direct", False):
                     p._mx_grad_sink = self._sink  # e.g. the embedding: its unit is not gathered in backward
+                    p._mx_grad_sink_dtype = self.grad_dtype
         self._inflight: deque = deque()
+        self._first = True  # first micro-batch of the step (fp32: reduce-scatter straight into grad_shard)
         self.step_num = 0
         self.last_grad_norm = None
         self._units_by_layer = {i: self.units[2 + i] for i in range(len(model.layers))}
@@ -434,18 +480,23 @@ class Zero3Trainer:
     def _sink(self, p, g):
         """A full gradient delivered by its op (grad_ready.deliver_grad)."""
         u = self._param_unit[id(p)]
-        if u.gbuf is None and g.is_contiguous() and g.numel() == u.full_numel:
+        if u.gbuf is None and g.is_contiguous() and g.numel() == u.full_numel and g.dtype == u.gdt:
             u.gbuf = g.view(-1)
         else:
             if u.gbuf is None:
-                u.gbuf = torch.zeros(u.full_numel, dtype=u.dtype, device=u.device)
+                u.gbuf = (u.grad_shard if u.direct()
+                          else torch.zeros(u.full_numel, dtype=u.gdt, device=u.device))
             k = u.params.index(p)
-            u.gbuf[u.offsets[k]:u.offsets[k] + u.numels[k]].copy_(g.reshape(-1))
+            dst = u.gbuf[u.offsets[k]:u.offsets[k] + u.numels[k]]
+            if u.gbuf is u.grad_shard and not self._first:
+                dst.add_(g.reshape(-1))
+            else:
+                dst.copy_(g.reshape(-1))
         self._grad_hook(p)
 
     def _reduce(self, u: Unit):
-        work, out = u.reduce_async()
-        self._inflight.append((u, work, out))
+        work, out, fold = u.reduce_async(self._first)
+        self._inflight.append((u, work, out if fold else None))
         self._done(u)
         while len(self._inflight) > self.max_inflight:
             self._drain_one()
@@ -454,7 +505,8 @@ class Zero3Trainer:
         u, work, out = self._inflight.popleft()
         if work is not None:
             work.wait()  # the compute stream waits for the RCCL stream; the host does not
-        u.grad_shard.add_(out)  # fp32 += bf16 (AdamW zeroes the shard every step)
+        if out is not None:
+            u.grad_shard.add_(out)  # fp32 += shard (AdamW zeroes the shard every step)
 
     def _drain(self):
         while self._inflight:
@@ -468,7 +520,7 @@ class Zero3Trainer:
         if nxt is not None and nxt.full is None:
             self._gather(nxt)
         u.materialize()
-        u.attach_grads()
+        u.attach_grads(self._first)
 
     def _pack(self, t):
         if t.device.type == "meta" or not isinstance(t, torch.Tensor):
@@ -494,7 +546,8 @@ class Zero3Trainer:
 
     def _gather(self, u: Unit, async_op=True):
         u.gather(async_op=async_op)
-        self._by_storage[u.full.untyped_storage().data_ptr()] = u
+        if not u.local:  # world 1: the "gathered" unit is the persistent shard, nothing to release
+            self._by_storage[u.full.untyped_storage().data_ptr()] = u
 
     def _use(self, u: Unit, prefetch: Unit | None = None):
         if u.full is None:
@@ -506,7 +559,7 @@ class Zero3Trainer:
     def _done(self, u: Unit):
         if u.resident:
             return
-        if u.full is not None:
+        if u.full is not None and not u.local:
             self._by_storage.pop(u.full.untyped_storage().data_ptr(), None)
         u.release()
 
@@ -547,21 +600,26 @@ class Zero3Trainer:
     def train_step(self, micro_batches):
         n = len(micro_batches)
         total = None
-        for ids, labels in micro_batches:
+        norms = self.units[0]  # resident unit: gradients accumulate over the micro-batches, one reduce per step
+        for k, (ids, labels) in enumerate(micro_batches):
+            self._first = k == 0
+            if k == 0 and norms.grad32:
+                norms.attach_grads(True)  # the RMSNorm kernels add their fp32 dγ into it
             loss = self._forward(ids, labels)
             loss.backward()  # 1/n folded into the optimizer's grad scale
             for u in self.units[1:]:  # units whose hooks did not all fire (unused params)
-                if not u.reduced and (u.seen or any(p.grad is not None for p in u.params)):
+                if not u.reduced and (u.seen or u.gbuf is not None or any(p.grad is not None for p in u.params)):
                     self._reduce(u)
                 elif u.full is not None:
                     self._done(u)
             total = loss.detach() if total is None else total + loss.detach()
         self._drain()
-        norms = self.units[0]  # resident unit: one (small) reduce-scatter per step
-        work, out = norms.reduce_async()
+        self._first = True
+        work, out, fold = norms.reduce_async(True)
         if work is not None:
             work.wait()
-        norms.grad_shard.add_(out)
+        if fold:
+            norms.grad_shard.add_(out)
         scale = 1.0 / (self.world * n)
         self.step_num += 1
         o = self.opt
@@ -592,12 +650,20 @@ class Zero3Trainer:
         return {"step": self.step_num, "master": self.master, "m": self.m, "v": self.v}
 
     def load_state_dict(self, sd):
-        self.step_num = int(sd["step"])
         self.master.copy_(sd["master"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
+        self.finish_load(int(sd["step"]))
+
+    def finish_load(self, step: int):
+        """After master/m/v were written in place (checkpoint.load, which reshards
+        unit by unit): set the step, rebuild the bf16 shards and the resident unit."""
+        self.step_num = int(step)
         self.shard_params.copy_(self.master)
         self._refresh_resident()
+
+    def params_ready(self):
+        """API parity with Trainer: nothing is in flight between steps."""
 
     def full_master_state(self) -> dict:
         """Every fp32 master weight, gathered unit by unit (collective: all ranks

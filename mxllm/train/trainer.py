@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from dataclasses import dataclass
 
@@ -16,7 +17,7 @@ import torch
 
 from .. import ops
 from ..parallel.ddp import DDP
-from ..parallel.flat import FlatParams
+from ..parallel.flat import FlatParams, production_order
 from ..parallel.runtime import DistEnv
 from ..utils.profiling import range_
 
@@ -43,29 +44,45 @@ class OptimConfig:
         return self.lr
 
 
+def _overlap_default() -> bool:
+    return os.environ.get("MXLLM_OVERLAP_ADAMW", "1") != "0"
+
+
 class Trainer:
     def __init__(self, model: torch.nn.Module, env: DistEnv, optim: OptimConfig | None = None, *,
                  bucket_mb: float = 128.0, first_bucket_mb: float = 16.0, broadcast_init: bool = False,
-                 shard_optimizer: bool = False):
+                 shard_optimizer: bool = False, overlap_optimizer: bool | None = None,
+                 grad_dtype: torch.dtype | str | None = None):
         """``shard_optimizer``: ZeRO-1 (mxllm/parallel/zero1.py) — gradients are
         reduce-scattered, each rank updates its 1/N slice, parameters are
-        all-gathered back.  At world 1 it is plain DDP (nothing to shard)."""
+        all-gathered back.  At world 1 it is plain DDP (nothing to shard).
+
+        ``overlap_optimizer`` (None = auto: GPU, full fine-tuning, DDP): the fused
+        AdamW is issued per forward parameter group on a side stream at the end of
+        the step and the NEXT forward waits per layer (see ``_launch_overlapped``).
+
+        ``grad_dtype``: dtype of the flat gradient buffer = the dtype gradients are
+        ACCUMULATED (micro-batches) and ALL-REDUCED in.  ``torch.float32``: fp32
+        accumulation and fp32 ring reduction (the dW GEMMs write fp32 output);
+        default: the parameter dtype (bf16)."""
         self.model = model
         self.env = env
         self.opt = optim or OptimConfig()
-        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        named = production_order(model, [(n, p) for n, p in model.named_parameters() if p.requires_grad])
         world = env.world_size
         self.zero1 = None
+        if isinstance(grad_dtype, str):
+            grad_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": None, "bfloat16": None}[grad_dtype]
         if shard_optimizer and world > 1:
             from ..parallel.zero1 import Zero1
 
-            self.flat = FlatParams(named, align=64 * world)
+            self.flat = FlatParams(named, align=64 * world, grad_dtype=grad_dtype, reverse=False)
             self.ddp = self.zero1 = Zero1(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
             self._master = self.zero1.master
             if getattr(model, "param_wait", "absent") is None:
                 model.param_wait = self.zero1.wait_params  # per-layer wait in the next forward
         else:
-            self.flat = FlatParams(named)
+            self.flat = FlatParams(named, grad_dtype=grad_dtype, reverse=False)
             self.ddp = DDP(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
             self._master = self.flat.master
         if broadcast_init:
@@ -75,14 +92,125 @@ class Trainer:
         self.v = torch.zeros_like(self._master)
         self.step_num = 0
         self.last_grad_norm: torch.Tensor | None = None
+        # ---- optimizer / next-forward overlap
+        self._chunks: list[tuple[int, int]] | None = None
+        self._pending: list = []
+        self._hold = None
+        if overlap_optimizer is None:
+            overlap_optimizer = (_overlap_default() and self.flat.device.type == "cuda" and self.zero1 is None
+                                 and not getattr(model, "lora", False))
+        if overlap_optimizer and self.zero1 is None and getattr(model, "param_wait", "absent") is None:
+            self._chunks = self._forward_chunks()
+            if self._chunks is not None:
+                self._side = torch.cuda.Stream(self.flat.device) if self.flat.device.type == "cuda" else None
+                model.param_wait = self._param_wait
+        self.overlap_optimizer = self._chunks is not None
 
     @property
     def lowp(self):
         return None if self.flat.master is self.flat.params else self.flat.params
 
+    @property
+    def grad_dtype(self) -> torch.dtype:
+        return self.flat.grad_dtype
+
+    # ------------------------------------------------------------------ overlap
+    def _forward_chunks(self) -> list[tuple[int, int]] | None:
+        """Flat-buffer ranges of the model's forward parameter groups
+        (``Llama._wait_groups``: embedding, each layer + the next norm, head), in
+        forward order.  The flat buffer is laid out group by group
+        (``flat.production_order``), so every group is ONE contiguous range; None if
+        that does not hold (the optimizer then runs as one launch)."""
+        groups_fn = getattr(self.model, "_wait_groups", None)
+        if groups_fn is None:
+            return None
+        slots = self.flat.slots
+        order = sorted(range(len(slots)), key=lambda k: slots[k].offset)
+        extent = {}
+        for j, k in enumerate(order):  # a slot owns its alignment pad up to the next slot
+            end = slots[order[j + 1]].offset if j + 1 < len(order) else self.flat.numel
+            extent[k] = (slots[k].offset, end)
+        slot_of = {id(p): k for k, p in enumerate(self.flat.param_list)}
+        chunks, self._group_chunk = [], {}
+        covered = 0
+        taken: set[int] = set()  # a parameter shared by two groups belongs to the first one that uses it
+        for g in groups_fn():
+            ks = sorted({slot_of[id(p)] for p in g if id(p) in slot_of} - taken, key=lambda k: extent[k][0])
+            if not ks:
+                continue
+            taken.update(ks)
+            lo, hi = extent[ks[0]][0], extent[ks[-1]][1]
+            if sum(extent[k][1] - extent[k][0] for k in ks) != hi - lo:
+                return None  # another group's slot inside the range
+            self._group_chunk[id(g)] = len(chunks)
+            chunks.append((lo, hi))
+            covered += hi - lo
+        if covered != self.flat.numel or len(chunks) < 2:
+            return None
+        return chunks
+
+    def _param_wait(self, group):
+        """``Llama.param_wait``: the compute stream waits for the update of the
+        chunk holding ``group`` (no host synchronisation)."""
+        k = self._group_chunk.get(id(group))
+        if k is None or k >= len(self._pending):
+            return
+        ev = self._pending[k]
+        if ev is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(ev)
+            self._pending[k] = None
+
+    def params_ready(self):
+        """Order the current stream after every in-flight parameter update
+        (overlapped AdamW chunks, ZeRO-1 all-gathers): call before reading
+        parameters outside a forward (checksums, checkpoints, export)."""
+        if self.zero1 is not None:
+            self.zero1.wait_params()
+        for k, ev in enumerate(self._pending):
+            if ev is not None:
+                torch.cuda.current_stream(self.flat.device).wait_event(ev)
+                self._pending[k] = None
+
+    def _launch_overlapped(self, gscale, **kw):
+        """The fused AdamW over each forward chunk on the side stream, in forward
+        order, with one event per chunk.  The NEXT forward waits for chunk i just
+        before layer i, so the update of the layers it has not reached yet runs
+        under its GEMMs (the update is still fully issued inside this step).
+        Elementwise kernel over the same slices with the same inputs: bitwise
+        identical to the one-launch update."""
+        lowp = self.lowp
+        side = self._side
+        if side is None:  # CPU: same chunked update, in order (tests)
+            for lo, hi in self._chunks:
+                ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
+                                None if lowp is None else lowp[lo:hi], grad_scale=gscale, zero_grad=True, **kw)
+            return
+        side.wait_stream(torch.cuda.current_stream(self.flat.device))
+        self._hold = gscale  # read on the side stream: keep it alive until the next step
+        if len(self._pending) != len(self._chunks):
+            self._pending = [None] * len(self._chunks)
+        with torch.cuda.stream(side):
+            for k, (lo, hi) in enumerate(self._chunks):
+                ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
+                                None if lowp is None else lowp[lo:hi], grad_scale=gscale, zero_grad=True, **kw)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self._pending[k] = ev
+
     def train_step(self, micro_batches: list[tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """One optimizer step over ``micro_batches`` [(ids, labels), ...].
         Returns the mean loss as a device tensor (no host sync)."""
+        total, scale = self.compute_grads(micro_batches)
+        self.step_num += 1
+        with range_("optimizer"):
+            self._optimizer_step(scale)
+        return total / len(micro_batches)
+
+    def compute_grads(self, micro_batches: list[tuple[torch.Tensor, torch.Tensor]]):
+        """Forward + backward of every micro-batch (gradients accumulated in the
+        flat buffer, reduced across ranks by the DDP buckets).  Returns (sum of
+        the micro-batch losses, scale that turns the flat gradient into the mean
+        gradient) — the flat buffer holds the SUM over ranks and micro-batches."""
         n = len(micro_batches)
         self.model.train()
         if self.zero1 is not None and getattr(self.model, "param_wait", None) is None:
@@ -100,10 +228,7 @@ class Trainer:
         self.flat.sync_grads_from_params()
         with range_("grad_allreduce_wait"):
             scale = self.ddp.finish() / n if n > 1 else self.ddp.finish()
-        self.step_num += 1
-        with range_("optimizer"):
-            self._optimizer_step(scale)
-        return total / n
+        return total, scale
 
     def _optimizer_step(self, scale: float):
         o = self.opt
@@ -131,6 +256,9 @@ class Trainer:
             z.gather_params()  # async, forward order; the next forward waits per layer
             if getattr(self.model, "sync_adapters_", None) is not None and getattr(self.model, "lora", False):
                 z.wait_params()
+        elif self._chunks is not None:
+            self._launch_overlapped(gscale, lr=o.lr_at(self.step_num), beta1=o.beta1, beta2=o.beta2, eps=o.eps,
+                                    weight_decay=o.weight_decay, step=self.step_num)
         else:
             ops.adamw_step_(self.flat.master, grads, self.m, self.v, self.lowp, lr=o.lr_at(self.step_num),
                             beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
@@ -151,14 +279,21 @@ class Trainer:
         return self.zero1 is not None
 
     def state_dict(self) -> dict:
+        self.params_ready()
         return {"step": self.step_num, "master": self._master, "m": self.m, "v": self.v,
                 "layout": self.flat.state_dict()}
 
     def load_state_dict(self, sd: dict):
-        self.step_num = int(sd["step"])
+        self.params_ready()
         self._master.copy_(sd["master"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
+        self.finish_load(int(sd["step"]))
+
+    def finish_load(self, step: int):
+        """After master/m/v were written in place (checkpoint.load): set the step
+        and rebuild the compute-dtype parameters from the fp32 master."""
+        self.step_num = int(step)
         z = self.zero1
         if z is not None:
             if z.master is not z.pshard:

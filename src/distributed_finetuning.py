@@ -81,6 +81,7 @@ def export_hf(run, trainer, rank):
     ZeRO-3 gathers unit by unit to rank 0).  Collective for ZeRO-3 / ZeRO-1."""
     from mxllm.models import save_hf_llama
 
+    trainer.params_ready()  # overlapped optimizer chunks / ZeRO-1 all-gathers have landed
     if run.parallel == "zero3":
         state = trainer.full_state_dict()
         if rank == 0:
@@ -185,10 +186,10 @@ def main(argv=None):
                 metrics.write(step=step, epoch=epoch, loss=lv, grad_norm=gn, tokens_per_s=tps, **extra)
                 t_last, n_since = time.perf_counter(), 0
             if sync_check and run.check_sync_every > 0 and (step + 1) % run.check_sync_every == 0:
+                trainer.params_ready()  # else the checksum may read half-updated parameters
                 check_in_sync(trainer.flat.params, what=f"trainable parameters after step {step}")
             if run.ckpt_dir and run.save_every and (step + 1) % run.save_every == 0:
-                checkpoint.save(run.ckpt_dir, trainer, step + 1, extra={"loader": loader.state()},
-                                sharded=run.parallel in ("zero3", "zero1"))
+                checkpoint.save(run.ckpt_dir, trainer, step + 1, extra={"loader": loader.state()})
         loader.close()
         if monitor is not None:
             monitor.stop()

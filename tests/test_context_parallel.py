@@ -79,11 +79,12 @@ def test_ring_attention_matches_full_sequence(world):
         assert p.exitcode == 0
 
     from mxllm.models import Llama
-    from mxllm.parallel.flat import FlatParams
+    from mxllm.parallel.flat import FlatParams, production_order
 
     cfg = _cfg()
     model = Llama(cfg, lora_r=0, seed=3).float()
-    flat = FlatParams([(n, p) for n, p in model.named_parameters() if p.requires_grad])
+    flat = FlatParams(production_order(model, [(n, p) for n, p in model.named_parameters() if p.requires_grad]),
+                      reverse=False)  # the Trainer's layout
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(0, cfg.vocab_size, (2, 64), generator=g)
     lab = torch.randint(0, cfg.vocab_size, (2, 64), generator=g)

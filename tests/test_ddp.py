@@ -63,7 +63,7 @@ def _worker(rank, world, port, out_q, full, bucket_mb, accum):
 def _single_grads(world, full, accum):
     os.environ["MXLLM_FORCE_CPU"] = "1"
     from mxllm.models import Llama, get_config
-    from mxllm.parallel.flat import FlatParams
+    from mxllm.parallel.flat import FlatParams, production_order
 
     cfg = get_config("tiny").replace(n_layers=2, vocab_size=300)
     model = Llama(cfg, lora_r=0 if full else 4, seed=3)
@@ -74,7 +74,8 @@ def _single_grads(world, full, accum):
                     for blk in mod.lora_b_blocks():
                         blk.normal_(0, 0.02, generator=torch.Generator().manual_seed(i))
         model.sync_adapters_()
-    flat = FlatParams([(n, p) for n, p in model.named_parameters() if p.requires_grad])
+    flat = FlatParams(production_order(model, [(n, p) for n, p in model.named_parameters() if p.requires_grad]),
+                      reverse=False)  # the Trainer's layout
     g = torch.Generator().manual_seed(11)
     ids = torch.randint(0, cfg.vocab_size, (world * 2 * accum, 32), generator=g)
     # per-rank mean over micro-batches, then mean over ranks == mean over equal chunks

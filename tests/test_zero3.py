@@ -31,13 +31,16 @@ def _run(rank, world, port, q, mode, steps):
     from mxllm.train.trainer import OptimConfig, Trainer
 
     env = runtime.init(rank=rank, world_size=world)
+    # "..._bf16": bf16 gradient reduction in both trainers (default: fp32 in both)
+    gdt = torch.bfloat16 if mode.endswith("_bf16") else torch.float32
+    mode = mode.removesuffix("_bf16")
     cfg = get_config("tiny").replace(n_layers=3, vocab_size=320)
     opt = OptimConfig(lr=3e-3, grad_clip=1.0, weight_decay=0.01)
     if mode.startswith("zero3"):
         # "zero3_ckpt" = every layer checkpointed, "zero3_ckpt2" = the first 2 of 3 (selective)
         ck = mode.split("_ckpt")[1] if "_ckpt" in mode else None
         tr = Zero3Trainer(cfg, env, opt, seed=7, activation_checkpointing=(int(ck) if ck else True) if ck is not None
-                          else False)
+                          else False, grad_dtype=gdt)
     else:  # replicated DDP from the identical per-unit seeded init
         from mxllm.parallel.zero3 import init_full_state
 
@@ -46,7 +49,7 @@ def _run(rank, world, port, q, mode, steps):
         with torch.no_grad():
             for n, p in model.named_parameters():
                 p.copy_(sd[n])
-        tr = Trainer(model, env, opt)
+        tr = Trainer(model, env, opt, grad_dtype=gdt)
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(0, cfg.vocab_size, (world * 2, 24), generator=g)
     losses = []
@@ -87,13 +90,15 @@ def _launch(mode, world, steps=3):
     return res
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
-def test_zero3_matches_ddp_per_parameter(world):
-    ddp_loss, ddp_w = _launch("ddp", world)
+@pytest.mark.parametrize("world,gd", [(1, ""), (2, ""), (4, ""), (2, "_bf16")])
+def test_zero3_matches_ddp_per_parameter(world, gd):
+    ddp_loss, ddp_w = _launch("ddp" + gd, world)
     modes = {1: ["zero3", "zero3_ckpt", "zero3_ckpt2"], 2: ["zero3", "zero3_ckpt2"]}.get(world, ["zero3", "zero3_ckpt"])
+    if gd:
+        modes = ["zero3"]
     got = {}
     for mode in modes:
-        z_loss, z_w = _launch(mode, world)
+        z_loss, z_w = _launch(mode + gd, world)
         got[mode] = z_w
         assert ddp_loss[-1] < ddp_loss[0]  # it trains
         for x, y in zip(ddp_loss, z_loss):
@@ -101,8 +106,7 @@ def test_zero3_matches_ddp_per_parameter(world):
         assert set(ddp_w) == set(z_w)
         for n, w in ddp_w.items():
             # 3 AdamW steps of lr 3e-3 move a weight by up to ~1e-2; the replicas may differ
-            # only by bf16 gradient summation order (all-reduce vs reduce-scatter)
-            # only by bf16 gradient summation order (all-reduce vs reduce-scatter): an element
+            # only by gradient summation order (all-reduce vs reduce-scatter): an element
             # whose summed gradient is ~0 can flip sign, moving by up to 2 lr per step
             d = abs(w - z_w[n])
             if world == 1:
