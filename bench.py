@@ -214,6 +214,7 @@ def _free_gpu_memory(env):
     if env.device.type == "cuda":
         torch.cuda.synchronize(env.device)
         torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(env.device)  # the next run's peak_hbm_gb is its own
 
 
 def _min_free_gb(env) -> float | None:

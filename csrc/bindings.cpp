@@ -218,32 +218,67 @@ at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu, int64_t out_pa
 }
 
 // ---------------------------------------------------------------- AdamW
-void adamw_step(at::Tensor master, at::Tensor grad, at::Tensor m, at::Tensor v,
-                const c10::optional<at::Tensor>& lowp, double lr, double b1, double b2, double eps, double wd,
-                double bc1, double bc2, const c10::optional<at::Tensor>& scale_t, double scale_f,
-                bool zero_grad) {
-  check_f32(master, "master");
+void adamw_step(const c10::optional<at::Tensor>& master, at::Tensor grad, at::Tensor m, at::Tensor v,
+                const c10::optional<at::Tensor>& lowp, const c10::optional<at::Tensor>& lo, double lr, double b1,
+                double b2, double eps, double wd, double bc1, double bc2, const c10::optional<at::Tensor>& scale_t,
+                double scale_f, bool zero_grad) {
+  // master: fp32, or absent with ``lo`` given (split master: lowp = high half, lo = int16 low half)
+  MX_CHECK(master.has_value() != lo.has_value(), "give either the fp32 master or the split low half");
   check_f32(m, "m");
   check_f32(v, "v");
   MX_CHECK(grad.is_cuda() && grad.is_contiguous(), "grad must be contiguous GPU");
   MX_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16, "grad f32/bf16");
-  const int64_t n = master.numel();
-  MX_CHECK(grad.numel() == n && m.numel() == n && v.numel() == n, "adamw size mismatch");
-  DevGuard g(master.device());
+  const int64_t n = m.numel();
+  MX_CHECK(grad.numel() == n && v.numel() == n, "adamw size mismatch");
+  float* mp = nullptr;
+  if (master.has_value()) {
+    check_f32(*master, "master");
+    MX_CHECK(master->numel() == n, "master size");
+    mp = master->data_ptr<float>();
+  }
+  DevGuard g(m.device());
   uint16_t* lp = nullptr;
   if (lowp.has_value()) {
     check_bf16(*lowp, "lowp");
     MX_CHECK(lowp->numel() == n, "lowp size");
     lp = reinterpret_cast<uint16_t*>(lowp->data_ptr());
   }
+  int16_t* lop = nullptr;
+  if (lo.has_value()) {
+    MX_CHECK(lo->is_cuda() && lo->is_contiguous() && lo->scalar_type() == at::kShort && lo->numel() == n,
+             "lo must be a contiguous int16 GPU tensor of the master's size");
+    MX_CHECK(lp != nullptr, "split master needs lowp (the high half)");
+    lop = lo->data_ptr<int16_t>();
+  }
   const float* st = nullptr;
   if (scale_t.has_value()) {
     check_f32(*scale_t, "scale_t");
     st = scale_t->data_ptr<float>();
   }
-  MX_OK(mx_adamw(master.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kBFloat16 ? 1 : 0,
-                 m.data_ptr<float>(), v.data_ptr<float>(), lp, n, (float)lr, (float)b1, (float)b2, (float)eps,
-                 (float)wd, (float)bc1, (float)bc2, st, (float)scale_f, zero_grad ? 1 : 0, cur_stream()));
+  MX_OK(mx_adamw(mp, grad.data_ptr(), grad.scalar_type() == at::kBFloat16 ? 1 : 0, m.data_ptr<float>(),
+                 v.data_ptr<float>(), lp, lop, n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
+                 (float)bc2, st, (float)scale_f, zero_grad ? 1 : 0, cur_stream()));
+}
+
+// fp32 <-> split master halves (hi bf16 = bits rounded half-up, lo int16 = remainder)
+void split_master(const at::Tensor& x, at::Tensor hi, at::Tensor lo) {
+  check_f32(x, "x");
+  check_bf16(hi, "hi");
+  MX_CHECK(lo.is_cuda() && lo.is_contiguous() && lo.scalar_type() == at::kShort, "lo int16 contiguous GPU");
+  MX_CHECK(hi.numel() == x.numel() && lo.numel() == x.numel(), "split_master size mismatch");
+  DevGuard g(x.device());
+  MX_OK(mx_split_master(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(hi.data_ptr()), lo.data_ptr<int16_t>(),
+                        x.numel(), cur_stream()));
+}
+
+void join_master(const at::Tensor& hi, const at::Tensor& lo, at::Tensor out) {
+  check_bf16(hi, "hi");
+  check_f32(out, "out");
+  MX_CHECK(lo.is_cuda() && lo.is_contiguous() && lo.scalar_type() == at::kShort, "lo int16 contiguous GPU");
+  MX_CHECK(hi.numel() == out.numel() && lo.numel() == out.numel(), "join_master size mismatch");
+  DevGuard g(out.device());
+  MX_OK(mx_join_master(reinterpret_cast<const uint16_t*>(hi.data_ptr()), lo.data_ptr<int16_t>(),
+                       out.data_ptr<float>(), out.numel(), cur_stream()));
 }
 
 // ---------------------------------------------------------------- embedding
@@ -463,9 +498,11 @@ at::Tensor sample(const at::Tensor& logits, double temperature, int64_t seed, in
   MX_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16/f32");
   DevGuard g(logits.device());
   auto out = at::empty({logits.size(0)}, logits.options().dtype(at::kLong));
+  auto ws = at::empty({std::max<int64_t>(1, mx_sample_ws_floats((int)logits.size(0)))},
+                      logits.options().dtype(at::kFloat));  // per-call partials (stream-ordered allocator)
   MX_OK(mx_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16 ? 1 : 0, out.data_ptr<int64_t>(),
                   (int)logits.size(0), (int)logits.size(1), (float)temperature, (uint32_t)seed, (uint32_t)step,
-                  cur_stream()));
+                  ws.data_ptr<float>(), cur_stream()));
   return out;
 }
 
@@ -484,9 +521,11 @@ at::Tensor sample_temp_rows(const at::Tensor& logits, const at::Tensor& temps, c
   chk(steps, at::kInt, "steps i32 [B]");
   DevGuard g(logits.device());
   auto out = at::empty({B}, logits.options().dtype(at::kLong));
+  auto ws = at::empty({std::max<int64_t>(1, mx_sample_ws_floats((int)B))}, logits.options().dtype(at::kFloat));
   MX_OK(mx_sample_temp_rows(logits.data_ptr(), logits.scalar_type() == at::kBFloat16 ? 1 : 0,
                             out.data_ptr<int64_t>(), (int)B, (int)logits.size(1), temps.data_ptr<float>(),
-                            seeds.data_ptr<int64_t>(), steps.data_ptr<int32_t>(), cur_stream()));
+                            seeds.data_ptr<int64_t>(), steps.data_ptr<int32_t>(), ws.data_ptr<float>(),
+                            cur_stream()));
   return out;
 }
 
@@ -739,7 +778,9 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
-  m.def("adamw_step(Tensor(a!) master, Tensor(e!) grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f, bool zero_grad=False) -> ()");
+  m.def("adamw_step(Tensor(a!)? master, Tensor(e!) grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, Tensor(f!)? lo, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f, bool zero_grad=False) -> ()");
+  m.def("split_master(Tensor x, Tensor(a!) hi, Tensor(b!) lo) -> ()");
+  m.def("join_master(Tensor hi, Tensor lo, Tensor(a!) out) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor w) -> Tensor");
   m.def("embedding_bwd(Tensor dy, Tensor ids, int V) -> Tensor");
   m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
@@ -774,6 +815,8 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("adamw_step", &adamw_step);
+  m.impl("split_master", &split_master);
+  m.impl("join_master", &join_master);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("ce_fwd_bwd", &ce_fwd_bwd);

@@ -27,9 +27,11 @@ extern "C" {
 int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream);
 int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
                   hipStream_t stream);
-int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
-             float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t, float scale_f,
-             int zero_grad, hipStream_t stream);
+int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int16_t* lo, int64_t n,
+             float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t,
+             float scale_f, int zero_grad, hipStream_t stream);
+int mx_split_master(const float* x, uint16_t* hi, int16_t* lo, int64_t n, hipStream_t stream);
+int mx_join_master(const uint16_t* hi, const int16_t* lo, float* x, int64_t n, hipStream_t stream);
 int mx_embedding_fwd(const int64_t* ids, const uint16_t* w, uint16_t* out, int64_t T, int H, int64_t V,
                      hipStream_t stream);
 int mx_embedding_bwd(const int64_t* ids, const uint16_t* dy, float* dw, int64_t T, int H, int64_t V,
@@ -60,10 +62,11 @@ int mx_rope_append(const uint16_t* qkv, const float* cosb, const float* sinb, co
 int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens, int len_off,
                    const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B, int Hq, int Hkv, int D,
                    int max_seq, int nsplit, float scale, hipStream_t stream);
+int64_t mx_sample_ws_floats(int B);
 int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature, uint32_t seed,
-              uint32_t step, hipStream_t stream);
+              uint32_t step, float* ws, hipStream_t stream);
 int mx_sample_temp_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, const float* temps,
-                        const int64_t* seeds, const int32_t* steps, hipStream_t stream);
+                        const int64_t* seeds, const int32_t* steps, float* ws, hipStream_t stream);
 // sampling.hip
 int mx_sample_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, const float* temps,
                    const float* top_ps, const int32_t* top_ks, const int64_t* seeds, const int32_t* steps,

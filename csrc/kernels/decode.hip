@@ -422,11 +422,11 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 // step; split over ~63 workgroups it is a few microseconds.  (A last-arriver
 // merge in the same kernel needed an agent-scope release fence per workgroup:
 // 94 us at batch 64.)  The result (and the Gumbel noise of each (seed, row,
-// step, index)) is the same as a single-pass argmax.
+// step, index)) is the same as a single-pass argmax.  The partials live in a
+// per-call workspace (allocated by the caller on its stream), so concurrent
+// samplers on different streams of one device never share them.
 constexpr int kSampMaxRows = 1024;   // rows per launch (more rows: several launches)
 constexpr int kSampMaxChunks = 64;   // partials per row (= one wave in the final pass)
-__device__ float g_samp_val[kSampMaxRows * kSampMaxChunks];
-__device__ int g_samp_idx[kSampMaxRows * kSampMaxChunks];
 
 __device__ __forceinline__ void samp_pick(float& best, int& bi, float ov, int oi) {
   if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
@@ -437,7 +437,8 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
                                                      int chunk, float inv_temp, uint32_t seed, uint32_t step,
                                                      int row0, const float* __restrict__ temps,
                                                      const int64_t* __restrict__ seeds,
-                                                     const int32_t* __restrict__ steps) {
+                                                     const int32_t* __restrict__ steps,
+                                                     float* __restrict__ g_samp_val, int* __restrict__ g_samp_idx) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int lrow = blockIdx.y;
@@ -486,7 +487,9 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
 }
 
 // partials of one row (chunk order) -> out[row]; grid rows, one wave
-__global__ void __launch_bounds__(64) sample_final_kernel(int64_t* __restrict__ out, int nch, int row0) {
+__global__ void __launch_bounds__(64) sample_final_kernel(int64_t* __restrict__ out, int nch, int row0,
+                                                          const float* __restrict__ g_samp_val,
+                                                          const int* __restrict__ g_samp_idx) {
   const int lrow = blockIdx.x, l = threadIdx.x;
   float best = -INFINITY;
   int bi = 0x7fffffff;
@@ -537,11 +540,18 @@ extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint1
   return (int)hipGetLastError();
 }
 
+// ws: float workspace of mx_sample_ws_floats(B) elements
+extern "C" int64_t mx_sample_ws_floats(int B) {
+  return 2 * (int64_t)std::min(B, kSampMaxRows) * kSampMaxChunks;
+}
+
 static int sample_launch(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
                          uint32_t seed, uint32_t step, const float* temps, const int64_t* seeds,
-                         const int32_t* steps, hipStream_t stream) {
+                         const int32_t* steps, float* ws, hipStream_t stream) {
   if (B <= 0) return 0;
-  if (V <= 0) return -1;
+  if (V <= 0 || !ws) return -1;
+  float* pv = ws;
+  int* pi = reinterpret_cast<int*>(ws + (int64_t)std::min(B, kSampMaxRows) * kSampMaxChunks);
   const float it = temperature > 0.f ? 1.f / temperature : 0.f;
   int chunk = 2048, nch = (V + chunk - 1) / chunk;
   if (nch > kSampMaxChunks) {
@@ -552,23 +562,23 @@ static int sample_launch(const void* logits, int is_bf16, int64_t* out, int B, i
     const dim3 grid(nch, std::min(kSampMaxRows, B - r0));
     if (is_bf16)
       sample_kernel<uint16_t><<<grid, 256, 0, stream>>>((const uint16_t*)logits, out, V, chunk, it, seed, step, r0,
-                                                         temps, seeds, steps);
+                                                         temps, seeds, steps, pv, pi);
     else
       sample_kernel<float><<<grid, 256, 0, stream>>>((const float*)logits, out, V, chunk, it, seed, step, r0, temps,
-                                                      seeds, steps);
-    sample_final_kernel<<<grid.y, 64, 0, stream>>>(out, nch, r0);
+                                                      seeds, steps, pv, pi);
+    sample_final_kernel<<<grid.y, 64, 0, stream>>>(out, nch, r0, pv, pi);
   }
   return (int)hipGetLastError();
 }
 
 extern "C" int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature,
-                         uint32_t seed, uint32_t step, hipStream_t stream) {
-  return sample_launch(logits, is_bf16, out, B, V, temperature, seed, step, nullptr, nullptr, nullptr, stream);
+                         uint32_t seed, uint32_t step, float* ws, hipStream_t stream) {
+  return sample_launch(logits, is_bf16, out, B, V, temperature, seed, step, nullptr, nullptr, nullptr, ws, stream);
 }
 
 // per-row temperature (<= 0: greedy), seed and step, no top-k / top-p: the draws of
 // sampling.hip's sample_topkp_kernel for such rows (same noise), split over the vocabulary
 extern "C" int mx_sample_temp_rows(const void* logits, int is_bf16, int64_t* out, int B, int V, const float* temps,
-                                   const int64_t* seeds, const int32_t* steps, hipStream_t stream) {
-  return sample_launch(logits, is_bf16, out, B, V, 0.f, 0u, 0u, temps, seeds, steps, stream);
+                                   const int64_t* seeds, const int32_t* steps, float* ws, hipStream_t stream) {
+  return sample_launch(logits, is_bf16, out, B, V, 0.f, 0u, 0u, temps, seeds, steps, ws, stream);
 }

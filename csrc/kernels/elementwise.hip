@@ -4,6 +4,8 @@
 //   * token-embedding gather / f32-atomic scatter-add
 // Every kernel moves 16 B per lane per access (G13), grid-strides with
 // <= 2048 workgroups x 256 threads (G11).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mx {
@@ -59,10 +61,25 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
 // Fused AdamW, 4 elements per lane per iteration (n % 4 == 0).  ZERO: the gradient
 // is cleared in the same pass (the next backward accumulates into it with beta=1),
 // so no separate memset re-streams the gradient buffer.
-template <bool GRAD_BF16, bool LOWP, bool ZERO>
+// SPLIT: the fp32 master is stored as two 16-bit halves — ``lowp`` (the bf16 compute
+// weight, the master rounded half-up on its bit pattern) and ``lo`` = master bits -
+// (lowp << 16) in [-32768, 32767] — reconstructed exactly in registers.  Same
+// optimizer arithmetic as the fp32 master, 2 B/param less state and HBM traffic
+// (the separate bf16 copy IS the master's high half).
+__device__ __forceinline__ float split_join(uint16_t h, int16_t l) {
+  return __uint_as_float(((uint32_t)h << 16) + (uint32_t)(int32_t)l);
+}
+__device__ __forceinline__ void split_make(float x, uint16_t& h, int16_t& l) {
+  const uint32_t b = __float_as_uint(x);
+  h = (uint16_t)((b + 0x8000u) >> 16);
+  l = (int16_t)(int32_t)(b - ((uint32_t)h << 16));
+}
+
+template <bool GRAD_BF16, bool LOWP, bool ZERO, bool SPLIT>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, void* __restrict__ gv,
                                                     float* __restrict__ m, float* __restrict__ v,
-                                                    uint16_t* __restrict__ lowp, int64_t n, float lr, float b1,
+                                                    uint16_t* __restrict__ lowp, int16_t* __restrict__ lo,
+                                                    int64_t n, float lr, float b1,
                                                     float b2, float eps, float wd, float inv_bc1, float inv_bc2,
                                                     const float* __restrict__ scale_t, float scale_f) {
   const float gs = scale_f * (scale_t ? scale_t[0] : 1.f);
@@ -78,10 +95,20 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, void*
       g = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(gv) + i);
       if constexpr (ZERO) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(gv) + i) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    f32x4 pp = *reinterpret_cast<f32x4*>(p + i);
+    f32x4 pp;
+    u16x4 hh;
+    s16x4 ll;
+    if constexpr (SPLIT) {
+      hh = *reinterpret_cast<const u16x4*>(lowp + i);
+      ll = *reinterpret_cast<const s16x4*>(lo + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pp[j] = split_join(hh[j], ll[j]);
+    } else {
+      pp = *reinterpret_cast<f32x4*>(p + i);
+    }
     f32x4 mm = *reinterpret_cast<f32x4*>(m + i);
     f32x4 vv = *reinterpret_cast<f32x4*>(v + i);
-    u16x4 lo;
+    u16x4 lw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float gj = g[j] * gs;
@@ -89,13 +116,45 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, void*
       vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
       const float den = sqrtf(vv[j] * inv_bc2) + eps;
       pp[j] = pp[j] * decay - step * mm[j] / den;
-      if constexpr (LOWP) lo[j] = f2bf(pp[j]);
+      if constexpr (SPLIT) {
+        uint16_t h;
+        int16_t l;
+        split_make(pp[j], h, l);
+        hh[j] = h;
+        ll[j] = l;
+      } else if constexpr (LOWP) {
+        lw[j] = f2bf(pp[j]);
+      }
     }
-    *reinterpret_cast<f32x4*>(p + i) = pp;
+    if constexpr (SPLIT) {
+      *reinterpret_cast<u16x4*>(lowp + i) = hh;
+      *reinterpret_cast<s16x4*>(lo + i) = ll;
+    } else {
+      *reinterpret_cast<f32x4*>(p + i) = pp;
+      if constexpr (LOWP) *reinterpret_cast<u16x4*>(lowp + i) = lw;
+    }
     *reinterpret_cast<f32x4*>(m + i) = mm;
     *reinterpret_cast<f32x4*>(v + i) = vv;
-    if constexpr (LOWP) *reinterpret_cast<u16x4*>(lowp + i) = lo;
   }
+}
+
+// fp32 master <-> (hi, lo) halves, element-wise (checkpoint load/save, init)
+__global__ void __launch_bounds__(256) split_master_kernel(const float* __restrict__ x, uint16_t* __restrict__ hi,
+                                                           int16_t* __restrict__ lo, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint16_t h;
+    int16_t l;
+    split_make(x[i], h, l);
+    hi[i] = h;
+    lo[i] = l;
+  }
+}
+
+__global__ void __launch_bounds__(256) join_master_kernel(const uint16_t* __restrict__ hi,
+                                                          const int16_t* __restrict__ lo, float* __restrict__ x,
+                                                          int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    x[i] = split_join(hi[i], lo[i]);
 }
 
 // out[t, :] = W[ids[t], :]  — one 256-thread block per token row
@@ -150,24 +209,51 @@ extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* d
   return (int)hipGetLastError();
 }
 
-extern "C" int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int64_t n, float lr,
-                        float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t,
+static int adamw_grid_cap() {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("MXLLM_ADAMW_GRID");  // experiments: fewer workgroups beside concurrent GEMMs
+    cap = e ? atoi(e) : 2048;
+    if (cap < 1) cap = 2048;
+  }
+  return cap;
+}
+
+// lo != nullptr: SPLIT master (p unused, lowp = the high half, required)
+extern "C" int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int16_t* lo, int64_t n,
+                        float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t,
                         float scale_f, int zero_grad, hipStream_t stream) {
   if (n % 4) return -1;
-  const int grid = grid_for(n / 4);
+  if (lo && !lowp) return -1;
+  int grid = grid_for(n / 4);
+  if (grid > adamw_grid_cap()) grid = adamw_grid_cap();
   const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
-#define ADAM_LAUNCH(GB, LP, Z)                                                                          \
-  adamw_kernel<GB, LP, Z><<<grid, 256, 0, stream>>>(p, g, m, v, lowp, n, lr, b1, b2, eps, wd, ib1, ib2, \
-                                                    scale_t, scale_f)
-#define ADAM_Z(GB, LP) \
-  do { if (zero_grad) ADAM_LAUNCH(GB, LP, true); else ADAM_LAUNCH(GB, LP, false); } while (0)
-  if (grad_bf16) {
-    if (lowp) ADAM_Z(true, true); else ADAM_Z(true, false);
+#define ADAM_LAUNCH(GB, LP, Z, SP)                                                                            \
+  adamw_kernel<GB, LP, Z, SP><<<grid, 256, 0, stream>>>(p, g, m, v, lowp, lo, n, lr, b1, b2, eps, wd, ib1, ib2, \
+                                                        scale_t, scale_f)
+#define ADAM_Z(GB, LP, SP) \
+  do { if (zero_grad) ADAM_LAUNCH(GB, LP, true, SP); else ADAM_LAUNCH(GB, LP, false, SP); } while (0)
+  if (lo) {
+    if (grad_bf16) ADAM_Z(true, true, true); else ADAM_Z(false, true, true);
+  } else if (grad_bf16) {
+    if (lowp) ADAM_Z(true, true, false); else ADAM_Z(true, false, false);
   } else {
-    if (lowp) ADAM_Z(false, true); else ADAM_Z(false, false);
+    if (lowp) ADAM_Z(false, true, false); else ADAM_Z(false, false, false);
   }
 #undef ADAM_Z
 #undef ADAM_LAUNCH
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_split_master(const float* x, uint16_t* hi, int16_t* lo, int64_t n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  split_master_kernel<<<grid_for(n), 256, 0, stream>>>(x, hi, lo, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_join_master(const uint16_t* hi, const int16_t* lo, float* x, int64_t n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  join_master_kernel<<<grid_for(n), 256, 0, stream>>>(hi, lo, x, n);
   return (int)hipGetLastError();
 }
 

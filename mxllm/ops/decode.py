@@ -80,8 +80,16 @@ def sample_rows(logits: torch.Tensor, temps, top_ps, top_ks, seeds, steps) -> to
     greedy.  GPU: ONE launch for the whole batch (csrc/kernels/sampling.hip:
     radix-select thresholds + Gumbel-max over the kept set, keyed by
     (seed, step, token) so a request's draws do not depend on batching).
-    CPU: ``filter_probs`` + torch.multinomial."""
+    CPU: ``filter_probs`` + torch.multinomial.  ``top_p <= 0`` (an empty nucleus)
+    is the limit of a vanishing nucleus: that row is sampled greedily on both paths;
+    a NaN top_p / temperature is rejected."""
     B = logits.shape[0]
+    temps, top_ps = list(temps), list(top_ps)
+    for i, (t, p) in enumerate(zip(temps, top_ps)):
+        if p != p or t != t:
+            raise ValueError(f"row {i}: top_p={p}, temperature={t} (NaN)")
+        if p <= 0:
+            temps[i], top_ps[i] = 0.0, 1.0
     if use_native(logits):
         ops = native()
         x = logits if logits.dtype in (torch.bfloat16, torch.float32) else logits.float()

@@ -36,10 +36,12 @@ class FlatParams:
     ``master``: fp32 copy (created when param_dtype != fp32).
     ``grad_dtype``: dtype of the flat grad buffer (defaults to param dtype);
     float32 with bf16 parameters = fp32 gradient accumulation and reduction.
+    ``split_master``: the fp32 master is a :class:`mxllm.ops.SplitMaster` over
+    ``params`` (exact fp32 values, 2 B/param less state and optimizer traffic).
     """
 
     def __init__(self, named_params: list[tuple[str, torch.nn.Parameter]], grad_dtype: torch.dtype | None = None,
-                 reverse: bool = True, align: int = ALIGN):
+                 reverse: bool = True, align: int = ALIGN, split_master: bool = False):
         if not named_params:
             raise ValueError("no trainable parameters")
         order = list(reversed(named_params)) if reverse else list(named_params)
@@ -65,7 +67,14 @@ class FlatParams:
                 view.copy_(p.data)
                 p.data = view
                 self._plist.append(p)
-        self.master = self.params if pdt == torch.float32 else self.params.float()
+        if pdt == torch.float32:
+            self.master = self.params
+        elif split_master:  # fp32 master = (params, int16 low halves): no separate bf16 copy
+            from ..ops.optim import SplitMaster
+
+            self.master = SplitMaster(self.params)
+        else:
+            self.master = self.params.float()
         # fp32 gradients of low-precision parameters (autograd cannot hold them in
         # ``.grad``): ops add into ``p._mx_grad32`` (grad_ready.accum_grad / the
         # fp32-output dW GEMMs), anything autograd accumulates in ``.grad`` is folded
@@ -82,8 +91,20 @@ class FlatParams:
 
     def _fold_hook(self, p):
         if p.grad is not None:
-            p._mx_grad32.add_(p.grad)
+            if getattr(p, "_mx_grad_fresh", False):
+                p._mx_grad32.copy_(p.grad)
+                p._mx_grad_fresh = False
+            else:
+                p._mx_grad32.add_(p.grad)
             p.grad = None
+
+    def zero_unwritten_(self):
+        """Zero the slots of parameters still flagged ``_mx_grad_fresh`` after a
+        backward (no op wrote their gradient: unused this step)."""
+        for k, p in enumerate(self._plist):
+            if getattr(p, "_mx_grad_fresh", False):
+                self._view(k, self.grads).zero_()
+                p._mx_grad_fresh = False
 
     def attach_grads(self):
         """Point every ``p.grad`` (fp32 mode: ``p._mx_grad32``) at its slice of

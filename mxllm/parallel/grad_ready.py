@@ -34,9 +34,16 @@ def direct_grad32(p):
 
 
 def accum_grad(p, g) -> bool:
-    """Add a computed gradient ``g`` (any float dtype) into ``p``'s fp32 target and
-    notify the owner; False when ``p`` has no fp32 target (return ``g`` to autograd)."""
-    t = direct_grad32(p) if p is not None else None
+    """Add a computed gradient ``g`` (any float dtype, e.g. the fp32 partials of the
+    RMSNorm dγ / embedding kernels) into ``p``'s owner-attached target — the fp32
+    one, else the preallocated ``.grad`` — with ONE rounding, and notify the owner.
+    A target flagged ``_mx_grad_fresh`` is overwritten (it was not zero-filled).
+    False when ``p`` has no such target (return ``g`` to autograd)."""
+    if p is None:
+        return False
+    t = direct_grad32(p)
+    if t is None:
+        t = direct_grad(p)
     if t is None:
         return False
     if getattr(p, "_mx_grad_fresh", False):

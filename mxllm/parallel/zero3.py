@@ -369,7 +369,8 @@ class Zero3Trainer:
 
     def __init__(self, cfg, env: DistEnv, optim=None, *, seed: int = 0, activation_checkpointing: bool | int = False,
                  process_group=None, emulate_world: int = 0, max_inflight: int | None = None,
-                 init_from: str | None = None, grad_dtype: torch.dtype | None = torch.float32):
+                 init_from: str | None = None, grad_dtype: torch.dtype | None = torch.float32,
+                 rs_group=None):
         """``grad_dtype``: dtype the unit gradients are formed, reduce-scattered and
         accumulated in — fp32 by default (no bf16 rounding at any ring hop; the dW
         GEMMs write fp32 output), ``torch.bfloat16`` halves the reduce-scatter
@@ -386,10 +387,14 @@ class Zero3Trainer:
         else:
             self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
             self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
-            rs_pg = process_group
-            if self.world > 1 and os.environ.get("MXLLM_Z3_SPLIT_COMMS", "1") != "0":
-                ranks = dist.get_process_group_ranks(process_group) if process_group is not None else None
-                rs_pg = dist.new_group(ranks=ranks)  # second communicator: reduce-scatters on their own stream
+            rs_pg = rs_group if rs_group is not None else process_group
+            # second communicator (reduce-scatters on their own stream).  new_group is
+            # collective over the DEFAULT group, so it is only created here for the
+            # default group; a caller sharding over a subgroup passes ``rs_group``
+            # (created where every rank reaches it) or gets one communicator
+            if (rs_group is None and process_group is None and self.world > 1
+                    and os.environ.get("MXLLM_Z3_SPLIT_COMMS", "1") != "0"):
+                rs_pg = dist.new_group()
             comm = Comm(self.world, self.rank, process_group, rs_pg)
         self.comm = comm
         self.emulated = comm.emulate
@@ -407,7 +412,11 @@ class Zero3Trainer:
             u.device, u.dtype, u.gdt = dev, torch.bfloat16, self.grad_dtype
         total = sum(u.shard_numel for u in self.units)
         self.shard_params = torch.empty(total, dtype=torch.bfloat16, device=dev)
-        self.master = torch.empty(total, dtype=torch.float32, device=dev)
+        # fp32 master as (bf16 shard, int16 low halves): exact fp32 values, no separate
+        # bf16 copy — 2 B/param less (70B at world 8: 17.6 GB per rank)
+        self.split_master = os.environ.get("MXLLM_SPLIT_MASTER", "1") != "0"
+        self.master = (ops.SplitMaster(self.shard_params) if self.split_master
+                       else torch.empty(total, dtype=torch.float32, device=dev))
         self.grads = torch.zeros(total, dtype=torch.float32, device=dev)
         self.m = torch.zeros(total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -418,7 +427,8 @@ class Zero3Trainer:
             u.master_view = self.master[off:off + u.shard_numel]
             off += u.shard_numel
         self._materialize_shards(seed, init_from)
-        self.master.copy_(self.shard_params)
+        if not self.split_master:
+            self.master.copy_(self.shard_params)  # (split: lo = 0 is the exact fp32 value already)
         self._by_storage: dict[int, Unit] = {}
         self._param_unit: dict[int, Unit] = {}
         for u in self.units:
@@ -659,7 +669,8 @@ class Zero3Trainer:
         """After master/m/v were written in place (checkpoint.load, which reshards
         unit by unit): set the step, rebuild the bf16 shards and the resident unit."""
         self.step_num = int(step)
-        self.shard_params.copy_(self.master)
+        if not self.split_master:
+            self.shard_params.copy_(self.master)
         self._refresh_resident()
 
     def params_ready(self):
@@ -671,10 +682,11 @@ class Zero3Trainer:
         out = {}
         for u in self.units:
             full = torch.empty(u.full_numel, dtype=torch.float32, device=self.device)
+            src = u.master_view.float().contiguous()
             if self.comm.real:
-                dist.all_gather_into_tensor(full, u.master_view.contiguous(), group=self.pg)
+                dist.all_gather_into_tensor(full, src, group=self.pg)
             else:
-                full.view(self.world, -1).copy_(u.master_view.unsqueeze(0).expand(self.world, -1))
+                full.view(self.world, -1).copy_(src.unsqueeze(0).expand(self.world, -1))
             for name, o, n, shp in zip(u.names, u.offsets, u.numels, u.shapes):
                 out[name] = full[o:o + n].view(shp).clone()
         return out

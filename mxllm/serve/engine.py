@@ -55,6 +55,14 @@ class SamplingParams:
     stop_ids: tuple = ()
     seed: int = 0
 
+    def __post_init__(self):
+        if not (self.top_p == self.top_p and self.temperature == self.temperature):
+            raise ValueError("top_p / temperature must not be NaN")
+        if self.top_p < 0:
+            raise ValueError(f"top_p must be in [0, 1] (0 = greedy), got {self.top_p}")
+        if self.max_new_tokens < 0:
+            raise ValueError(f"max_new_tokens must be >= 0, got {self.max_new_tokens}")
+
 
 @dataclass
 class Request:

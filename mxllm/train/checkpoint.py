@@ -239,7 +239,7 @@ def _load_v1(d, man, trainer, rank, world):
         segs = _remap_segments(man["layout"], trainer.flat.state_dict())
         sd = {}
         for key, like in (("master", trainer._master), ("m", trainer.m), ("v", trainer.v)):
-            out = torch.zeros_like(like)
+            out = torch.zeros(like.numel(), dtype=torch.float32, device=like.device)
             for olo, ohi, nlo in segs:
                 out[nlo:nlo + ohi - olo].copy_(tensors[key][olo:ohi])
             sd[key] = out

@@ -82,14 +82,15 @@ class Trainer:
             if getattr(model, "param_wait", "absent") is None:
                 model.param_wait = self.zero1.wait_params  # per-layer wait in the next forward
         else:
-            self.flat = FlatParams(named, grad_dtype=grad_dtype, reverse=False)
+            self.flat = FlatParams(named, grad_dtype=grad_dtype, reverse=False,
+                                   split_master=os.environ.get("MXLLM_SPLIT_MASTER", "1") != "0")
             self.ddp = DDP(self.flat, bucket_mb=bucket_mb, first_bucket_mb=first_bucket_mb)
             self._master = self.flat.master
         if broadcast_init:
             self.ddp.broadcast_params(0)
         self._sync_adapters()
-        self.m = torch.zeros_like(self._master)
-        self.v = torch.zeros_like(self._master)
+        self.m = torch.zeros(self._master.numel(), dtype=torch.float32, device=self._master.device)
+        self.v = torch.zeros_like(self.m)
         self.step_num = 0
         self.last_grad_norm: torch.Tensor | None = None
         # ---- optimizer / next-forward overlap
@@ -105,10 +106,28 @@ class Trainer:
                 self._side = torch.cuda.Stream(self.flat.device) if self.flat.device.type == "cuda" else None
                 model.param_wait = self._param_wait
         self.overlap_optimizer = self._chunks is not None
+        # "fresh" gradients: every gradient of the step is formed by an op that can
+        # OVERWRITE its flat slot (dW GEMMs with beta 0, the RMSNorm / embedding
+        # kernels' accum_grad), so AdamW need not zero the gradient buffer behind
+        # itself (2-4 B/param less HBM traffic per step).  GPU kernels only; not
+        # with LoRA (its kernels accumulate), ZeRO-1 (buckets are cleared after the
+        # reduce-scatter) or parameters used twice (tied embeddings: autograd sums)
+        self.fresh_grads = (os.environ.get("MXLLM_FRESH_GRADS", "1") != "0" and self.flat.device.type == "cuda"
+                            and self.zero1 is None and not getattr(model, "lora", False)
+                            and not any(getattr(p, "_mx_no_direct", False) for p in self.flat.param_list))
 
     @property
     def lowp(self):
-        return None if self.flat.master is self.flat.params else self.flat.params
+        """The bf16 copy AdamW refreshes (None: fp32 params, or a split master whose
+        high half IS the parameter buffer)."""
+        if self.flat.master is self.flat.params or isinstance(self.flat.master, ops.SplitMaster):
+            return None
+        return self.flat.params
+
+    def master_fp32(self) -> torch.Tensor:
+        """The fp32 master weights as one tensor (flat layout; a copy when split)."""
+        self.params_ready()
+        return self._master.float()
 
     @property
     def grad_dtype(self) -> torch.dtype:
@@ -183,7 +202,8 @@ class Trainer:
         if side is None:  # CPU: same chunked update, in order (tests)
             for lo, hi in self._chunks:
                 ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
-                                None if lowp is None else lowp[lo:hi], grad_scale=gscale, zero_grad=True, **kw)
+                                None if lowp is None else lowp[lo:hi], grad_scale=gscale,
+                                zero_grad=not self.fresh_grads, **kw)
             return
         side.wait_stream(torch.cuda.current_stream(self.flat.device))
         self._hold = gscale  # read on the side stream: keep it alive until the next step
@@ -192,7 +212,8 @@ class Trainer:
         with torch.cuda.stream(side):
             for k, (lo, hi) in enumerate(self._chunks):
                 ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
-                                None if lowp is None else lowp[lo:hi], grad_scale=gscale, zero_grad=True, **kw)
+                                None if lowp is None else lowp[lo:hi], grad_scale=gscale,
+                                zero_grad=not self.fresh_grads, **kw)
                 ev = torch.cuda.Event()
                 ev.record(side)
                 self._pending[k] = ev
@@ -215,6 +236,9 @@ class Trainer:
         self.model.train()
         if self.zero1 is not None and getattr(self.model, "param_wait", None) is None:
             self.zero1.wait_params()  # model without per-layer waits: all parameters first
+        if self.fresh_grads:
+            for p in self.flat.param_list:
+                p._mx_grad_fresh = True
         total = None
         for i, (ids, labels) in enumerate(micro_batches):
             last = i == n - 1
@@ -226,6 +250,8 @@ class Trainer:
                     (loss / n if n > 1 else loss).backward()
             total = loss.detach() if total is None else total + loss.detach()
         self.flat.sync_grads_from_params()
+        if self.fresh_grads:
+            self.flat.zero_unwritten_()
         with range_("grad_allreduce_wait"):
             scale = self.ddp.finish() / n if n > 1 else self.ddp.finish()
         return total, scale
@@ -262,7 +288,8 @@ class Trainer:
         else:
             ops.adamw_step_(self.flat.master, grads, self.m, self.v, self.lowp, lr=o.lr_at(self.step_num),
                             beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
-                            step=self.step_num, grad_scale=gscale, zero_grad=True)  # grads cleared in the same pass
+                            step=self.step_num, grad_scale=gscale,
+                            zero_grad=not self.fresh_grads)  # else grads cleared in the same pass
         self._sync_adapters()
         self.flat.attach_grads()
 
@@ -300,7 +327,7 @@ class Trainer:
                 z.pshard.copy_(z.master)
             z.gather_params()
             z.wait_params()
-        elif self.flat.master is not self.flat.params:
+        elif self.flat.master is not self.flat.params and not isinstance(self.flat.master, ops.SplitMaster):
             self.flat.params.copy_(self.flat.master)
         self._sync_adapters()
 

@@ -1,5 +1,5 @@
 """Per-step kernel time breakdown from a rocprofv3 kernel trace: the window
-between the last two fused-AdamW launches (one per optimizer step) -> one step.
+between the last two grad-norm launches (one per optimizer step) -> one step.
 usage: python scripts/step_breakdown.py <run_kernel_trace.csv> [top]"""
 import collections
 import csv
@@ -10,7 +10,9 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+    # one grad-norm kernel per optimizer step (AdamW may be issued as several chunk launches)
+    key = "sqnorm_partial" if any("sqnorm_partial" in r["Kernel_Name"] for r in rows) else "adamw_kernel"
+    marks = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
     a, b = marks[-2], marks[-1]
     win = rows[a + 1:b + 1]
     t0, t1 = int(win[0]["Start_Timestamp"]), int(win[-1]["End_Timestamp"])

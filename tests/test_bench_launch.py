@@ -67,3 +67,29 @@ def test_zero3_emulation_is_labelled():
     assert r.returncode == 0, r.stderr[-3000:]
     j = _json_lines(r.stdout)[0]
     assert j["emulated_world"] == 4 and "EMULATED" in j["config"]["parallelism"] and "PROXY" in j["note"]
+
+
+def test_world8_rehearsal_with_config3_and_config4():
+    """CPU rehearsal of the driver's 8-GPU run: ``bench.py --gpus 8`` self-launches 8
+    gloo ranks; after the headline the in-process config-3 (full fine-tune, DDP over
+    all 8 ranks) and the config-4 child job (ZeRO-3 over 8 ranks) report inside the
+    ONE JSON line, labelled with the model that actually ran."""
+    import time
+
+    t0 = time.time()
+    r = _bench("--gpus", "8", "--config3", "on", "--full-model", "tiny", "--full-steps", "1", "--full-warmup", "1",
+               "--config4", "on", "--config4-model", "tiny", "--config4-steps", "1", "--config4-warmup", "1",
+               timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert time.time() - t0 < 180
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["n_gpus"] == 8 and j["config"]["parallelism"] == "dp8"
+    c3 = j["config3_8b_full_dp8"]
+    assert "error" not in c3, c3
+    assert c3["n_gpus"] == 8 and c3["config"]["finetune"].startswith("full") and "config 3" in c3["label"]
+    c4 = j["config4_full_zero3"]
+    assert "error" not in c4, c4
+    assert c4["config"]["parallelism"] == "zero3-dp8" and c4["config"]["grad_reduce_dtype"] == "fp32"
+    assert "tiny" in c4["label"] and "70B" not in c4["label"]

@@ -180,3 +180,37 @@ def test_lora_dx_image_matches_augmented_buffer():
             for m in (a, b):
                 m.lora_a.add_(0.05)
                 m.sync_adapter_()
+
+
+def test_split_master_roundtrip_exact():
+    """SplitMaster (mxllm/ops/optim.py): fp32 -> (bf16 hi, int16 lo) -> fp32 is the
+    identity on the bits; hi is the value rounded half-up on its bit pattern (= RNE
+    except at exact ties); AdamW through a split master equals AdamW on fp32."""
+    from mxllm.ops import SplitMaster, adamw_step_
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.cat([torch.randn(10000, generator=g) * s for s in (1e-30, 1e-3, 1.0, 1e4, 1e30)])
+    x = torch.cat([x, -x, torch.tensor([0.0, -0.0, 1.0 + 2 ** -8, -(1.0 + 2 ** -8), 3.0 + 2 ** -7])])
+    sm = SplitMaster(torch.empty(x.numel(), dtype=torch.bfloat16))
+    sm.copy_(x)
+    assert torch.equal(sm.float().view(torch.int32), x.view(torch.int32))
+    bits = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    want_hi = ((bits + 0x8000) >> 16) & 0xFFFF
+    assert torch.equal(sm.hi.view(torch.int16).to(torch.int64) & 0xFFFF, want_hi)
+    ne = (bits & 0xFFFF) != 0x8000  # not a tie: same as round-to-nearest-even
+    assert torch.equal(sm.hi[ne], x[ne].bfloat16())
+    # slices are views of both halves
+    sm[5:10].copy_(torch.full((5,), 2.5))
+    assert torch.equal(sm.float()[5:10], torch.full((5,), 2.5))
+    # AdamW: split master == fp32 master, bit for bit
+    n = 4096
+    p32 = torch.randn(n, generator=g)
+    grad = torch.randn(n, generator=g).bfloat16()
+    m1, v1, m2, v2 = (torch.zeros(n) for _ in range(4))
+    sp = SplitMaster(torch.empty(n, dtype=torch.bfloat16))
+    sp.copy_(p32)
+    for step in range(1, 4):
+        kw = dict(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.01, step=step, grad_scale=0.5)
+        adamw_step_(p32, grad, m1, v1, None, **kw)
+        adamw_step_(sp, grad, m2, v2, None, **kw)
+    assert torch.equal(sp.float(), p32) and torch.equal(m1, m2) and torch.equal(v1, v2)

@@ -84,3 +84,47 @@ def test_gpu_temperature_rows_split_kernel_matches_topkp_kernel(gpu, dtype, V):
     # routed entry point
     ids = dops.sample_rows(x, temps.tolist(), [1.0] * B, [0] * B, seeds.tolist(), steps.tolist())
     assert torch.equal(ids, native().sample_rows(x, temps, ones, zeros, seeds, steps))
+
+
+def test_top_p_zero_is_greedy_cpu():
+    """top_p <= 0 (an empty nucleus) samples greedily; NaN is rejected; SamplingParams
+    validates its range (the kernel and the oracle used to disagree)."""
+    from mxllm.serve.engine import SamplingParams
+
+    x = torch.randn(3, 50, generator=torch.Generator().manual_seed(1))
+    ids = dops.sample_rows(x, [1.0, 2.0, 0.5], [0.0, -1.0, 1e-9], [0, 0, 0], [1, 2, 3], [0, 0, 0])
+    assert ids[0] == x[0].argmax() and ids[1] == x[1].argmax()
+    with pytest.raises(ValueError):
+        dops.sample_rows(x, [1.0] * 3, [float("nan")] * 3, [0] * 3, [0] * 3, [0] * 3)
+    with pytest.raises(ValueError):
+        SamplingParams(top_p=-0.5)
+    SamplingParams(top_p=0.0)
+
+
+@pytest.mark.gpu
+def test_top_p_zero_is_greedy_gpu(gpu):
+    x = torch.randn(4, 128256, device=gpu).bfloat16()
+    ids = dops.sample_rows(x, [1.0, 0.7, 1.0, 0.0], [0.0, -2.0, 0.9, 0.5], [0, 0, 0, 0], [1, 2, 3, 4], [0, 0, 0, 0])
+    want = x.float().argmax(-1)
+    assert ids[0] == want[0] and ids[1] == want[1] and ids[3] == want[3]
+
+
+@pytest.mark.gpu
+def test_concurrent_samplers_on_two_streams(gpu):
+    """The vocabulary-split sampler keeps its partials in a per-call workspace: two
+    samplers running concurrently on different streams do not corrupt each other."""
+    from mxllm.ops import native
+
+    xs = [torch.randn(64, 128256, device=gpu).bfloat16() for _ in range(2)]
+    want = [x.float().argmax(-1) for x in xs]
+    streams = [torch.cuda.Stream(gpu) for _ in range(2)]
+    torch.cuda.synchronize(gpu)
+    outs = [[], []]
+    for _ in range(20):
+        for k in range(2):
+            with torch.cuda.stream(streams[k]):
+                outs[k].append(native().sample(xs[k], 0.0, 0, 0))
+    torch.cuda.synchronize(gpu)
+    for k in range(2):
+        for o in outs[k]:
+            assert torch.equal(o, want[k])

@@ -182,7 +182,7 @@ def test_zero3_emulated_world4_one_step_gpu(gpu, ck):
     want = shard0.clone()
     ref_ops.adamw_(want, exp, m, v, lr=o.lr, beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
                    step=1, grad_scale=gscale)
-    d = (z.master - want).abs()
+    d = (z.master.float() - want).abs()
     # step 1 of AdamW moves every weight by ~lr * sign(g): only near-zero gradients can differ
     assert float(d.mean()) < 2e-5 and int((d > 2e-4).sum()) <= max(8, 2e-3 * d.numel()), float(d.max())
 
@@ -205,3 +205,33 @@ def test_bench_config2_field_tiny(gpu, tmp_path):
     assert "error" not in c2, c2
     assert c2["value"] > 0 and "config 2" in c2["label"] and c2["config"]["finetune"].startswith("full")
     assert "overlapped" in c2["config"]["optimizer"]
+
+
+@pytest.mark.parametrize("gbf16,zero", [(True, False), (True, True), (False, False)])
+def test_split_master_adamw_kernel_bitwise(gpu, gbf16, zero):
+    """The SPLIT AdamW kernel (fp32 master as bf16 high half + int16 low half)
+    against the fp32-master kernel: master / m / v bit for bit after 3 steps, the
+    high half = the master rounded half-up on its bits, the gradient cleared iff
+    asked; split/join kernels round-trip exactly."""
+    from mxllm.ops import SplitMaster, adamw_step_
+
+    n = (1 << 20) + 64
+    g = torch.Generator(device=gpu).manual_seed(7)
+    p32 = torch.randn(n, device=gpu, generator=g) * 0.05
+    sm = SplitMaster(torch.empty(n, dtype=torch.bfloat16, device=gpu))
+    sm.copy_(p32)
+    assert torch.equal(sm.float().view(torch.int32), p32.view(torch.int32))
+    m1, v1, m2, v2 = (torch.zeros(n, device=gpu) for _ in range(4))
+    for step in range(1, 4):
+        grad = torch.randn(n, device=gpu, generator=g)
+        grad = grad.bfloat16() if gbf16 else grad
+        g2 = grad.clone()
+        kw = dict(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.01, step=step,
+                  grad_scale=torch.tensor([0.7], device=gpu))
+        adamw_step_(p32, grad, m1, v1, None, zero_grad=zero, **kw)
+        adamw_step_(sm, g2, m2, v2, None, zero_grad=zero, **kw)
+        assert bool((g2 == 0).all()) == zero
+    assert torch.equal(sm.float().view(torch.int32), p32.view(torch.int32))
+    assert torch.equal(m1, m2) and torch.equal(v1, v2)
+    bits = p32.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(sm.hi.view(torch.int16).to(torch.int64) & 0xFFFF, ((bits + 0x8000) >> 16) & 0xFFFF)
