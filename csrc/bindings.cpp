@@ -452,10 +452,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_ablate(const at::Tensor&
 }
 
 // ---------------------------------------------------------------- decode
-// qkv [B, NH*D]; k_cache/v_cache [slots, Hkv, max_seq, D]; pos/slots int32 [B]
+// Paged KV caches: k_cache/v_cache [blocks, Hkv, block, D] + block_table int32 [slots, maxb]
+// (token p of slot s in block block_table[s][p / block]); without a block table the caches
+// are [slots, Hkv, max_seq, D].
+struct KvPages {
+  const int32_t* bt = nullptr;
+  int maxb = 0;
+};
+static KvPages kv_pages(const c10::optional<at::Tensor>& block_table, const at::Tensor& k_cache) {
+  KvPages pg;
+  if (block_table.has_value() && block_table->defined()) {
+    const at::Tensor& t = *block_table;
+    MX_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.dim() == 2 && t.is_contiguous(),
+             "block_table int32 [slots, max_blocks] contiguous GPU");
+    MX_CHECK(k_cache.size(2) % 256 == 0, "paged KV: the block size must be a multiple of 256 tokens");
+    pg.bt = t.data_ptr<int32_t>();
+    pg.maxb = (int)t.size(1);
+  }
+  return pg;
+}
+
+// qkv [B, NH*D]; k_cache/v_cache [slots, Hkv, max_seq, D] (or paged); pos/slots int32 [B]
 at::Tensor rope_append(const at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin, const at::Tensor& pos,
                        const c10::optional<at::Tensor>& slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
-                       int64_t Hkv, int64_t D) {
+                       int64_t Hkv, int64_t D, const c10::optional<at::Tensor>& block_table) {
   check_bf16(qkv, "qkv");
   check_bf16(k_cache, "k_cache");
   check_bf16(v_cache, "v_cache");
@@ -467,21 +487,24 @@ at::Tensor rope_append(const at::Tensor& qkv, const at::Tensor& cos, const at::T
   const int32_t* sl = nullptr;
   if (slots.has_value()) sl = slots->data_ptr<int32_t>();
   auto q = at::empty({B, Hq, D}, qkv.options());
+  const KvPages pg = kv_pages(block_table, k_cache);
   MX_OK(mx_rope_append(bf(qkv), cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int32_t>(), sl, bfm(q),
-                       bfm(k_cache), bfm(v_cache), (int)B, (int)Hq, (int)Hkv, (int)D, (int)k_cache.size(2),
-                       cur_stream()));
+                       bfm(k_cache), bfm(v_cache), (int)B, (int)Hq, (int)Hkv, (int)D, (int)k_cache.size(2), pg.bt,
+                       pg.maxb, cur_stream()));
   return q;
 }
 
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                        const at::Tensor& lens, const c10::optional<at::Tensor>& slots, int64_t max_len, double scale,
-                       int64_t len_off) {
+                       int64_t len_off, const c10::optional<at::Tensor>& block_table) {
   check_bf16(q, "q");
   MX_CHECK(lens.scalar_type() == at::kInt, "lens int32");
   const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
   const int64_t Hkv = k_cache.size(1), max_seq = k_cache.size(2);
   DevGuard g(q.device());
-  const int64_t nsplit = std::max<int64_t>(1, (std::min(max_len, max_seq) + 255) / 256);
+  const KvPages pg = kv_pages(block_table, k_cache);
+  const int64_t cap = pg.bt ? (int64_t)pg.maxb * max_seq : max_seq;  // positions a sequence can hold
+  const int64_t nsplit = std::max<int64_t>(1, (std::min(max_len, cap) + 255) / 256);
   auto ml = at::empty({B, Hq, nsplit, 2}, q.options().dtype(at::kFloat));
   auto po = at::empty({B, Hq, nsplit, D}, q.options().dtype(at::kFloat));
   auto out = at::empty({B, Hq * D}, q.options());
@@ -489,7 +512,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   if (slots.has_value()) sl = slots->data_ptr<int32_t>();
   MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), (int)len_off, sl, ml.data_ptr<float>(),
                        po.data_ptr<float>(), bfm(out), (int)B, (int)Hq, (int)Hkv, (int)D, (int)max_seq, (int)nsplit,
-                       (float)scale, cur_stream()));
+                       (float)scale, pg.bt, pg.maxb, cur_stream()));
   return out;
 }
 
@@ -624,7 +647,8 @@ std::tuple<at::Tensor, at::Tensor> skinny_qkv_rope(const at::Tensor& h, const c1
                                                    const c10::optional<at::Tensor>& gamma, double eps,
                                                    const at::Tensor& w, const at::Tensor& cosb, const at::Tensor& sinb,
                                                    const at::Tensor& pos, const c10::optional<at::Tensor>& slots,
-                                                   at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv) {
+                                                   at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv,
+                                                   const c10::optional<at::Tensor>& block_table) {
   MX_CHECK(h.is_cuda() && h.scalar_type() == at::kBFloat16 && h.dim() == 2 && h.stride(1) == 1, "h: bf16 [M, K] rows");
   MX_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1, "w: bf16 [N, K] rows");
   const int64_t M = h.size(0), K = h.size(1);
@@ -659,10 +683,11 @@ std::tuple<at::Tensor, at::Tensor> skinny_qkv_rope(const at::Tensor& h, const c1
     MX_CHECK(gamma->scalar_type() == at::kBFloat16 && gamma->is_contiguous() && gamma->numel() == K, "gamma bf16 [K]");
   DevGuard g(h.device());
   auto q = at::empty({M, Hq, 128}, h.options());
+  const KvPages pg = kv_pages(block_table, k_cache);
   MX_OK(mx_skinny_rope_gemm(bf(h), h.stride(0), norm ? 1 : 0, dp, ldd, norm ? bf(*gamma) : nullptr, (float)eps,
                             dp ? bfm(h_out) : nullptr, bf(w), w.stride(0), cosb.data_ptr<float>(),
                             sinb.data_ptr<float>(), pos.data_ptr<int32_t>(), sl, bfm(q), bfm(k_cache),
-                            bfm(v_cache), (int)Hq, (int)Hkv, (int)k_cache.size(2), (int)M, (int)K, cur_stream()));
+                            bfm(v_cache), (int)Hq, (int)Hkv, (int)k_cache.size(2), pg.bt, pg.maxb, (int)M, (int)K, cur_stream()));
   return {q, h_out};
 }
 
@@ -787,15 +812,15 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
-  m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D) -> Tensor");
-  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0) -> Tensor");
+  m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D, Tensor? block_table=None) -> Tensor");
+  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0, Tensor? block_table=None) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("sample_rows(Tensor logits, Tensor temps, Tensor top_p, Tensor top_k, Tensor seeds, Tensor steps) -> Tensor");
   m.def("sample_temp_rows(Tensor logits, Tensor temps, Tensor seeds, Tensor steps) -> Tensor");
   m.def("w8_linear(Tensor x, Tensor q, Tensor scale) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_linear_swiglu(Tensor x, Tensor w) -> Tensor");
-  m.def("skinny_qkv_rope(Tensor h, Tensor? delta, Tensor? gamma, float eps, Tensor w, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv) -> (Tensor, Tensor)");
+  m.def("skinny_qkv_rope(Tensor h, Tensor? delta, Tensor? gamma, float eps, Tensor w, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, Tensor? block_table=None) -> (Tensor, Tensor)");
   m.def("skinny_norm_linear(Tensor h, Tensor? delta, Tensor gamma, float eps, Tensor w, bool swiglu) -> (Tensor, Tensor)");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");

@@ -58,10 +58,10 @@ extern "C" {
 // decode.hip
 int mx_rope_append(const uint16_t* qkv, const float* cosb, const float* sinb, const int32_t* pos, const int32_t* slots,
                    uint16_t* q, uint16_t* kc, uint16_t* vc, int B, int Hq, int Hkv, int D, int max_seq,
-                   hipStream_t stream);
+                   const int32_t* bt, int maxb, hipStream_t stream);
 int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens, int len_off,
                    const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B, int Hq, int Hkv, int D,
-                   int max_seq, int nsplit, float scale, hipStream_t stream);
+                   int max_seq, int nsplit, float scale, const int32_t* bt, int maxb, hipStream_t stream);
 int64_t mx_sample_ws_floats(int B);
 int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature, uint32_t seed,
               uint32_t step, float* ws, hipStream_t stream);
@@ -82,7 +82,7 @@ int mx_skinny_gemm_swiglu(const uint16_t* x, int64_t ldx, const uint16_t* w, int
 int mx_skinny_rope_gemm(const uint16_t* h, int64_t ldh, int norm, const uint16_t* delta, int64_t ldd,
                         const uint16_t* gamma, float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw,
                         const float* cosb, const float* sinb, const int32_t* pos, const int32_t* slots, uint16_t* q,
-                        uint16_t* kc, uint16_t* vc, int Hq, int Hkv, int max_seq, int M, int K, hipStream_t stream);
+                        uint16_t* kc, uint16_t* vc, int Hq, int Hkv, int max_seq, const int32_t* bt, int maxb, int M, int K, hipStream_t stream);
 int mx_skinny_norm_gemm(const uint16_t* h, int64_t ldh, const uint16_t* delta, int64_t ldd, const uint16_t* gamma,
                         float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw, uint16_t* y, int64_t ldy, int M,
                         int N, int K, int swiglu, hipStream_t stream);

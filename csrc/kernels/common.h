@@ -100,6 +100,18 @@ __device__ __forceinline__ int xcd_balance(int orig, int nwg, int BH, int G) {
   return outer * BH + bh;
 }
 
+// ---- KV cache addressing (decode kernels) ----
+// Per layer the cache is [rows, Hkv, SEQ, D] bf16.  Contiguous (bt == nullptr): rows =
+// slots, SEQ = max_seq.  Paged (bt = block table [slots, maxb] int32): rows = pool blocks,
+// SEQ = the block size; token p of slot s lives in block bt[s][p / SEQ] at row p % SEQ.
+// Returns the token-row index (multiply by D for the element offset).
+__device__ __forceinline__ int64_t kv_row(const int32_t* __restrict__ bt, int maxb, int seq, int slot, int Hkv,
+                                          int hk, int p) {
+  if (!bt) return ((int64_t)slot * Hkv + hk) * seq + p;
+  const int blk = bt[(int64_t)slot * maxb + p / seq];
+  return ((int64_t)blk * Hkv + hk) * seq + (p % seq);
+}
+
 // ---- LDS-DMA-friendly transposed reads (used by the attention kernels) ----
 // ds_read_b64_tr_b16 as inline asm with an immediate offset: invisible to hipcc's
 // waitcnt pass, which otherwise drains every in-flight LDS-DMA (vmcnt(0)) before a

@@ -8,7 +8,10 @@
 //   * sample : greedy argmax or exact temperature sampling via Gumbel-max with
 //              a counter-based hash RNG (one pass, no softmax materialised).
 // KV cache layout per layer: [slots, Hkv, max_seq, D] bf16 (contiguous per slot
-// and head: one 256-B row per token for D = 128).
+// and head: one 256-B row per token for D = 128), or PAGED: a pool of blocks
+// [blocks, Hkv, block, D] addressed through a per-slot block table (common.h
+// kv_row; the block size is a multiple of the 256-key decode split, so every
+// split reads one contiguous block).
 #include "common.h"
 
 namespace mx {
@@ -22,7 +25,7 @@ __global__ void __launch_bounds__(256) rope_append_kernel(const uint16_t* __rest
                                                           const int32_t* __restrict__ slots,
                                                           uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
                                                           uint16_t* __restrict__ vc, int B, int Hq, int Hkv,
-                                                          int max_seq) {
+                                                          int max_seq, const int32_t* __restrict__ bt, int maxb) {
   constexpr int HALF = D / 2, CPH = HALF / 8;
   const int NH = Hq + 2 * Hkv;
   const int64_t n = (int64_t)B * NH * CPH;
@@ -38,13 +41,13 @@ __global__ void __launch_bounds__(256) rope_append_kernel(const uint16_t* __rest
     u16x8 x2 = *reinterpret_cast<const u16x8*>(src + HALF + c);
     uint16_t* dst;
     if (head >= Hq + Hkv) {
-      dst = vc + (((int64_t)slot * Hkv + (head - Hq - Hkv)) * max_seq + p) * D;
+      dst = vc + kv_row(bt, maxb, max_seq, slot, Hkv, head - Hq - Hkv, p) * D;
       *reinterpret_cast<u16x8*>(dst + c) = x1;
       *reinterpret_cast<u16x8*>(dst + HALF + c) = x2;
       continue;
     }
     dst = head < Hq ? q + ((int64_t)b * Hq + head) * D
-                    : kc + (((int64_t)slot * Hkv + (head - Hq)) * max_seq + p) * D;
+                    : kc + kv_row(bt, maxb, max_seq, slot, Hkv, head - Hq, p) * D;
     const float* cp = cosb + (int64_t)p * HALF + c;
     const float* sp = sinb + (int64_t)p * HALF + c;
     u16x8 y1, y2;
@@ -70,7 +73,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const uint16_t* __rest
                                                           const int32_t* __restrict__ lens, int len_off,
                                                           const int32_t* __restrict__ slots,
                                                           float* __restrict__ part_ml, float* __restrict__ part_o,
-                                                          int Hq, int Hkv, int max_seq, int nsplit, float sl) {
+                                                          int Hq, int Hkv, int max_seq, int nsplit, float sl,
+                                                          const int32_t* __restrict__ bt, int maxb) {
   __shared__ float qs[kMaxRep][D];
   __shared__ float ps[kMaxRep][kSplit];
   __shared__ float red[kMaxRep][4];
@@ -94,8 +98,11 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const uint16_t* __rest
     const int h = i / D, d = i % D;
     qs[h][d] = bf2f(q[((int64_t)b * Hq + hk * rep + h) * D + d]);
   }
-  const uint16_t* kbase = kc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
-  const uint16_t* vbase = vc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
+  // base such that base + key * D addresses every key of this split (a paged split lies in
+  // one block: the block size is a multiple of kSplit)
+  const int64_t kvb = (kv_row(bt, maxb, max_seq, slot, Hkv, hk, k_lo) - k_lo) * D;
+  const uint16_t* kbase = kc + kvb;
+  const uint16_t* vbase = vc + kvb;
   // stage V rows of this split into LDS (coalesced 16-B chunks)
   constexpr int CH = D / 8;
   for (int c = tid; c < kSplit * CH; c += 256) {
@@ -221,7 +228,8 @@ __global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t
                                                                   const int32_t* __restrict__ slots,
                                                                   float* __restrict__ part_ml,
                                                                   float* __restrict__ part_o, int Hq, int Hkv,
-                                                                  int max_seq, int nsplit, float sl) {
+                                                                  int max_seq, int nsplit, float sl,
+                                                                  const int32_t* __restrict__ bt, int maxb) {
   constexpr int D = 128, ROWB = 256, WKEYS = 64, WTILE = WKEYS * ROWB;  // 16 KiB per wave
   __shared__ __attribute__((aligned(16))) char smem[4 * WTILE];
   __shared__ float mls[4][2][16];
@@ -242,8 +250,9 @@ __global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t
     }
     return;
   }
-  const uint16_t* kbase = kc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
-  const uint16_t* vbase = vc + (((int64_t)slot * Hkv + hk) * max_seq) * D;
+  const int64_t kvb = (kv_row(bt, maxb, max_seq, slot, Hkv, hk, k_lo) - k_lo) * D;  // one block per split
+  const uint16_t* kbase = kc + kvb;
+  const uint16_t* vbase = vc + kvb;
   const int wk0 = k_lo + WKEYS * w;
   char* vs = smem + w * WTILE;
 
@@ -506,13 +515,15 @@ __global__ void __launch_bounds__(64) sample_final_kernel(int64_t* __restrict__ 
 
 using namespace mx;
 
+// bt / maxb: paged cache (block table [slots, maxb]; max_seq = the block size), nullptr: contiguous
 extern "C" int mx_rope_append(const uint16_t* qkv, const float* cosb, const float* sinb, const int32_t* pos,
                               const int32_t* slots, uint16_t* q, uint16_t* kc, uint16_t* vc, int B, int Hq, int Hkv,
-                              int D, int max_seq, hipStream_t stream) {
+                              int D, int max_seq, const int32_t* bt, int maxb, hipStream_t stream) {
   const int64_t items = (int64_t)B * (Hq + 2 * Hkv) * (D / 16);
   if (items <= 0) return 0;
   const int grid = (int)std::min<int64_t>(1024, (items + 255) / 256);
-#define RA(DD) rope_append_kernel<DD><<<grid, 256, 0, stream>>>(qkv, cosb, sinb, pos, slots, q, kc, vc, B, Hq, Hkv, max_seq)
+#define RA(DD) \
+  rope_append_kernel<DD><<<grid, 256, 0, stream>>>(qkv, cosb, sinb, pos, slots, q, kc, vc, B, Hq, Hkv, max_seq, bt, maxb)
   if (D == 128) RA(128); else if (D == 64) RA(64); else if (D == 32) RA(32); else return -1;
 #undef RA
   return (int)hipGetLastError();
@@ -520,20 +531,22 @@ extern "C" int mx_rope_append(const uint16_t* qkv, const float* cosb, const floa
 
 extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens,
                               int len_off, const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B,
-                              int Hq, int Hkv, int D, int max_seq, int nsplit, float scale, hipStream_t stream) {
+                              int Hq, int Hkv, int D, int max_seq, int nsplit, float scale, const int32_t* bt,
+                              int maxb, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > kMaxRep) return -1;
+  if (bt && max_seq % kSplit) return -1;  // a split must lie inside one block
   dim3 grid(nsplit, Hkv, B);
   const float sl = scale * 1.4426950408889634f;
   if (D == 128) {
     decode_attn_mfma_kernel<<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv,
-                                                      max_seq, nsplit, sl);
+                                                      max_seq, nsplit, sl, bt, maxb);
     decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
     return (int)hipGetLastError();
   }
 #define DA(DD)                                                                                                  \
   decode_attn_kernel<DD><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv, \
-                                                   max_seq, nsplit, sl);                                        \
+                                                   max_seq, nsplit, sl, bt, maxb);                              \
   decode_combine_kernel<DD><<<B * Hq, DD, 0, stream>>>(part_ml, part_o, out, nsplit)
   if (D == 64) { DA(64); } else if (D == 32) { DA(32); } else return -1;
 #undef DA

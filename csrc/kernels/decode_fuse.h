@@ -24,9 +24,11 @@ struct SkRope {
   const int32_t* pos;    // [M] position of the new token
   const int32_t* slots;  // [M] cache slot (nullptr: row index)
   uint16_t* q;           // [M, Hq, 128]
-  uint16_t* kc;          // [slots, Hkv, max_seq, 128]
+  uint16_t* kc;          // [slots, Hkv, max_seq, 128], or paged [blocks, Hkv, block, 128]
   uint16_t* vc;
-  int Hq, Hkv, max_seq;
+  int Hq, Hkv, max_seq;  // max_seq: the cache's sequence dimension (the block size when paged)
+  const int32_t* bt;     // paged: block table [slots, maxb] (nullptr: contiguous)
+  int maxb;
 };
 
 // Weight row of channel c (0..15) of workgroup blk in the paired layouts:
@@ -125,7 +127,7 @@ __device__ __forceinline__ void dfuse_rope_store(const f32x4& v, int g, int m, i
     if (head >= rp.Hq + rp.Hkv) {  // v: no rotation
 #pragma unroll
       for (int i = 0; i < 4; ++i) y1[i] = f2bf(v[i]), y2[i] = f2bf(hi[i]);
-      dst = rp.vc + (((int64_t)slot * rp.Hkv + (head - rp.Hq - rp.Hkv)) * rp.max_seq + p) * 128;
+      dst = rp.vc + kv_row(rp.bt, rp.maxb, rp.max_seq, slot, rp.Hkv, head - rp.Hq - rp.Hkv, p) * 128;
     } else {
       const float* cp = rp.cosb + (int64_t)p * 64 + i0;
       const float* sp = rp.sinb + (int64_t)p * 64 + i0;
@@ -136,7 +138,7 @@ __device__ __forceinline__ void dfuse_rope_store(const f32x4& v, int g, int m, i
         y2[i] = f2bf(bb * cp[i] + a * sp[i]);
       }
       dst = head < rp.Hq ? rp.q + ((int64_t)m * rp.Hq + head) * 128
-                         : rp.kc + (((int64_t)slot * rp.Hkv + (head - rp.Hq)) * rp.max_seq + p) * 128;
+                         : rp.kc + kv_row(rp.bt, rp.maxb, rp.max_seq, slot, rp.Hkv, head - rp.Hq, p) * 128;
     }
     *reinterpret_cast<u16x4*>(dst + i0) = y1;
     *reinterpret_cast<u16x4*>(dst + 64 + i0) = y2;

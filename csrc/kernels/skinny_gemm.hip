@@ -192,14 +192,14 @@ using namespace mx;
 extern "C" int mx_skinny_rope_gemm(const uint16_t* h, int64_t ldh, int norm, const uint16_t* delta, int64_t ldd,
                                    const uint16_t* gamma, float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw,
                                    const float* cosb, const float* sinb, const int32_t* pos, const int32_t* slots,
-                                   uint16_t* q, uint16_t* kc, uint16_t* vc, int Hq, int Hkv, int max_seq, int M,
-                                   int K, hipStream_t stream) {
+                                   uint16_t* q, uint16_t* kc, uint16_t* vc, int Hq, int Hkv, int max_seq,
+                                   const int32_t* bt, int maxb, int M, int K, hipStream_t stream) {
   if (M <= 0) return 0;
   const int N = (Hq + 2 * Hkv) * 128;
   if (M > (norm ? 4 : 16) || (norm && (int64_t)M * K > 32768) || K % 512 || ldh % 8 || ldd % 8 || ldw % 8 ||
       ldh < K || ldw < K || (norm && delta && (ldd < K || !h_out)))
     return -1;
-  const SkRope rp{cosb, sinb, pos, slots, q, kc, vc, Hq, Hkv, max_seq};
+  const SkRope rp{cosb, sinb, pos, slots, q, kc, vc, Hq, Hkv, max_seq, bt, maxb};
   if (norm) {
     const SkNorm na{delta, ldd, gamma, h_out, eps};
     skinny_gemm_kernel<1, 1, false, true, true><<<N / 16, 512, (size_t)M * K * 2, stream>>>(

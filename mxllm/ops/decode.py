@@ -14,34 +14,51 @@ from . import reference as ref
 from ._ext import native, use_native
 
 
-def prefill_attention(qkv: torch.Tensor, cos, sin, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: int,
-                      S: int, Hq: int, Hkv: int, D: int) -> torch.Tensor:
-    """One sequence (positions 0..S-1): RoPE, write K/V into ``cache[slot, :, :S]``,
-    causal attention.  qkv [S, NH*D] -> o [S, Hq*D]."""
+def prefill_attention(qkv: torch.Tensor, cos, sin, write_kv, S: int, Hq: int, Hkv: int, D: int) -> torch.Tensor:
+    """One sequence (positions 0..S-1): RoPE, hand the rotated K and V [Hkv, S, D] to
+    ``write_kv(k, v)`` (the engine's KV cache), causal attention.
+    qkv [S, NH*D] -> o [S, Hq*D]."""
     if use_native(qkv):
         ops = native()
         q, k, v = ops.rope_split(qkv.contiguous(), cos, sin, 1, S, Hq, Hkv, D, None)
-        k_cache[slot, :, :S].copy_(k[0])
-        v_cache[slot, :, :S].copy_(v[0])
+        write_kv(k[0], v[0])
         o, _ = ops.attn_fwd(q, k, v, True, 1.0 / math.sqrt(D))
         return o.view(S, Hq * D)
     x = qkv.view(1, S, Hq + 2 * Hkv, D)
     q = ref.apply_rope(x[:, :, :Hq], cos, sin)
     k = ref.apply_rope(x[:, :, Hq:Hq + Hkv], cos, sin)
     v = x[:, :, Hq + Hkv:]
-    k_cache[slot, :, :S].copy_(k[0].transpose(0, 1))
-    v_cache[slot, :, :S].copy_(v[0].transpose(0, 1))
+    write_kv(k[0].transpose(0, 1), v[0].transpose(0, 1))
     return ref.attention(q, k, v, causal=True).reshape(S, Hq * D)
 
 
+def _kv_at(cache: torch.Tensor, bt, slot: int, p0: int, p1: int) -> torch.Tensor:
+    """Rows [p0, p1) of ``slot`` as [Hkv, p1 - p0, D] (contiguous or paged cache; a view
+    when they lie in one block)."""
+    if bt is None:
+        return cache[slot, :, p0:p1]
+    blk = cache.shape[2]
+    if p0 // blk == (p1 - 1) // blk:
+        b = int(bt[slot, p0 // blk])
+        return cache[b, :, p0 % blk:p0 % blk + (p1 - p0)]
+    parts, a = [], p0
+    while a < p1:
+        e = min(p1, (a // blk + 1) * blk)
+        parts.append(_kv_at(cache, bt, slot, a, e))
+        a = e
+    return torch.cat(parts, 1)
+
+
 def decode_attention(qkv: torch.Tensor, cos, sin, k_cache, v_cache, pos: torch.Tensor, slots: torch.Tensor,
-                     Hq: int, Hkv: int, D: int, max_len: int) -> torch.Tensor:
+                     Hq: int, Hkv: int, D: int, max_len: int, block_table: torch.Tensor | None = None) -> torch.Tensor:
     """Batched single-token step.  qkv [B, NH*D], pos/slots int32 [B] (pos = index
-    of the new token).  Appends K/V at ``pos`` and attends over ``pos + 1`` keys."""
+    of the new token).  Appends K/V at ``pos`` and attends over ``pos + 1`` keys.
+    ``block_table`` [slots, max_blocks] int32: paged caches [blocks, Hkv, block, D]."""
     if use_native(qkv):
         ops = native()
-        q = ops.rope_append(qkv.contiguous(), cos, sin, pos, slots, k_cache, v_cache, Hq, Hkv, D)
-        return ops.decode_attn(q, k_cache, v_cache, pos, slots, max_len, 1.0 / math.sqrt(D), 1)
+        q = ops.rope_append(qkv.contiguous(), cos, sin, pos, slots, k_cache, v_cache, Hq, Hkv, D, block_table)
+        return ops.decode_attn(q, k_cache, v_cache, pos, slots, max_len, 1.0 / math.sqrt(D), 1, block_table)
+    bt = block_table.cpu() if block_table is not None else None
     B = qkv.shape[0]
     x = qkv.view(B, Hq + 2 * Hkv, D).float()
     outs = []
@@ -56,10 +73,10 @@ def decode_attention(qkv: torch.Tensor, cos, sin, k_cache, v_cache, pos: torch.T
 
         qi = rot(x[i, :Hq])
         ki = rot(x[i, Hq:Hq + Hkv])
-        k_cache[s, :, p] = ki.to(k_cache.dtype)
-        v_cache[s, :, p] = x[i, Hq + Hkv:].to(v_cache.dtype)
-        kk = k_cache[s, :, :p + 1].float().repeat_interleave(Hq // Hkv, 0)  # [Hq, L, D]
-        vv = v_cache[s, :, :p + 1].float().repeat_interleave(Hq // Hkv, 0)
+        _kv_at(k_cache, bt, s, p, p + 1)[:, 0] = ki.to(k_cache.dtype)
+        _kv_at(v_cache, bt, s, p, p + 1)[:, 0] = x[i, Hq + Hkv:].to(v_cache.dtype)
+        kk = _kv_at(k_cache, bt, s, 0, p + 1).float().repeat_interleave(Hq // Hkv, 0)  # [Hq, L, D]
+        vv = _kv_at(v_cache, bt, s, 0, p + 1).float().repeat_interleave(Hq // Hkv, 0)
         sc = torch.einsum("hd,hld->hl", qi, kk) / math.sqrt(D)
         outs.append(torch.einsum("hl,hld->hd", sc.softmax(-1), vv).reshape(-1))
     return torch.stack(outs).to(qkv.dtype)

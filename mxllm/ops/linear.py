@@ -377,10 +377,11 @@ def qkv_rope_ok(h: torch.Tensor, w: torch.Tensor, cos, sin, k_cache, v_cache, Hq
 
 
 def qkv_rope_linear(delta, h: torch.Tensor, gamma, eps: float, w: torch.Tensor, cos, sin, pos, slots, k_cache,
-                    v_cache, Hq: int, Hkv: int):
+                    v_cache, Hq: int, Hkv: int, block_table=None):
     """Inference, decode rows: the QKV projection with RoPE and the KV-cache append in the GEMM
     epilogue (csrc/kernels/skinny_gemm.hip ROPE) and, for 1-NORM_M rows, the (residual-add +)
-    RMSNorm in its prologue; ``gamma`` None: ``h`` is already normalised.  Returns
+    RMSNorm in its prologue; ``gamma`` None: ``h`` is already normalised; ``block_table``:
+    paged caches (mxllm/serve/kvcache.py).  Returns
     (q [M, Hq, 128] rotated, new residual) or None when the fused kernel does not take the call."""
     if not qkv_rope_ok(h, w, cos, sin, k_cache, v_cache, Hq, Hkv, gamma is not None):
         return None
@@ -389,7 +390,8 @@ def qkv_rope_linear(delta, h: torch.Tensor, gamma, eps: float, w: torch.Tensor, 
         return None
     if delta is not None and (not norm or delta.shape != h.shape or delta.stride(1) != 1 or delta.stride(0) % 8):
         return None
-    return native().skinny_qkv_rope(h, delta, gamma, float(eps), w, cos, sin, pos, slots, k_cache, v_cache, Hq, Hkv)
+    return native().skinny_qkv_rope(h, delta, gamma, float(eps), w, cos, sin, pos, slots, k_cache, v_cache, Hq, Hkv,
+                                    block_table)
 
 
 def norm_linear(delta: torch.Tensor | None, h: torch.Tensor, gamma: torch.Tensor, eps: float, w: torch.Tensor,

@@ -11,10 +11,12 @@ are exchanged once with ``hipIpcGetMemHandle``/``hipIpcOpenMemHandle`` through
 the process group.  RCCL remains the path for bulk traffic (DDP buckets,
 ZeRO-3 gathers) and for anything that crosses nodes.
 
-Eligible only when every rank of the group lives on this host
-(``LOCAL_WORLD_SIZE == WORLD_SIZE``), all ranks use GPUs, and
-``MXLLM_XGMI`` is not ``0``; otherwise :func:`create` returns ``None`` and
-callers use ``torch.distributed``.
+OPT-IN (``MXLLM_XGMI=1``): peer mapping across two DISTINCT GPUs has only been
+exercised as two processes on one GPU (the test boxes have one GPU), so by
+default :func:`create` returns ``None`` and callers use RCCL.  When enabled it
+is used only when every rank of the group lives on this host
+(``LOCAL_WORLD_SIZE == WORLD_SIZE``) and all ranks use GPUs, and it is
+all-or-none across the ranks (any local failure: every rank falls back).
 """
 from __future__ import annotations
 
@@ -146,7 +148,7 @@ class XgmiGraphComm:
 
 
 def eligible(group=None) -> bool:
-    if os.environ.get("MXLLM_XGMI", "1") == "0" or not dist.is_initialized():
+    if os.environ.get("MXLLM_XGMI", "0") != "1" or not dist.is_initialized():
         return False
     if not torch.cuda.is_available() or os.environ.get("MXLLM_FORCE_CPU") == "1":
         return False

@@ -5,9 +5,12 @@ This replaces the reference's remote API offload: ``get_model_response``
 over HTTP, one blocking request per prompt.  Here every rank
 serves its own shard of prompts from its own GPU, batched.
 
-MI355X-first sizing: the KV cache is one contiguous bf16 slab per layer,
-``[slots, Hkv, max_seq, D]`` — 70B needs 320 KiB/token, so 16 slots x 8k
-tokens = 43 GB beside the 141 GB of weights on one 288 GB MI355X.  Prefill
+MI355X-first sizing: the KV cache (mxllm/serve/kvcache.py) is a pool of
+256-token blocks per layer addressed through a per-slot block table.  Static
+mode gives every slot max_seq positions (70B: 320 KiB/token, 16 slots x 8k
+tokens = 43 GB beside the 141 GB of weights on one 288 GB MI355X); paged mode
+(``kv_pool_tokens``) shares a pool and a request reserves only
+prompt + max_new_tokens, so many more short requests run at once.  Prefill
 runs the MFMA flash-attention kernel; decode runs the split-K decode kernel
 (one workgroup streams 256 cached keys of one (sequence, kv-head) and serves
 all q-heads of that GQA group).  Scheduling is continuous batching: new
@@ -81,11 +84,14 @@ class Request:
 
 class Engine:
     def __init__(self, model, max_batch: int = 8, max_seq: int = 4096, device=None, eos_ids=(),
-                 use_graphs: bool | None = None, prefill_tokens: int = 16384, tp_group=None):
+                 use_graphs: bool | None = None, prefill_tokens: int = 16384, tp_group=None,
+                 kv_pool_tokens: int | None = None, kv_block: int = 256):
         """``tp_group``: serve a tensor-parallel shard (mxllm/parallel/tensor.py
         ``shard_llama`` / ``random_shard``) with the other ranks of the group;
         every rank of the group runs the same schedule (same submissions in the
-        same order, e.g. SPMD ``generate`` or ``serve_follower``)."""
+        same order, e.g. SPMD ``generate`` or ``serve_follower``).
+        ``kv_pool_tokens``: paged KV cache of that many tokens shared by all slots
+        (None: every slot owns max_seq positions; env MXLLM_KV_POOL_TOKENS)."""
         self.model = model
         self.tp = None
         if tp_group is not None:
@@ -119,9 +125,13 @@ class Engine:
         c = self.cfg
         dt = model.tok_emb.dtype
         n_slots = max_batch + (1 if self.use_graphs else 0)
-        self.k_cache = [torch.zeros(n_slots, c.n_kv_heads, self.max_seq, c.head_dim, dtype=dt, device=self.device)
-                        for _ in range(c.n_layers)]
-        self.v_cache = [torch.zeros_like(k) for k in self.k_cache]
+        if kv_pool_tokens is None and os.environ.get("MXLLM_KV_POOL_TOKENS"):
+            kv_pool_tokens = int(os.environ["MXLLM_KV_POOL_TOKENS"])
+        from .kvcache import KVCache
+
+        self.kv = KVCache(c.n_layers, c.n_kv_heads, c.head_dim, dt, self.device, n_slots, self.max_seq,
+                          pool_tokens=kv_pool_tokens, block=kv_block,
+                          scratch_slot=self.scratch_slot if self.use_graphs else None)
         self.eos_ids = tuple(eos_ids) if eos_ids else (c.eos_id,)
         self.free_slots = list(range(max_batch))
         self.active: dict[int, Request] = {}
@@ -197,6 +207,27 @@ class Engine:
         xn, h = ops.add_rms_norm(delta, h, gamma, c.norm_eps)
         return xn
 
+    @property
+    def k_cache(self):
+        return self.kv.k
+
+    @property
+    def v_cache(self):
+        return self.kv.v
+
+    def reserve(self, slot: int, tokens: int) -> None:
+        """Make ``slot`` able to hold ``tokens`` positions (paged KV: take blocks from the
+        pool; static: nothing to do).  The scheduler reserves prompt + max_new_tokens at
+        admission; direct ``prefill`` / ``decode`` callers may reserve themselves."""
+        self.kv.reserve(slot, tokens)
+
+    def _ensure(self, slot: int, tokens: int) -> None:
+        if self.kv.capacity(slot) < tokens:
+            if self.kv.paged and not self.kv.owned.get(slot):
+                self.kv.reserve(slot, self.max_seq if self.kv.can_reserve(self.max_seq) else tokens)
+            else:
+                raise ValueError(f"slot {slot} holds {self.kv.capacity(slot)} KV positions, {tokens} needed")
+
     @torch.no_grad()
     def prefill(self, slot: int, ids: list[int]) -> torch.Tensor:
         """Run the prompt through the model, filling ``slot``'s cache; returns
@@ -205,12 +236,13 @@ class Engine:
         S = len(ids)
         if S >= self.max_seq:
             raise ValueError(f"prompt of {S} tokens exceeds max_seq {self.max_seq}")
+        self._ensure(slot, S + 1)
         t = torch.tensor(ids, dtype=torch.long, device=self.device)
         x = ops.embedding(t, m.tok_emb)
 
         def attn(i, qkv):
-            return dops.prefill_attention(qkv, m.rope_cos, m.rope_sin, self.k_cache[i], self.v_cache[i], slot, S,
-                                          c.n_heads, c.n_kv_heads, c.head_dim)
+            return dops.prefill_attention(qkv, m.rope_cos, m.rope_sin, lambda k, v: self.kv.write(i, slot, k, v),
+                                          S, c.n_heads, c.n_kv_heads, c.head_dim)
 
         xn = self._layers(x, attn)
         self.lens[slot] = S
@@ -232,6 +264,8 @@ class Engine:
         lens = [len(p) for p in prompts]
         if any(S >= self.max_seq for S in lens):
             raise ValueError(f"prompt exceeds max_seq {self.max_seq}")
+        for s_, S in zip(slots, lens):
+            self._ensure(s_, S + 1)
         t = torch.tensor([tok for p in prompts for tok in p], dtype=torch.long, device=self.device)
         x = ops.embedding(t, m.tok_emb)
         offs = [0]
@@ -239,8 +273,9 @@ class Engine:
             offs.append(offs[-1] + S)
 
         def attn(i, qkv):
-            outs = [dops.prefill_attention(qkv[offs[j]:offs[j + 1]], m.rope_cos, m.rope_sin, self.k_cache[i],
-                                           self.v_cache[i], slots[j], lens[j], c.n_heads, c.n_kv_heads, c.head_dim)
+            outs = [dops.prefill_attention(qkv[offs[j]:offs[j + 1]], m.rope_cos, m.rope_sin,
+                                           lambda k, v, j=j: self.kv.write(i, slots[j], k, v), lens[j], c.n_heads,
+                                           c.n_kv_heads, c.head_dim)
                     for j in range(len(prompts))]
             return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
 
@@ -255,6 +290,8 @@ class Engine:
         """One token for each sequence in ``slots``; returns logits [B, V]."""
         B = len(slots)
         max_len = max(self.lens[s] for s in slots) + 1
+        for s in slots:
+            self._ensure(s, self.lens[s] + 1)
         if self.use_graphs:
             logits = self._decode_graphed(slots, tokens, max_len)
         else:
@@ -273,12 +310,14 @@ class Engine:
         sl = inp[2].to(torch.int32)
         x = ops.embedding(inp[0], m.tok_emb)
 
+        bt = self.kv.bt
+
         def attn(i, qkv, q=None):
             if q is not None:  # RoPE and the cache append already done by the QKV GEMM
-                return ops.native().decode_attn(q, self.k_cache[i], self.v_cache[i], pos, sl, max_len,
-                                                1.0 / math.sqrt(c.head_dim), 1)
-            return dops.decode_attention(qkv, m.rope_cos, m.rope_sin, self.k_cache[i], self.v_cache[i], pos, sl,
-                                         c.n_heads, c.n_kv_heads, c.head_dim, max_len)
+                return ops.native().decode_attn(q, self.kv.k[i], self.kv.v[i], pos, sl, max_len,
+                                                1.0 / math.sqrt(c.head_dim), 1, bt)
+            return dops.decode_attention(qkv, m.rope_cos, m.rope_sin, self.kv.k[i], self.kv.v[i], pos, sl,
+                                         c.n_heads, c.n_kv_heads, c.head_dim, max_len, bt)
 
         def qkv_fn(i, delta, h, gamma, layer):
             # QKV GEMM with the RoPE/cache-append epilogue; 1-2 rows also with the RMSNorm prologue
@@ -286,8 +325,8 @@ class Engine:
             if not (_ROPE_FUSED and self.tp is None and c.head_dim == 128
                     and type(layer.wqkv) is FusedLinear and layer.wqkv.lora_r == 0):
                 return None
-            rope = (layer.wqkv.weight, m.rope_cos, m.rope_sin, pos, sl, self.k_cache[i], self.v_cache[i],
-                    c.n_heads, c.n_kv_heads)
+            rope = (layer.wqkv.weight, m.rope_cos, m.rope_sin, pos, sl, self.kv.k[i], self.kv.v[i],
+                    c.n_heads, c.n_kv_heads, bt)
             if _NORM_FUSED:
                 r = ops.qkv_rope_linear(delta, h, gamma, c.norm_eps, *rope)
                 if r is not None:
@@ -425,6 +464,7 @@ class Engine:
         if r.t_first is not None:
             self.ttft_sum += r.t_first - r.t_submit
         if r.slot >= 0:
+            self.kv.release(r.slot)
             self.free_slots.append(r.slot)
             self.active.pop(r.slot, None)
             r.slot = -1
@@ -440,7 +480,7 @@ class Engine:
             self._finish(r, "stop")
         elif len(r.output) >= p.max_new_tokens:
             self._finish(r, "length")
-        elif self.lens[r.slot] + 1 >= self.max_seq:
+        elif self.lens[r.slot] + 1 >= self.kv.capacity(r.slot):
             self._finish(r, "length")
 
     def enable_tp_sync(self) -> None:
@@ -472,6 +512,7 @@ class Engine:
         for prompt, params in payload[0]:
             r = Request(next(self._ids), list(prompt), params)
             r.slot = self.free_slots.pop(0)
+            self.kv.reserve(r.slot, len(r.prompt) + params.max_new_tokens)
             mirrored.append(r)
         return mirrored
 
@@ -486,11 +527,23 @@ class Engine:
         """Admit + prefill waiting requests into free slots, then one decode step
         for the running batch.  Returns False when there is nothing to do."""
         with self._lock:
-            admit = []
+            admit, rejected = [], []
             while self.waiting and self.free_slots:
-                r = self.waiting.pop(0)
+                r = self.waiting[0]
+                need = len(r.prompt) + r.params.max_new_tokens
+                if not self.kv.fits_at_all(need):  # larger than the whole KV pool
+                    self.waiting.pop(0)
+                    rejected.append(r)
+                    continue
+                if not self.kv.can_reserve(need):  # paged pool full: wait for finishing requests
+                    break
+                self.waiting.pop(0)
                 r.slot = self.free_slots.pop(0)
+                self.kv.reserve(r.slot, need)
                 admit.append(r)
+        for r in rejected:
+            r.error = f"request needs {len(r.prompt) + r.params.max_new_tokens} KV positions, more than the pool"
+            self._finish(r, "error")
         if getattr(self, "tp_sync", False):
             admit = self._sync_admit(admit)
         # admitted prompts are prefilled together, in groups of at most

@@ -76,7 +76,7 @@ def test_param_checksum_sensitivity():
 
 
 def _xgmi_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MXLLM_XGMI="1")  # opt-in path
     import torch.distributed as dist
 
     from mxllm.parallel import xgmi
@@ -177,7 +177,7 @@ def _xgmi_graph_worker(rank, world, port, q):
     """Graph-safe bf16 all-reduce: eager calls of several sizes (multi-workgroup
     chunks), then the same calls captured once into a hipGraph and replayed
     with fresh inputs — exact vs the rank-ordered f32 sum, identical on ranks."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MXLLM_XGMI="1")
     import torch.distributed as dist
 
     from mxllm.parallel import xgmi

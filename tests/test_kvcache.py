@@ -1,0 +1,123 @@
+"""Paged KV cache (mxllm/serve/kvcache.py; VERDICT r2 missing #5).
+
+CPU: a paged engine (shared pool, 256-token blocks handed out per request)
+generates exactly what the static engine generates, the scheduler holds
+requests back while the pool is full and admits them as others finish, requests
+larger than the whole pool fail cleanly, and blocks are returned.
+GPU: the HIP decode kernels (RoPE + cache append, split-K decode attention, the
+fused QKV GEMM epilogue) on a SCATTERED block table match the contiguous cache
+bit for bit, and the graphed paged engine matches the static one.
+"""
+import pytest
+import torch
+
+from mxllm.models import Llama, get_config
+from mxllm.serve.engine import Engine
+from mxllm.serve.kvcache import KVCache
+
+
+def _model(device="cpu"):
+    torch.manual_seed(0)
+    return Llama(get_config("tiny"), device=device, seed=0).eval()
+
+
+def test_kvcache_write_gather_roundtrip():
+    kv = KVCache(2, 2, 32, torch.float32, "cpu", n_slots=3, max_seq=1000, pool_tokens=2048)
+    kv.reserve(1, 700)
+    kv.reserve(0, 300)
+    assert kv.capacity(1) == 768 and kv.capacity(0) == 512 and kv.free_blocks == 8 - 3 - 2
+    k = torch.randn(2, 600, 32)
+    v = torch.randn(2, 600, 32)
+    kv.write(1, 1, k, v)
+    gk, gv = kv.gather(1, 1, 600)
+    assert torch.equal(gk, k) and torch.equal(gv, v)
+    kv.release(1)
+    assert kv.free_blocks == 6
+    kv.reserve(2, 5000)  # capped at max_seq: 4 blocks
+    assert kv.capacity(2) == 1000 and kv.free_blocks == 2
+    with pytest.raises(RuntimeError):
+        kv.reserve(1, 1000)  # 4 more blocks: the pool is exhausted
+
+
+def test_paged_engine_matches_static():
+    m = _model()
+    prompts = [[i, i + 3, i + 7, 11] * (1 + i % 3) for i in range(1, 8)]
+    static = Engine(m, max_batch=4, max_seq=512)
+    paged = Engine(m, max_batch=4, max_seq=512, kv_pool_tokens=1024)  # 4 blocks: at most 4 requests of <256
+    a = static.generate(prompts, max_new_tokens=6)
+    b = paged.generate(prompts, max_new_tokens=6)
+    assert a == b
+    assert paged.kv.free_blocks == 4  # every block returned
+
+
+def test_paged_pool_limits_concurrency_and_rejects_oversized():
+    m = _model()
+    eng = Engine(m, max_batch=8, max_seq=1024, kv_pool_tokens=512)  # 2 blocks of 256
+    reqs = [eng.submit([1, 2, 3, 4], None) for _ in range(5)]
+    big = eng.submit(list(range(1, 300)), None)  # 299 + 64 new tokens -> 2 blocks: fits the pool
+    huge = eng.submit(list(range(1, 600)), None)  # 599 + 64 -> 3 blocks > pool of 2
+    peak = 0
+    while not all(r.done.is_set() for r in reqs + [big, huge]):
+        eng.step()
+        peak = max(peak, len(eng.active))
+    assert peak <= 2  # the pool, not the 8 slots, bounds concurrency
+    assert all(r.finish_reason in ("length", "stop") for r in reqs + [big])
+    assert huge.finish_reason == "error" and "pool" in huge.error
+    assert eng.kv.free_blocks == 2
+
+
+@pytest.mark.gpu
+def test_decode_kernels_on_scattered_blocks_match_contiguous(gpu):
+    from mxllm.ops import decode as dops
+    from mxllm.ops import native
+
+    Hq, Hkv, D, B, blk = 32, 8, 128, 3, 256
+    L = [700, 1, 1022]  # tokens already cached per sequence (+2 appended below stay inside 4 blocks)
+    maxb = 4
+    torch.manual_seed(0)
+    cont_k = torch.randn(B, Hkv, maxb * blk, D, device=gpu).bfloat16()
+    cont_v = torch.randn(B, Hkv, maxb * blk, D, device=gpu).bfloat16()
+    # the same rows in a scattered pool of 16 blocks
+    perm = torch.randperm(16)[:B * maxb].view(B, maxb).int()
+    pk = torch.zeros(16, Hkv, blk, D, device=gpu, dtype=torch.bfloat16)
+    pv = torch.zeros_like(pk)
+    for b in range(B):
+        for j in range(maxb):
+            pk[perm[b, j]] = cont_k[b, :, j * blk:(j + 1) * blk]
+            pv[perm[b, j]] = cont_v[b, :, j * blk:(j + 1) * blk]
+    bt = perm.to(gpu)
+    m = Llama(get_config("tiny-d128"), device=gpu, seed=1)  # its head_dim-128 RoPE tables
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=gpu).bfloat16()
+    pos = torch.tensor(L, device=gpu, dtype=torch.int32)
+    slots = torch.arange(B, device=gpu, dtype=torch.int32)
+    o_c = dops.decode_attention(qkv, m.rope_cos, m.rope_sin, cont_k, cont_v, pos, slots, Hq, Hkv, D, 1024)
+    o_p = dops.decode_attention(qkv, m.rope_cos, m.rope_sin, pk, pv, pos, slots, Hq, Hkv, D, 1024, bt)
+    assert torch.equal(o_c, o_p)
+    for b in range(B):  # the appended rows landed in the right block
+        j, r = divmod(L[b], blk)
+        assert torch.equal(pk[perm[b, j], :, r], cont_k[b, :, L[b]])
+        assert torch.equal(pv[perm[b, j], :, r], cont_v[b, :, L[b]])
+    # the fused QKV GEMM epilogue (RoPE + append) on the block table
+    w = torch.randn((Hq + 2 * Hkv) * D, 512, device=gpu).bfloat16() * 0.05
+    h = torch.randn(B, 512, device=gpu).bfloat16()
+    q_c, _ = native().skinny_qkv_rope(h, None, None, 1e-5, w, m.rope_cos, m.rope_sin, pos + 1, slots, cont_k,
+                                      cont_v, Hq, Hkv)
+    q_p, _ = native().skinny_qkv_rope(h, None, None, 1e-5, w, m.rope_cos, m.rope_sin, pos + 1, slots, pk, pv, Hq,
+                                      Hkv, bt)
+    assert torch.equal(q_c, q_p)
+    for b in range(B):
+        j, r = divmod(L[b] + 1, blk)
+        assert torch.equal(pk[perm[b, j], :, r], cont_k[b, :, L[b] + 1])
+
+
+@pytest.mark.gpu
+def test_paged_engine_matches_static_gpu(gpu):
+    m = Llama(get_config("tiny-d128"), device=gpu, seed=2).eval()
+    prompts = [list(range(1 + i, 40 + 37 * i)) for i in range(6)]
+    static = Engine(m, max_batch=4, max_seq=1024)
+    paged = Engine(m, max_batch=4, max_seq=1024, kv_pool_tokens=1536)
+    assert paged.use_graphs
+    a = static.generate(prompts, max_new_tokens=12)
+    b = paged.generate(prompts, max_new_tokens=12)
+    assert a == b
+    assert paged.kv.free_blocks == 6
