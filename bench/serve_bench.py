@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--top-p", type=float, default=1.0, help="e2e requests: nucleus sampling (with --temperature)")
     ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--kv-pool-tokens", type=int, default=None,
+                    help="paged KV cache shared by all slots (default: every slot owns max_seq positions)")
     ap.add_argument("--tp-shard-proxy", type=int, default=0,
                     help="one GPU: run rank 0's TP-N shard without the collectives (per-GPU compute floor)")
     a = ap.parse_args()
@@ -89,7 +91,7 @@ def main():
         sum(b.numel() * b.element_size() for n, b in model.named_buffers() if n.endswith((".q", ".scale")))
     bmax = max(int(b) for b in a.batches.split(","))
     max_seq = max(a.prompt_len, a.ctx + a.decode_steps, a.e2e_prompt_len + a.new_tokens) + 8
-    eng = Engine(model, max_batch=max(bmax, 1), max_seq=max_seq, tp_group=tp_group)
+    eng = Engine(model, max_batch=max(bmax, 1), max_seq=max_seq, tp_group=tp_group, kv_pool_tokens=a.kv_pool_tokens)
     g = torch.Generator().manual_seed(0)
 
     def prompt(n):
@@ -120,6 +122,7 @@ def main():
     for bs in [int(b) for b in a.batches.split(",")]:
         slots = list(range(bs))
         for s in slots:
+            eng.reserve(s, a.ctx + 4 * a.decode_steps + 8)  # paged KV: this slot's blocks (static: no-op)
             eng.lens[s] = a.ctx
         tok = torch.randint(0, full_cfg.vocab_size, (bs,), generator=g)
         for _ in range(3):  # capture + warm
@@ -152,6 +155,7 @@ def main():
                 out.setdefault("decode_plus_sampling", {})[mode] = {"batch": bs, "ms_per_step": round(1e3 * dt2, 3)}
         for s in slots:
             eng.lens[s] = 0
+            eng.kv.release(s)
 
     # ---- end-to-end continuous batching
     if a.requests > 0:
@@ -170,7 +174,10 @@ def main():
                       "max_batch": eng2.max_batch, "wall_s": round(dt, 3),
                       "output_tokens_per_s": round(ntok / dt, 1),
                       "total_tokens_per_s": round((ntok + a.requests * a.e2e_prompt_len) / dt, 1),
-                      "mean_ttft_ms": round(1e3 * (eng2.ttft_sum - ttft0) / max(1, eng2.finished - f0), 1)}
+                      "mean_ttft_ms": round(1e3 * (eng2.ttft_sum - ttft0) / max(1, eng2.finished - f0), 1),
+                      "kv_cache": ({"paged": True, "pool_tokens": a.kv_pool_tokens, "block": eng2.kv.block,
+                                    "gb": round(eng2.kv.nbytes() / 1e9, 2)} if eng2.kv.paged else
+                                   {"paged": False, "gb": round(eng2.kv.nbytes() / 1e9, 2)})}
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
