@@ -194,6 +194,7 @@ class Unit:
         self.gbuf: torch.Tensor | None = None  # gathered-size bf16 gradient buffer (backward only)
         self.seen: set[int] = set()
         self.reduced = False  # this micro-batch's gradient already handed to the reduce-scatter
+        self.grad_written = False  # grad_shard written this step (the next write of the step accumulates)
         self.n_trainable = len(self.params)
         self.device = None
         self.dtype = None
@@ -254,7 +255,9 @@ class Unit:
         # honours the fresh flag; the CPU reference ops accumulate through autograd
         fresh = ops.use_native(self.shard)
         if self.direct():
-            self.gbuf = self.grad_shard  # zero past the parameters (AdamW clears it every step)
+            self.gbuf = self.grad_shard  # its pad past the parameters is never written: stays zero
+            if first and not fresh:
+                self.gbuf.zero_()  # CPU reference ops accumulate through autograd
             fresh = fresh and first
         elif fresh:
             self.gbuf = torch.empty(self.full_numel, dtype=self.gdt, device=self.device)
@@ -506,17 +509,24 @@ class Zero3Trainer:
 
     def _reduce(self, u: Unit):
         work, out, fold = u.reduce_async(self._first)
-        self._inflight.append((u, work, out if fold else None))
+        # the first write of a step overwrites grad_shard (AdamW does not clear it): the
+        # reduce-scatter / direct GEMM output lands in it, or the first fold is a copy
+        first_write = not u.grad_written
+        u.grad_written = True
+        self._inflight.append((u, work, out if fold else None, first_write))
         self._done(u)
         while len(self._inflight) > self.max_inflight:
             self._drain_one()
 
     def _drain_one(self):
-        u, work, out = self._inflight.popleft()
+        u, work, out, first_write = self._inflight.popleft()
         if work is not None:
             work.wait()  # the compute stream waits for the RCCL stream; the host does not
         if out is not None:
-            u.grad_shard.add_(out)  # fp32 += shard (AdamW zeroes the shard every step)
+            if first_write:
+                u.grad_shard.copy_(out)
+            else:
+                u.grad_shard.add_(out)
 
     def _drain(self):
         while self._inflight:
@@ -629,7 +639,11 @@ class Zero3Trainer:
         if work is not None:
             work.wait()
         if fold:
-            norms.grad_shard.add_(out)
+            norms.grad_shard.copy_(out)
+        for u in self.units[1:]:
+            if not u.grad_written:  # no gradient at all this step (unused): a zero update input
+                u.grad_shard.zero_()
+            u.grad_written = False
         scale = 1.0 / (self.world * n)
         self.step_num += 1
         o = self.opt
@@ -643,7 +657,7 @@ class Zero3Trainer:
             gscale = scale
         ops.adamw_step_(self.master, self.grads, self.m, self.v, self.shard_params, lr=o.lr_at(self.step_num),
                         beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay, step=self.step_num,
-                        grad_scale=gscale, zero_grad=True)  # shard grads cleared in the same pass
+                        grad_scale=gscale, zero_grad=False)  # every shard is overwritten by the next step
         self._refresh_resident()
         return total / n
 
