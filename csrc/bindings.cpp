@@ -516,6 +516,49 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   return out;
 }
 
+// The split-K partials without the combine: (part_ml [B, Hq, nsplit, 2], part_o [B, Hq, nsplit, D]),
+// merged by the o-projection's prologue (skinny_merge_linear).  D = 128.
+std::tuple<at::Tensor, at::Tensor> decode_attn_partials(const at::Tensor& q, const at::Tensor& k_cache,
+                                                        const at::Tensor& v_cache, const at::Tensor& lens,
+                                                        const c10::optional<at::Tensor>& slots, int64_t max_len,
+                                                        double scale, int64_t len_off,
+                                                        const c10::optional<at::Tensor>& block_table) {
+  check_bf16(q, "q");
+  MX_CHECK(lens.scalar_type() == at::kInt, "lens int32");
+  const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
+  MX_CHECK(D == 128, "decode_attn_partials: head_dim 128");
+  const int64_t Hkv = k_cache.size(1), max_seq = k_cache.size(2);
+  DevGuard g(q.device());
+  const KvPages pg = kv_pages(block_table, k_cache);
+  const int64_t cap = pg.bt ? (int64_t)pg.maxb * max_seq : max_seq;
+  const int64_t nsplit = std::max<int64_t>(1, (std::min(max_len, cap) + 255) / 256);
+  auto ml = at::empty({B, Hq, nsplit, 2}, q.options().dtype(at::kFloat));
+  auto po = at::empty({B, Hq, nsplit, D}, q.options().dtype(at::kFloat));
+  const int32_t* sl = nullptr;
+  if (slots.has_value()) sl = slots->data_ptr<int32_t>();
+  MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), (int)len_off, sl, ml.data_ptr<float>(),
+                       po.data_ptr<float>(), nullptr, (int)B, (int)Hq, (int)Hkv, (int)D, (int)max_seq, (int)nsplit,
+                       (float)scale, pg.bt, pg.maxb, cur_stream()));
+  return {ml, po};
+}
+
+// y [M, N] = merge(part_ml, part_o) . W^T (decode o-projection with the split merge in the prologue)
+at::Tensor skinny_merge_linear(const at::Tensor& ml, const at::Tensor& po, const at::Tensor& w) {
+  MX_CHECK(ml.is_cuda() && ml.scalar_type() == at::kFloat && ml.is_contiguous() && ml.dim() == 4 && ml.size(3) == 2,
+           "part_ml f32 [M, Hq, nsplit, 2]");
+  MX_CHECK(po.is_cuda() && po.scalar_type() == at::kFloat && po.is_contiguous() && po.dim() == 4 &&
+               po.size(0) == ml.size(0) && po.size(1) == ml.size(1) && po.size(2) == ml.size(2) && po.size(3) == 128,
+           "part_o f32 [M, Hq, nsplit, 128]");
+  MX_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1, "w bf16 [N, K] rows");
+  const int64_t M = ml.size(0), K = ml.size(1) * 128, N = w.size(0);
+  MX_CHECK(w.size(1) == K, "w [N, Hq * 128]");
+  DevGuard g(w.device());
+  auto y = at::empty({M, N}, w.options());
+  MX_OK(mx_skinny_merge_gemm(ml.data_ptr<float>(), po.data_ptr<float>(), (int)ml.size(2), bf(w), w.stride(0), bfm(y),
+                             N, (int)M, (int)N, (int)K, cur_stream()));
+  return y;
+}
+
 at::Tensor sample(const at::Tensor& logits, double temperature, int64_t seed, int64_t step) {
   MX_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "logits [B, V] contiguous GPU");
   MX_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16/f32");
@@ -814,6 +857,8 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
   m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D, Tensor? block_table=None) -> Tensor");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0, Tensor? block_table=None) -> Tensor");
+  m.def("decode_attn_partials(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0, Tensor? block_table=None) -> (Tensor, Tensor)");
+  m.def("skinny_merge_linear(Tensor ml, Tensor po, Tensor w) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");
   m.def("sample_rows(Tensor logits, Tensor temps, Tensor top_p, Tensor top_k, Tensor seeds, Tensor steps) -> Tensor");
   m.def("sample_temp_rows(Tensor logits, Tensor temps, Tensor seeds, Tensor steps) -> Tensor");
@@ -851,6 +896,8 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("attn_bwd_ablate", &attn_bwd_ablate);
   m.impl("rope_append", &rope_append);
+  m.impl("decode_attn_partials", &decode_attn_partials);
+  m.impl("skinny_merge_linear", &skinny_merge_linear);
   m.impl("decode_attn", &decode_attn);
   m.impl("sample", &sample);
   m.impl("sample_rows", &sample_rows);

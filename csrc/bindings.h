@@ -83,6 +83,8 @@ int mx_skinny_rope_gemm(const uint16_t* h, int64_t ldh, int norm, const uint16_t
                         const uint16_t* gamma, float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw,
                         const float* cosb, const float* sinb, const int32_t* pos, const int32_t* slots, uint16_t* q,
                         uint16_t* kc, uint16_t* vc, int Hq, int Hkv, int max_seq, const int32_t* bt, int maxb, int M, int K, hipStream_t stream);
+int mx_skinny_merge_gemm(const float* ml, const float* po, int nsplit, const uint16_t* w, int64_t ldw, uint16_t* y,
+                         int64_t ldy, int M, int N, int K, hipStream_t stream);
 int mx_skinny_norm_gemm(const uint16_t* h, int64_t ldh, const uint16_t* delta, int64_t ldd, const uint16_t* gamma,
                         float eps, uint16_t* h_out, const uint16_t* w, int64_t ldw, uint16_t* y, int64_t ldy, int M,
                         int N, int K, int swiglu, hipStream_t stream);

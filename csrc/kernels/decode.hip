@@ -538,12 +538,13 @@ extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint1
   if (bt && max_seq % kSplit) return -1;  // a split must lie inside one block
   dim3 grid(nsplit, Hkv, B);
   const float sl = scale * 1.4426950408889634f;
-  if (D == 128) {
+  if (D == 128) {  // out == nullptr: partials only (the o-projection merges them: skinny_gemm.hip MERGE)
     decode_attn_mfma_kernel<<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv,
                                                       max_seq, nsplit, sl, bt, maxb);
-    decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
+    if (out) decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
     return (int)hipGetLastError();
   }
+  if (!out) return -1;
 #define DA(DD)                                                                                                  \
   decode_attn_kernel<DD><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv, \
                                                    max_seq, nsplit, sl, bt, maxb);                              \

@@ -98,6 +98,75 @@ __device__ __forceinline__ void dfuse_norm_rows(const uint16_t* __restrict__ X, 
   __syncthreads();
 }
 
+// Split-K decode attention partials (decode.hip decode_attn_*: per (row, q-head, split) the
+// running max / sum in part_ml [M, Hq, nsplit, 2] and the unnormalised output in part_o
+// [M, Hq, nsplit, 128]) merged into the attention output rows xs [M, Hq * 128] (LDS) -- the
+// o-projection GEMM's X -- with decode_combine_kernel's arithmetic and order (same bits).
+struct SkMerge {
+  const float* ml;
+  const float* po;
+  int nsplit;
+};
+
+__device__ __forceinline__ void dfuse_merge_rows(int M, int K, const SkMerge& mg, uint16_t* xs) {
+  const int ns = mg.nsplit;
+  for (int e = threadIdx.x * 8; e < M * K; e += blockDim.x * 8) {
+    const int m = e / K, col = e % K, hq = col >> 7, d0 = col & 127;
+    const int64_t bh = (int64_t)m * (K >> 7) + hq;
+    const float* ml = mg.ml + bh * ns * 2;
+    u16x8 out;
+    if (ns <= 8) {
+      float mv[8], lv[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bool on = s < ns;
+        mv[s] = on ? ml[2 * s] : -INFINITY;
+        lv[s] = on ? ml[2 * s + 1] : 0.f;
+      }
+      float Mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) Mx = fmaxf(Mx, mv[s]);
+      float wgt[8], L = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        wgt[s] = mv[s] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mv[s] - Mx);
+        if (mv[s] != -INFINITY) L += wgt[s] * lv[s];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          if (s < ns && mv[s] != -INFINITY) {
+            const f32x4 ov = *reinterpret_cast<const f32x4*>(mg.po + (bh * ns + s) * 128 + d0 + j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] += wgt[s] * ov[i];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[j + i] = f2bf(L > 0.f ? acc[i] / L : 0.f);
+      }
+    } else {
+      float Mx = -INFINITY;
+      for (int s = 0; s < ns; ++s) Mx = fmaxf(Mx, ml[2 * s]);
+      float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < ns; ++s) {
+        const float mm = ml[2 * s];
+        if (mm == -INFINITY) continue;
+        const float wg = __builtin_amdgcn_exp2f(mm - Mx);
+        L += wg * ml[2 * s + 1];
+        const float* op = mg.po + (bh * ns + s) * 128 + d0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += wg * op[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) out[i] = f2bf(L > 0.f ? acc[i] / L : 0.f);
+    }
+    *reinterpret_cast<u16x8*>(xs + e) = out;
+  }
+  __syncthreads();
+}
+
 // Epilogues.  Lane (c, g) of the reducing wave holds v = channels 4g..4g+3 (final f32 values,
 // weight scale applied) of token m = c (+ 16 mb); the paired channels are in lane ^ 32.  Every
 // lane of the wave must call (the pairing is a lane shuffle).

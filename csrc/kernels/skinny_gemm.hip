@@ -44,14 +44,17 @@ __device__ __forceinline__ f32x4 mfma16_sk(const u16x8& a, const u16x8& b, const
 // MB: 16-token blocks (1 or 2); X rows >= M are clamped to M-1 and discarded.
 // NC: 16-channel groups per workgroup: each X fragment then feeds NC MFMAs, so X traffic per
 // streamed weight byte drops NC-fold (it equals the weight traffic at 16 tokens with NC = 1).
-template <int MB, int NC, bool SWO = false, bool NORM = false, bool ROPE = false>
+template <int MB, int NC, bool SWO = false, bool NORM = false, bool ROPE = false, bool MERGE = false>
 __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx,
                                                           const uint16_t* __restrict__ W, int64_t ldw,
                                                           uint16_t* __restrict__ Y, int64_t ldy, int M, int K,
-                                                          int F = 0, SkNorm na = {}, SkRope rp = {}) {
+                                                          int F = 0, SkNorm na = {}, SkRope rp = {},
+                                                          SkMerge mg = {}) {
   static_assert(!SWO || NC == 1, "SwiGLU epilogue: one channel group");
   static_assert(!ROPE || (NC == 1 && !SWO), "RoPE epilogue: one channel group");
   static_assert(!NORM || (MB == 1 && NC == 1), "fused RMSNorm: <= 16 rows, one channel group");
+  static_assert(!MERGE || (MB == 1 && NC == 1 && !NORM && !SWO && !ROPE), "fused split merge: plain GEMM rows");
+  constexpr bool LDSX = NORM || MERGE;  // X rows built in LDS by the prologue
   constexpr int NW = 8, UNR = NC == 1 ? 8 : 4;
   __shared__ f32x4 red[NW][NC][MB][64];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -72,7 +75,7 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
   // NORM: the first UNR chunks' weight loads go out before the prologue, so the weight stream's
   // latency overlaps the RMSNorm instead of following it
   u16x8 apre[UNR][NC][2];
-  if constexpr (NORM) {
+  if constexpr (LDSX) {
     if (nit >= UNR) {
 #pragma unroll
       for (int u = 0; u < UNR; ++u)
@@ -83,11 +86,15 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
         }
     }
   }
-  if constexpr (NORM) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [M, K] normalised rows
-    __shared__ float nscr[2][4];
-    __shared__ float nrs[4];
-    dfuse_norm_rows(X, ldx, M, K, na, xs, nscr, nrs);
+  if constexpr (LDSX) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [M, K] normalised / merged rows
+    if constexpr (NORM) {
+      __shared__ float nscr[2][4];
+      __shared__ float nrs[4];
+      dfuse_norm_rows(X, ldx, M, K, na, xs, nscr, nrs);
+    } else {
+      dfuse_merge_rows(M, K, mg, xs);
+    }
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) xr[mb] = xs + (int64_t)min(mb * 16 + c, M - 1) * K + (int64_t)w * kq + 16 * g;
   } else {
@@ -122,7 +129,7 @@ __global__ void __launch_bounds__(512) skinny_gemm_kernel(const uint16_t* __rest
       }
   };
   int it = 0;
-  if constexpr (NORM) {
+  if constexpr (LDSX) {
     if (nit >= UNR) {  // first block: weights prefetched above, X fragments from LDS
       u16x8 b[UNR][MB][2];
 #pragma unroll
@@ -208,6 +215,23 @@ extern "C" int mx_skinny_rope_gemm(const uint16_t* h, int64_t ldh, int norm, con
     skinny_gemm_kernel<1, 1, false, false, true><<<N / 16, 512, 0, stream>>>(h, ldh, w, ldw, nullptr, 0, M, K, 0,
                                                                                SkNorm{}, rp);
   }
+  return (int)hipGetLastError();
+}
+
+// y[M, N] = merge(split partials) . W^T: the decode o-projection with decode.hip's split-K
+// attention merge (decode_combine_kernel) in its prologue -- every workgroup rebuilds the
+// attention output rows [M, Hq * 128] in LDS from part_ml [M, Hq, nsplit, 2] / part_o
+// [M, Hq, nsplit, 128] (same bits as the combine kernel).  Saves the combine launch of every
+// layer.  M <= 4, M * K <= 32768, K = Hq * 128 (% 512), N % 16 == 0.
+extern "C" int mx_skinny_merge_gemm(const float* ml, const float* po, int nsplit, const uint16_t* w, int64_t ldw,
+                                    uint16_t* y, int64_t ldy, int M, int N, int K, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 4 || (int64_t)M * K > 32768 || N % 16 || K % 512 || ldw % 8 || ldy % 4 || ldw < K || ldy < N ||
+      nsplit < 1)
+    return -1;
+  const SkMerge mg{ml, po, nsplit};
+  skinny_gemm_kernel<1, 1, false, false, false, true><<<N / 16, 512, (size_t)M * K * 2, stream>>>(
+      nullptr, 0, w, ldw, y, ldy, M, K, 0, SkNorm{}, SkRope{}, mg);
   return (int)hipGetLastError();
 }
 

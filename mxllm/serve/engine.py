@@ -46,6 +46,8 @@ from ..ops import decode as dops
 _SWIGLU_FUSED = os.environ.get("MXLLM_SWIGLU_FUSED", "1") != "0"  # A/B switch (bench/serve_bench.py)
 _NORM_FUSED = os.environ.get("MXLLM_NORM_FUSED", "1") != "0"  # A/B switch: RMSNorm in the decode GEMM prologue
 _ROPE_FUSED = os.environ.get("MXLLM_ROPE_FUSED", "1") != "0"  # A/B switch: RoPE + cache append in the QKV epilogue
+# A/B switch: the split-K attention merge in the o-projection GEMM's prologue (decode rows <= 4)
+_MERGE_FUSED = os.environ.get("MXLLM_MERGE_FUSED", "1") != "0"
 log = logging.getLogger("mxllm.engine")
 
 
@@ -194,7 +196,10 @@ class Engine:
             else:
                 qkv, h = self._norm_proj(delta, h, gamma, layer.wqkv, False)
                 o = attn_fn(i, qkv)
-            a = layer.wo(o)
+            if isinstance(o, tuple):  # split-K partials: merged in the o-projection's prologue
+                a = ops.native().skinny_merge_linear(o[0], o[1], layer.wo.weight)
+            else:
+                a = layer.wo(o)
             if self.tp is not None:  # row-parallel Wo: sum the heads' partial outputs
                 self.tp.all_reduce_(a)
             mid, h = self._norm_proj(a, h, layer.mlp_norm, layer.wgu, True)
@@ -311,9 +316,19 @@ class Engine:
         x = ops.embedding(inp[0], m.tok_emb)
 
         bt = self.kv.bt
+        B = inp.shape[1]
+        nsplit = (min(max_len, self.kv.maxb * self.kv.block) + 255) // 256
+        merge = _MERGE_FUSED and c.head_dim == 128 and B <= 4 and nsplit <= 16
 
         def attn(i, qkv, q=None):
             if q is not None:  # RoPE and the cache append already done by the QKV GEMM
+                wo = m.layers[i].wo
+                K = q.shape[1] * 128  # this rank's heads (tensor parallel: a shard)
+                if (merge and type(wo) is FusedLinear and wo.lora_r == 0 and wo.weight.shape[0] % 16 == 0
+                        and K % 512 == 0 and B * K <= 32768 and wo.weight.shape[1] == K):
+                    # partials only: the split merge runs in the o-projection's prologue
+                    return ops.native().decode_attn_partials(q, self.kv.k[i], self.kv.v[i], pos, sl, max_len,
+                                                             1.0 / math.sqrt(c.head_dim), 1, bt)
                 return ops.native().decode_attn(q, self.kv.k[i], self.kv.v[i], pos, sl, max_len,
                                                 1.0 / math.sqrt(c.head_dim), 1, bt)
             return dops.decode_attention(qkv, m.rope_cos, m.rope_sin, self.kv.k[i], self.kv.v[i], pos, sl,

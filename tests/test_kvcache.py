@@ -121,3 +121,25 @@ def test_paged_engine_matches_static_gpu(gpu):
     b = paged.generate(prompts, max_new_tokens=12)
     assert a == b
     assert paged.kv.free_blocks == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,ctx,Hq", [(1, 1000, 32), (3, 2100, 64), (4, 300, 32)])
+def test_merged_o_projection_matches_combine_then_gemm(gpu, B, ctx, Hq):
+    """decode_attn_partials + skinny_merge_linear (the split-K merge in the o-projection
+    GEMM's prologue) == decode_attn (separate combine kernel) + the decode GEMM, bit for bit."""
+    from mxllm.ops import native
+
+    Hkv, D = 8, 128
+    torch.manual_seed(1)
+    kc = torch.randn(B, Hkv, 4096, D, device=gpu).bfloat16()
+    vc = torch.randn(B, Hkv, 4096, D, device=gpu).bfloat16()
+    q = torch.randn(B, Hq, D, device=gpu).bfloat16()
+    lens = torch.tensor([ctx - 7 * b for b in range(B)], device=gpu, dtype=torch.int32)
+    slots = torch.arange(B, device=gpu, dtype=torch.int32)
+    w = torch.randn(4096, Hq * D, device=gpu).bfloat16() * 0.02
+    o = native().decode_attn(q, kc, vc, lens, slots, ctx + 1, D ** -0.5, 1)
+    ref = native().skinny_linear(o, w)
+    ml, po = native().decode_attn_partials(q, kc, vc, lens, slots, ctx + 1, D ** -0.5, 1)
+    y = native().skinny_merge_linear(ml, po, w)
+    assert torch.equal(y, ref)
