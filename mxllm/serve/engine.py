@@ -46,8 +46,11 @@ from ..ops import decode as dops
 _SWIGLU_FUSED = os.environ.get("MXLLM_SWIGLU_FUSED", "1") != "0"  # A/B switch (bench/serve_bench.py)
 _NORM_FUSED = os.environ.get("MXLLM_NORM_FUSED", "1") != "0"  # A/B switch: RMSNorm in the decode GEMM prologue
 _ROPE_FUSED = os.environ.get("MXLLM_ROPE_FUSED", "1") != "0"  # A/B switch: RoPE + cache append in the QKV epilogue
-# A/B switch: the split-K attention merge in the o-projection GEMM's prologue (decode rows <= 4)
-_MERGE_FUSED = os.environ.get("MXLLM_MERGE_FUSED", "1") != "0"
+# the split-K attention merge in the o-projection GEMM's prologue (decode rows <= 4): OFF by
+# default -- measured 8B decode, same box: batch 1 3.424 vs 3.433 ms (a wash), batch 4 4.113 vs
+# 3.841 ms (the prologue slows the weight stream more than the combine launch costs;
+# profiles/r3d_decode_merge_ab.md).  MXLLM_MERGE_FUSED=1 turns it on.
+_MERGE_FUSED = os.environ.get("MXLLM_MERGE_FUSED", "0") == "1"
 log = logging.getLogger("mxllm.engine")
 
 
