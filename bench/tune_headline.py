@@ -68,6 +68,21 @@ def main():
     from mxllm.parallel import runtime
 
     raw = a.out + ".raw.csv"
+    import threading
+    import time
+
+    t0 = time.time()
+
+    def heartbeat():  # tuning one large shape takes minutes: show progress (and stay alive)
+        while True:
+            time.sleep(20)
+            try:
+                n = len(torch.cuda.tunable.get_results())
+            except Exception:  # noqa: BLE001
+                n = -1
+            print(f"[tune] {time.time() - t0:.0f} s, {n} GEMM shapes tuned so far", flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     tun = torch.cuda.tunable
     tun.enable(True)
     tun.tuning_enable(True)
