@@ -31,6 +31,7 @@
 // reference src/distributed_inference.py:61-76); the math follows PEFT's LoRA.
 #include "common.h"
 #include <stdlib.h>
+#include <string.h>
 
 namespace mx {
 
@@ -158,6 +159,139 @@ __global__ void __launch_bounds__(256, 1) lora_xwt_kernel(const uint16_t* __rest
     for (int q = 0; q < 4; ++q) reinterpret_cast<float4*>(wp)[tid + 256 * q] = v[q];
     if (!fused_red) return;  // lora_xwt_reduce_kernel finishes
     if (!arrive_last(&g_xwt_cnt[mt], S, &s_last)) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[tid + 256 * q];
+      for (int sp = 1; sp < S; ++sp) {
+        const float4 t = reinterpret_cast<const float4*>(ws + ((int64_t)sp * mtiles + mt) * 4096)[tid + 256 * q];
+        s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
+      }
+      v[q] = s;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
+    uint2 o;
+    o.x = pack_bf16x2(alpha * v[q].x, alpha * v[q].y);
+    o.y = pack_bf16x2(alpha * v[q].z, alpha * v[q].w);
+    *reinterpret_cast<uint2*>(out + (int64_t)(mt * 64 + row) * ldo + col) = o;
+  }
+}
+
+// lora_xwt through LDS: the same product, with BOTH operands staged by LDS-DMA in
+// full 128-B lines (8 rows x 128 B per wave instruction) instead of fragment-shaped
+// register loads (16 rows x 64 B per instruction, which keep the texture path busy
+// ~2x for the same bytes).  Per wave: 2 stages x (X 8 KiB + V 8 KiB), its own
+// region, no workgroup barrier in the loop; the issuing wave's counted vmcnt orders
+// its ds_reads behind its DMA.  Image: 64 rows x 128 B, 16-B chunk ch of row r at
+// chunk position ch ^ (r & 7) — conflict-free for the ds_read_b128 fragment reads
+// (row c of a 16-row block, chunk 4 ks + g) under gfx950's ds_read_b128 lane groups.
+// grid (M/64, S), 256 threads; M % 64 == 0, K % 64 == 0; writes out[:, 0:64].
+__global__ void __launch_bounds__(256, 1) lora_xwt_lds_kernel(const uint16_t* __restrict__ X, int64_t ldx,
+                                                              const uint16_t* __restrict__ V, int64_t ldv,
+                                                              uint16_t* __restrict__ out, int64_t ldo,
+                                                              float* __restrict__ ws, int M, int K, int S,
+                                                              float alpha, int fused_red) {
+  constexpr int TB = 8192, STG = 16384, WREG = 2 * STG;
+  // ONE shared object (a second one can make hipcc drain vmcnt in the loop); the
+  // last-arriver flag lives in its tail
+  __shared__ __attribute__((aligned(16))) char smem[4 * WREG + 16];
+  int* s_last = reinterpret_cast<int*>(smem + 4 * WREG);
+  const int mtiles = M >> 6, mt = blockIdx.x, split = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb = K >> 6, nw = S * 4, gw = split * 4 + w;
+  const int b0 = (int)((int64_t)gw * nb / nw), b1 = (int)((int64_t)(gw + 1) * nb / nw);
+  char* wreg = smem + w * WREG;
+  const uint32_t wbase = lds_addr(wreg);
+  // DMA sources: lane -> row 8 q + (lane >> 3), LDS chunk position lane & 7 holds
+  // source chunk (lane & 7) ^ (row & 7)
+  const int lrow = lane >> 3, sch = (lane & 7) ^ lrow;
+  const uint16_t* xsrc = X + (int64_t)(mt * 64 + lrow) * ldx + 8 * sch;
+  const uint16_t* vsrc = V + (int64_t)lrow * ldv + 8 * sch;
+  auto issue = [&](int b, int s) {
+    const int k0 = b * 64;
+    char* xs = wreg + s * STG;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_global_load_lds((lgptr_t)(xsrc + (int64_t)(8 * q) * ldx + k0), (llptr_t)(xs + q * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_global_load_lds((lgptr_t)(vsrc + (int64_t)(8 * q) * ldv + k0), (llptr_t)(xs + TB + q * 1024),
+                                       16, 0, 0);
+  };
+  // fragment reads: row 16 i + c, chunk 4 ks + g  ->  position (g ^ (c & 7)) ^ 4 ks
+  const uint32_t rb0 = wbase + c * 128 + 16 * (g ^ (c & 7));
+  const uint32_t rb1 = wbase + c * 128 + 16 * ((g ^ (c & 7)) ^ 4);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto block = [&](auto SC, int b) {
+    constexpr int s = decltype(SC)::value;
+    if (b + 1 < b1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this block landed, the next may fly
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u16x8 xa[2][4], va[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xa[0][i] = rd128_off(rb0, s * STG + i * 2048);
+      xa[1][i] = rd128_off(rb1, s * STG + i * 2048);
+      va[0][i] = rd128_off(rb0, s * STG + TB + i * 2048);
+      va[1][i] = rd128_off(rb1, s * STG + TB + i * 2048);
+    }
+    lds_wait();
+    __builtin_amdgcn_sched_barrier(0);  // the MFMAs below must not be hoisted above the wait
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pin(xa[0][i]), pin(xa[1][i]), pin(va[0][i]), pin(va[1][i]);
+    }
+    if (b + 2 < b1) issue(b + 2, s);  // refill this stage (its reads have retired)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = lmfma(xa[ks][i], va[ks][j], acc[i][j]);
+  };
+  if (b0 < b1) issue(b0, 0);
+  if (b0 + 1 < b1) issue(b0 + 1, 1);
+  for (int b = b0; b < b1; b += 2) {
+    block(std::integral_constant<int, 0>{}, b);
+    if (b + 1 < b1) block(std::integral_constant<int, 1>{}, b + 1);
+  }
+  // 4 waves -> one 64 x 64 tile (each wave's own region: its DMA has drained)
+  float* rw = reinterpret_cast<float*>(wreg);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rw[(16 * i + 4 * g + e) * kRS + 16 * j + c] = acc[i][j][e];
+  __syncthreads();
+  float4 v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
+    float4 s = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(smem) + row * kRS + col);
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const float4 t = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(smem + ww * WREG) +
+                                                        row * kRS + col);
+      s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
+    }
+    v[q] = s;
+  }
+  if (S > 1) {
+    float* wp = ws + ((int64_t)split * mtiles + mt) * 4096;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) reinterpret_cast<float4*>(wp)[tid + 256 * q] = v[q];
+    if (!fused_red) return;  // lora_xwt_reduce_kernel finishes
+    if (!arrive_last(&g_xwt_cnt[mt], S, s_last)) return;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[tid + 256 * q];
@@ -442,9 +576,18 @@ extern "C" int mx_lora_xwt(const uint16_t* X, int64_t ldx, const uint16_t* V, in
   if (M % 64 || K % 64 || Vrows % 64 || M / 64 > kMaxTiles) return (int)hipErrorInvalidValue;
   const int mtiles = M / 64, S = lora_splits(mtiles, K / 64, 16);
   const int fused = lora_env("MXLLM_LORA_FUSED_RED", 0);
+  // LDS-staged kernel (16-B aligned rows required by its 16-B DMA pieces); the
+  // register-fragment kernel stays for A/B (MXLLM_LORA_XWT=reg)
+  const char* kv = getenv("MXLLM_LORA_XWT");  // read per call: an in-process A/B can flip it
+  const bool reg = kv && !strcmp(kv, "reg");
+  const bool lds = !reg && ((uintptr_t)X % 16 == 0) && ((uintptr_t)V % 16 == 0) && ldx % 8 == 0 && ldv % 8 == 0;
   for (int c0 = 0; c0 < Vrows; c0 += 64) {
-    lora_xwt_kernel<<<dim3(mtiles, S), 256, 0, stream>>>(X, ldx, V + (int64_t)c0 * ldv, ldv, out + c0, ldo, ws, M, K,
-                                                         S, alpha, fused);
+    if (lds)
+      lora_xwt_lds_kernel<<<dim3(mtiles, S), 256, 0, stream>>>(X, ldx, V + (int64_t)c0 * ldv, ldv, out + c0, ldo, ws,
+                                                               M, K, S, alpha, fused);
+    else
+      lora_xwt_kernel<<<dim3(mtiles, S), 256, 0, stream>>>(X, ldx, V + (int64_t)c0 * ldv, ldv, out + c0, ldo, ws, M,
+                                                           K, S, alpha, fused);
     if (S > 1 && !fused) lora_xwt_reduce_kernel<<<mtiles, 256, 0, stream>>>(ws, S, mtiles, out + c0, ldo, alpha);
   }
   return (int)hipGetLastError();

@@ -402,10 +402,14 @@ def test_quant_rows_e4m3(gpu):
     assert rel_err(q.view(torch.float8_e4m3fn).float() * s, xf) < 0.04
 
 
-@pytest.mark.parametrize("T,K,vrows", [(256, 512, 64), (256, 4096, 64), (4096, 1024, 128), (64, 192, 64)])
-def test_lora_xwt(gpu, T, K, vrows):
+@pytest.mark.parametrize("kern", ["lds", "reg"])
+@pytest.mark.parametrize("T,K,vrows", [(256, 512, 64), (256, 4096, 64), (4096, 1024, 128), (64, 192, 64),
+                                       (4096, 8192, 64)])
+def test_lora_xwt(gpu, T, K, vrows, kern, monkeypatch):
     """out[:, :vrows] = alpha x V^T into the tail of a padded buffer (S = 1 and the
-    ordered split reduction), columns past the tail untouched."""
+    ordered split reduction), columns past the tail untouched; both kernels: the
+    LDS-DMA-staged one (default) and the register-fragment one (MXLLM_LORA_XWT=reg)."""
+    monkeypatch.setenv("MXLLM_LORA_XWT", kern)
     torch.manual_seed(3)
     buf = torch.randn(T, K + vrows + 8, device=gpu, dtype=torch.bfloat16)
     x = buf[:, :K]
