@@ -1,7 +1,8 @@
 """A/B of the two lora_xwt kernels (csrc/kernels/lora.hip) at the Llama-3.1-70B
 LoRA shapes (T = 4096 tokens, pad 64): the register-fragment kernel
-(MXLLM_LORA_XWT=reg) vs the LDS-DMA-staged one (default), interleaved rounds in
-ONE process; prints the median us/call and the streamed operand's bandwidth."""
+(MXLLM_LORA_XWT=reg) vs the LDS-DMA-staged one (default), the latter also with its
+split reduction merged in-launch (MXLLM_LORA_FUSED_RED=1, "lds_f"), interleaved rounds
+in ONE process; prints the median us/call and the streamed operand's bandwidth."""
 import json
 import os
 import statistics
@@ -27,12 +28,17 @@ def timeit(fn, iters=20):
     return 1e3 * a.elapsed_time(b) / iters
 
 
+def setv(v):
+    os.environ["MXLLM_LORA_XWT"] = "reg" if v == "reg" else "lds"
+    os.environ["MXLLM_LORA_FUSED_RED"] = "1" if v == "lds_f" else "0"
+
+
 def main():
     from mxllm.ops import _ext
 
     nat = _ext.native()
     res = []
-    tot = {"reg": 0.0, "lds": 0.0}
+    tot = {"reg": 0.0, "lds": 0.0, "lds_f": 0.0}
     for name, (K, N) in PROJ.items():
         wbuf = torch.randn(N + P, K + P, device="cuda", dtype=torch.bfloat16) * 0.02
         xa = torch.randn(T, K + P, device="cuda", dtype=torch.bfloat16)
@@ -43,21 +49,22 @@ def main():
         for cname, (fn, nbytes) in calls.items():
             # numerics: both kernels vs fp32
             outs = {}
-            for v in ("reg", "lds"):
-                os.environ["MXLLM_LORA_XWT"] = v
+            for v in ("reg", "lds", "lds_f"):
+                setv(v)
                 fn()
                 torch.cuda.synchronize()
                 outs[v] = (xa[:, K:] if cname == "fwd" else dya[:, N:]).float().clone()
             diff = (outs["reg"] - outs["lds"]).abs().max().item()
-            t = {"reg": [], "lds": []}
+            same = bool(torch.equal(outs["lds"], outs["lds_f"]))
+            t = {"reg": [], "lds": [], "lds_f": []}
             for _ in range(7):
-                for v in ("reg", "lds"):
-                    os.environ["MXLLM_LORA_XWT"] = v
+                for v in ("reg", "lds", "lds_f"):
+                    setv(v)
                     t[v].append(timeit(fn))
             med = {v: statistics.median(x) for v, x in t.items()}
             for v in med:
                 tot[v] += med[v]
-            row = {"proj": name, "call": cname, "MB": round(nbytes / 1e6, 1), "max_abs_diff": diff}
+            row = {"proj": name, "call": cname, "MB": round(nbytes / 1e6, 1), "max_abs_diff": diff, "fused_red_bitwise": same}
             for v in med:
                 row[f"{v}_us"] = round(med[v], 1)
                 row[f"{v}_TBps"] = round(nbytes / med[v] / 1e6, 2)
@@ -65,6 +72,7 @@ def main():
             res.append(row)
         del wbuf, xa, dya, bt
     os.environ.pop("MXLLM_LORA_XWT", None)
+    os.environ.pop("MXLLM_LORA_FUSED_RED", None)
     print(json.dumps({"layer_us": {k: round(v, 1) for k, v in tot.items()},
                       "step_ms_80_layers": {k: round(v * 80 / 1e3, 2) for k, v in tot.items()}}), flush=True)
 

@@ -496,12 +496,23 @@ at::Tensor rope_append(const at::Tensor& qkv, const at::Tensor& cos, const at::T
 
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                        const at::Tensor& lens, const c10::optional<at::Tensor>& slots, int64_t max_len, double scale,
-                       int64_t len_off, const c10::optional<at::Tensor>& block_table) {
+                       int64_t len_off, const c10::optional<at::Tensor>& block_table,
+                       const c10::optional<at::Tensor>& counters) {
   check_bf16(q, "q");
   MX_CHECK(lens.scalar_type() == at::kInt, "lens int32");
   const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
   const int64_t Hkv = k_cache.size(1), max_seq = k_cache.size(2);
   DevGuard g(q.device());
+  // counters: int32 [>= B * Hkv], zero, owned by the caller (a decode engine): the split
+  // partials are merged in-launch by the last workgroup of each (seq, kv-head), which
+  // resets its counter -> no combine launch (head_dim 128)
+  unsigned int* cnt = nullptr;
+  if (counters.has_value() && D == 128) {
+    MX_CHECK(counters->scalar_type() == at::kInt && counters->is_contiguous() && counters->numel() >= B * Hkv &&
+                 counters->device() == q.device(),
+             "decode_attn: counters must be a contiguous int32 tensor of >= B * Hkv zeros on q's device");
+    cnt = reinterpret_cast<unsigned int*>(counters->data_ptr<int32_t>());
+  }
   const KvPages pg = kv_pages(block_table, k_cache);
   const int64_t cap = pg.bt ? (int64_t)pg.maxb * max_seq : max_seq;  // positions a sequence can hold
   const int64_t nsplit = std::max<int64_t>(1, (std::min(max_len, cap) + 255) / 256);
@@ -512,7 +523,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   if (slots.has_value()) sl = slots->data_ptr<int32_t>();
   MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), (int)len_off, sl, ml.data_ptr<float>(),
                        po.data_ptr<float>(), bfm(out), (int)B, (int)Hq, (int)Hkv, (int)D, (int)max_seq, (int)nsplit,
-                       (float)scale, pg.bt, pg.maxb, cur_stream()));
+                       (float)scale, pg.bt, pg.maxb, cnt, cur_stream()));
   return out;
 }
 
@@ -538,7 +549,7 @@ std::tuple<at::Tensor, at::Tensor> decode_attn_partials(const at::Tensor& q, con
   if (slots.has_value()) sl = slots->data_ptr<int32_t>();
   MX_OK(mx_decode_attn(bf(q), bf(k_cache), bf(v_cache), lens.data_ptr<int32_t>(), (int)len_off, sl, ml.data_ptr<float>(),
                        po.data_ptr<float>(), nullptr, (int)B, (int)Hq, (int)Hkv, (int)D, (int)max_seq, (int)nsplit,
-                       (float)scale, pg.bt, pg.maxb, cur_stream()));
+                       (float)scale, pg.bt, pg.maxb, nullptr, cur_stream()));
   return {ml, po};
 }
 
@@ -856,7 +867,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
   m.def("rope_append(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor? slots, Tensor(a!) k_cache, Tensor(b!) v_cache, int Hq, int Hkv, int D, Tensor? block_table=None) -> Tensor");
-  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0, Tensor? block_table=None) -> Tensor");
+  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0, Tensor? block_table=None, Tensor? counters=None) -> Tensor");
   m.def("decode_attn_partials(Tensor q, Tensor k_cache, Tensor v_cache, Tensor lens, Tensor? slots, int max_len, float scale, int len_off=0, Tensor? block_table=None) -> (Tensor, Tensor)");
   m.def("skinny_merge_linear(Tensor ml, Tensor po, Tensor w) -> Tensor");
   m.def("sample(Tensor logits, float temperature, int seed, int step) -> Tensor");

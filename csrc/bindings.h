@@ -61,7 +61,8 @@ int mx_rope_append(const uint16_t* qkv, const float* cosb, const float* sinb, co
                    const int32_t* bt, int maxb, hipStream_t stream);
 int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens, int len_off,
                    const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B, int Hq, int Hkv, int D,
-                   int max_seq, int nsplit, float scale, const int32_t* bt, int maxb, hipStream_t stream);
+                   int max_seq, int nsplit, float scale, const int32_t* bt, int maxb, unsigned int* cnt,
+                   hipStream_t stream);
 int64_t mx_sample_ws_floats(int B);
 int mx_sample(const void* logits, int is_bf16, int64_t* out, int B, int V, float temperature, uint32_t seed,
               uint32_t step, float* ws, hipStream_t stream);

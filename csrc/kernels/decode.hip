@@ -221,35 +221,32 @@ __device__ __forceinline__ u16x4 tr_read16(const char* p) {
 // 16-B chunk swizzle of a 256-B row (conflict-free row and transposed reads)
 __device__ __forceinline__ int dswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-__global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t* __restrict__ q,
-                                                                  const uint16_t* __restrict__ kc,
-                                                                  const uint16_t* __restrict__ vc,
-                                                                  const int32_t* __restrict__ lens, int len_off,
-                                                                  const int32_t* __restrict__ slots,
-                                                                  float* __restrict__ part_ml,
-                                                                  float* __restrict__ part_o, int Hq, int Hkv,
-                                                                  int max_seq, int nsplit, float sl,
-                                                                  const int32_t* __restrict__ bt, int maxb) {
-  constexpr int D = 128, ROWB = 256, WKEYS = 64, WTILE = WKEYS * ROWB;  // 16 KiB per wave
-  __shared__ __attribute__((aligned(16))) char smem[4 * WTILE];
-  __shared__ float mls[4][2][16];
-  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
-  const int rep = Hq / Hkv;
-  const int len = lens[b] + len_off;
-  const int slot = slots ? slots[b] : b;
-  const int k_lo = split * kSplit;
-  const int k_hi = min(len, k_lo + kSplit);
+// stores / loads of the split partials that another workgroup of the SAME launch merges:
+// write-through (sc1, relaxed agent-scope atomic store), so no release fence (an L2
+// write-back per workgroup) is needed, and loads that bypass this CU's L1 (guide
+// §6 Guideline 16, the sc1 hand-off form)
+template <bool SC1>
+__device__ __forceinline__ void st_part(float* p, float v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+__device__ __forceinline__ float ld_part(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one split of decode_attn_mfma_kernel: (m, l, o) partial of 256 keys for every
+// q-head of the GQA group (see the kernel's header comment)
+template <bool SC1>
+__device__ __forceinline__ void decode_split_body(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                                                  const uint16_t* __restrict__ vc, float* __restrict__ part_o,
+                                                  float* __restrict__ pml, char* smem, float (*mls)[2][16], int b,
+                                                  int hk, int rep, int Hq, int split, int nsplit, int k_lo, int k_hi,
+                                                  int slot, int max_seq, float sl, const int32_t* __restrict__ bt,
+                                                  int maxb, int Hkv) {
+  constexpr int D = 128, ROWB = 256, WKEYS = 64, WTILE = WKEYS * ROWB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, g = lane >> 4;
-  float* pml = part_ml + (((int64_t)b * Hq + hk * rep) * nsplit + split) * 2;
-  if (k_lo >= k_hi) {  // empty split (workgroup-uniform): neutral partial
-    if (tid < rep) {
-      pml[(int64_t)tid * nsplit * 2] = -INFINITY;
-      pml[(int64_t)tid * nsplit * 2 + 1] = 0.f;
-    }
-    return;
-  }
   const int64_t kvb = (kv_row(bt, maxb, max_seq, slot, Hkv, hk, k_lo) - k_lo) * D;  // one block per split
   const uint16_t* kbase = kc + kvb;
   const uint16_t* vbase = vc + kvb;
@@ -362,10 +359,80 @@ __global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t
       L += f * mls[ww][1][h];
       acc += f * reinterpret_cast<const float*>(smem + ww * WTILE)[d * 16 + h];
     }
-    part_o[(((int64_t)b * Hq + hk * rep + h) * nsplit + split) * D + d] = acc;
+    st_part<SC1>(&part_o[(((int64_t)b * Hq + hk * rep + h) * nsplit + split) * D + d], acc);
     if (d == 0) {
-      pml[(int64_t)h * nsplit * 2] = M;
-      pml[(int64_t)h * nsplit * 2 + 1] = L;
+      st_part<SC1>(&pml[(int64_t)h * nsplit * 2], M);
+      st_part<SC1>(&pml[(int64_t)h * nsplit * 2 + 1], L);
+    }
+  }
+}
+
+template <bool FUSED>
+__global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t* __restrict__ q,
+                                                                  const uint16_t* __restrict__ kc,
+                                                                  const uint16_t* __restrict__ vc,
+                                                                  const int32_t* __restrict__ lens, int len_off,
+                                                                  const int32_t* __restrict__ slots,
+                                                                  float* __restrict__ part_ml,
+                                                                  float* __restrict__ part_o, int Hq, int Hkv,
+                                                                  int max_seq, int nsplit, float sl,
+                                                                  const int32_t* __restrict__ bt, int maxb,
+                                                                  uint16_t* __restrict__ out,
+                                                                  unsigned int* __restrict__ cnt) {
+  constexpr int D = 128, WTILE = 64 * 256;  // 16 KiB per wave
+  __shared__ __attribute__((aligned(16))) char smem[4 * WTILE];
+  __shared__ float mls[4][2][16];
+  __shared__ int s_last;
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int rep = Hq / Hkv;
+  const int len = lens[b] + len_off;
+  const int slot = slots ? slots[b] : b;
+  const int k_lo = split * kSplit;
+  const int k_hi = min(len, k_lo + kSplit);
+  const int tid = threadIdx.x;
+  float* pml = part_ml + (((int64_t)b * Hq + hk * rep) * nsplit + split) * 2;
+  if (k_lo >= k_hi) {  // empty split (workgroup-uniform): neutral partial
+    if (tid < rep) {
+      st_part<FUSED>(&pml[(int64_t)tid * nsplit * 2], -INFINITY);
+      st_part<FUSED>(&pml[(int64_t)tid * nsplit * 2 + 1], 0.f);
+    }
+  } else {
+    decode_split_body<FUSED>(q, kc, vc, part_o, pml, smem, mls, b, hk, rep, Hq, split, nsplit, k_lo, k_hi, slot,
+                             max_seq, sl, bt, maxb, Hkv);
+  }
+  if constexpr (FUSED) {
+    // In-launch combine: the last of the nsplit workgroups of this (seq, kv-head) to
+    // arrive merges the partials.  Partials were stored write-through (sc1) and every
+    // storing wave drains them before the barrier -> the relaxed agent-scope ticket
+    // publishes them; the merger reads them with sc1 loads (no L1 copy) and resets
+    // the counter, so it is zero again for the next call.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned int* c = cnt + (int64_t)b * Hkv + hk;
+      const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == (unsigned)(nsplit - 1);
+      if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the same arithmetic, in the same order, as decode_combine_kernel
+    for (int idx = tid; idx < rep * D; idx += 256) {
+      const int h = idx / D, d = idx % D;
+      const int64_t bh = (int64_t)b * Hq + hk * rep + h;
+      const float* ml = part_ml + bh * nsplit * 2;
+      float M = -INFINITY;
+      for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, ld_part(ml + 2 * sp));
+      float L = 0.f, acc = 0.f;
+      for (int sp = 0; sp < nsplit; ++sp) {
+        const float m = ld_part(ml + 2 * sp);
+        if (m == -INFINITY) continue;
+        const float wgt = __builtin_amdgcn_exp2f(m - M);
+        L += wgt * ld_part(ml + 2 * sp + 1);
+        acc += wgt * ld_part(part_o + (bh * nsplit + sp) * D + d);
+      }
+      out[bh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
     }
   }
 }
@@ -532,16 +599,22 @@ extern "C" int mx_rope_append(const uint16_t* qkv, const float* cosb, const floa
 extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* lens,
                               int len_off, const int32_t* slots, float* part_ml, float* part_o, uint16_t* out, int B,
                               int Hq, int Hkv, int D, int max_seq, int nsplit, float scale, const int32_t* bt,
-                              int maxb, hipStream_t stream) {
+                              int maxb, unsigned int* cnt, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > kMaxRep) return -1;
   if (bt && max_seq % kSplit) return -1;  // a split must lie inside one block
   dim3 grid(nsplit, Hkv, B);
   const float sl = scale * 1.4426950408889634f;
   if (D == 128) {  // out == nullptr: partials only (the o-projection merges them: skinny_gemm.hip MERGE)
-    decode_attn_mfma_kernel<<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv,
-                                                      max_seq, nsplit, sl, bt, maxb);
-    if (out) decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
+    // cnt (zeroed [B * Hkv] counters, owned by the caller): the splits merge in-launch
+    if (out && cnt) {
+      decode_attn_mfma_kernel<true><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq,
+                                                              Hkv, max_seq, nsplit, sl, bt, maxb, out, cnt);
+    } else {
+      decode_attn_mfma_kernel<false><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq,
+                                                               Hkv, max_seq, nsplit, sl, bt, maxb, out, nullptr);
+      if (out) decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
+    }
     return (int)hipGetLastError();
   }
   if (!out) return -1;

@@ -71,6 +71,36 @@ __device__ __forceinline__ bool arrive_last(unsigned int* cnt, int S, int* s_fla
   return last;
 }
 
+// The same hand-off without fences (guide §6 Guideline 16, sc1 form): partials are
+// stored write-through (relaxed agent-scope atomic stores = sc1), every storing wave
+// drains them before the barrier, one relaxed agent-scope ticket publishes them, and the
+// last arriver reads them with sc1 loads (no stale L1 copy, no acquire needed).
+__device__ __forceinline__ void st4_sc1(float* p, const float4& v) {
+  __hip_atomic_store(p + 0, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 ld4_sc1(const float* p) {
+  float* q = const_cast<float*>(p);
+  return float4{__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+}
+__device__ __forceinline__ bool arrive_last_sc1(unsigned int* cnt, int S, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(S - 1);
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ lora_xwt
@@ -288,15 +318,19 @@ __global__ void __launch_bounds__(256, 1) lora_xwt_lds_kernel(const uint16_t* __
   }
   if (S > 1) {
     float* wp = ws + ((int64_t)split * mtiles + mt) * 4096;
+    if (!fused_red) {  // lora_xwt_reduce_kernel finishes
 #pragma unroll
-    for (int q = 0; q < 4; ++q) reinterpret_cast<float4*>(wp)[tid + 256 * q] = v[q];
-    if (!fused_red) return;  // lora_xwt_reduce_kernel finishes
-    if (!arrive_last(&g_xwt_cnt[mt], S, s_last)) return;
+      for (int q = 0; q < 4; ++q) reinterpret_cast<float4*>(wp)[tid + 256 * q] = v[q];
+      return;
+    }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[tid + 256 * q];
+    for (int q = 0; q < 4; ++q) st4_sc1(wp + 4 * (tid + 256 * q), v[q]);
+    if (!arrive_last_sc1(&g_xwt_cnt[mt], S, s_last)) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // fixed split order (bit-reproducible, = the reduce kernel)
+      float4 s = ld4_sc1(ws + (int64_t)mt * 4096 + 4 * (tid + 256 * q));
       for (int sp = 1; sp < S; ++sp) {
-        const float4 t = reinterpret_cast<const float4*>(ws + ((int64_t)sp * mtiles + mt) * 4096)[tid + 256 * q];
+        const float4 t = ld4_sc1(ws + ((int64_t)sp * mtiles + mt) * 4096 + 4 * (tid + 256 * q));
         s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
       }
       v[q] = s;
@@ -497,17 +531,25 @@ __global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float
   }
   if (a.S > 1) {
     float* wp = ws + ((int64_t)split * a.ntiles + tile) * 4096;
+    if (!a.fused_red) {  // lora_xtg_reduce_kernel finishes
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (tid + 256 * q < nel) wp[tid + 256 * q] = v[q];
+      return;
+    }
+    // in-launch merge, sc1 hand-off (see arrive_last_sc1)
 #pragma unroll
     for (int q = 0; q < 16; ++q)
-      if (tid + 256 * q < nel) wp[tid + 256 * q] = v[q];
-    if (!a.fused_red) return;
-    if (!arrive_last(&g_xtg_cnt[tile], a.S, &s_last)) return;
+      if (tid + 256 * q < nel) __hip_atomic_store(wp + tid + 256 * q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!arrive_last_sc1(&g_xtg_cnt[tile], a.S, &s_last)) return;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = tid + 256 * q;
       if (e < nel) {
-        float s = ws[(int64_t)tile * 4096 + e];
-        for (int sp = 1; sp < a.S; ++sp) s += ws[((int64_t)sp * a.ntiles + tile) * 4096 + e];
+        float s = __hip_atomic_load(ws + (int64_t)tile * 4096 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int sp = 1; sp < a.S; ++sp)
+          s += __hip_atomic_load(ws + ((int64_t)sp * a.ntiles + tile) * 4096 + e, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
         v[q] = s;
       }
     }

@@ -50,14 +50,18 @@ def _kv_at(cache: torch.Tensor, bt, slot: int, p0: int, p1: int) -> torch.Tensor
 
 
 def decode_attention(qkv: torch.Tensor, cos, sin, k_cache, v_cache, pos: torch.Tensor, slots: torch.Tensor,
-                     Hq: int, Hkv: int, D: int, max_len: int, block_table: torch.Tensor | None = None) -> torch.Tensor:
+                     Hq: int, Hkv: int, D: int, max_len: int, block_table: torch.Tensor | None = None,
+                     counters: torch.Tensor | None = None) -> torch.Tensor:
     """Batched single-token step.  qkv [B, NH*D], pos/slots int32 [B] (pos = index
     of the new token).  Appends K/V at ``pos`` and attends over ``pos + 1`` keys.
-    ``block_table`` [slots, max_blocks] int32: paged caches [blocks, Hkv, block, D]."""
+    ``block_table`` [slots, max_blocks] int32: paged caches [blocks, Hkv, block, D].
+    ``counters``: zeroed int32 [>= B * Hkv] owned by the caller — the split-K
+    partials then merge inside the attention launch (no combine kernel)."""
     if use_native(qkv):
         ops = native()
         q = ops.rope_append(qkv.contiguous(), cos, sin, pos, slots, k_cache, v_cache, Hq, Hkv, D, block_table)
-        return ops.decode_attn(q, k_cache, v_cache, pos, slots, max_len, 1.0 / math.sqrt(D), 1, block_table)
+        return ops.decode_attn(q, k_cache, v_cache, pos, slots, max_len, 1.0 / math.sqrt(D), 1, block_table,
+                               counters)
     bt = block_table.cpu() if block_table is not None else None
     B = qkv.shape[0]
     x = qkv.view(B, Hq + 2 * Hkv, D).float()

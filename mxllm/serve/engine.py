@@ -137,6 +137,13 @@ class Engine:
         self.kv = KVCache(c.n_layers, c.n_kv_heads, c.head_dim, dt, self.device, n_slots, self.max_seq,
                           pool_tokens=kv_pool_tokens, block=kv_block,
                           scratch_slot=self.scratch_slot if self.use_graphs else None)
+        # decode attention: the split-K partials merge inside the attention launch (the last
+        # workgroup of each (seq, kv-head) combines; these counters stay zero between calls),
+        # no separate combine kernel; MXLLM_DECODE_COMBINE=kernel keeps the two-launch form
+        self._attn_cnt = None
+        if self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_COMBINE", "kernel") == "fused":
+            self._attn_cnt = torch.zeros((n_slots + 64) * self.kv.k[0].shape[1], dtype=torch.int32,
+                                         device=self.device)
         self.eos_ids = tuple(eos_ids) if eos_ids else (c.eos_id,)
         self.free_slots = list(range(max_batch))
         self.active: dict[int, Request] = {}
@@ -322,6 +329,9 @@ class Engine:
         B = inp.shape[1]
         nsplit = (min(max_len, self.kv.maxb * self.kv.block) + 255) // 256
         merge = _MERGE_FUSED and c.head_dim == 128 and B <= 4 and nsplit <= 16
+        cnt = self._attn_cnt
+        if cnt is not None and B * self.kv.k[0].shape[1] > cnt.numel():
+            cnt = None
 
         def attn(i, qkv, q=None):
             if q is not None:  # RoPE and the cache append already done by the QKV GEMM
@@ -333,9 +343,9 @@ class Engine:
                     return ops.native().decode_attn_partials(q, self.kv.k[i], self.kv.v[i], pos, sl, max_len,
                                                              1.0 / math.sqrt(c.head_dim), 1, bt)
                 return ops.native().decode_attn(q, self.kv.k[i], self.kv.v[i], pos, sl, max_len,
-                                                1.0 / math.sqrt(c.head_dim), 1, bt)
+                                                1.0 / math.sqrt(c.head_dim), 1, bt, cnt)
             return dops.decode_attention(qkv, m.rope_cos, m.rope_sin, self.kv.k[i], self.kv.v[i], pos, sl,
-                                         c.n_heads, c.n_kv_heads, c.head_dim, max_len, bt)
+                                         c.n_heads, c.n_kv_heads, c.head_dim, max_len, bt, cnt)
 
         def qkv_fn(i, delta, h, gamma, layer):
             # QKV GEMM with the RoPE/cache-append epilogue; 1-2 rows also with the RMSNorm prologue

@@ -423,6 +423,12 @@ def test_lora_xwt(gpu, T, K, vrows, kern, monkeypatch):
     first = buf[:, K:K + vrows].clone()
     _ops().lora_xwt(x, v, buf[:, K:K + vrows], 2.0)
     assert torch.equal(buf[:, K:K + vrows], first)  # bit-reproducible
+    if kern == "lds":  # split partials merged in-launch (sc1 hand-off): same bits, counters reset
+        monkeypatch.setenv("MXLLM_LORA_FUSED_RED", "1")
+        for _ in range(2):
+            buf[:, K:K + vrows] = 0
+            _ops().lora_xwt(x, v, buf[:, K:K + vrows], 2.0)
+            assert torch.equal(buf[:, K:K + vrows], first)
 
 
 @pytest.mark.parametrize("T,K,splits,r,acc", [(256, 512, [512, 128, 128], 16, False),
@@ -430,9 +436,10 @@ def test_lora_xwt(gpu, T, K, vrows, kern, monkeypatch):
                                               (512, 256, [1024, 1024], 16, True),
                                               (256, 320, [192], 16, False),
                                               (256, 512, [512, 256, 256], 32, True)])
-def test_lora_grads(gpu, T, K, splits, r, acc):
+def test_lora_grads(gpu, T, K, splits, r, acc, monkeypatch):
     """dA = g^T x and the diagonal blocks dB_i = dy_i^T st_i in one launch,
-    accumulated into bf16 grads or written fresh; off-diagonal blocks untouched."""
+    accumulated into bf16 grads or written fresh; off-diagonal blocks untouched;
+    the in-launch split merge (MXLLM_LORA_FUSED_RED=1) gives the same bits."""
     torch.manual_seed(4)
     n, N = len(splits), sum(splits)
     R = n * r
@@ -464,6 +471,11 @@ def test_lora_grads(gpu, T, K, splits, r, acc):
     ga1, gb1 = ga0.clone(), gb0.clone()
     _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
     assert torch.equal(ga1, ga) and torch.equal(gb1, gb)  # bit-reproducible
+    monkeypatch.setenv("MXLLM_LORA_FUSED_RED", "1")
+    for _ in range(2):
+        ga1, gb1 = ga0.clone(), gb0.clone()
+        _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
+        assert torch.equal(ga1, ga) and torch.equal(gb1, gb)
 
 
 @pytest.mark.parametrize("R,C,ld", [(4096, 8192, None), (64, 64, None), (37, 130, None), (130, 4096, 4160),

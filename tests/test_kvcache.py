@@ -143,3 +143,23 @@ def test_merged_o_projection_matches_combine_then_gemm(gpu, B, ctx, Hq):
     ml, po = native().decode_attn_partials(q, kc, vc, lens, slots, ctx + 1, D ** -0.5, 1)
     y = native().skinny_merge_linear(ml, po, w)
     assert torch.equal(y, ref)
+
+
+@pytest.mark.gpu
+def test_engine_in_launch_decode_merge_matches_combine_kernel(gpu, monkeypatch):
+    """MXLLM_DECODE_COMBINE=fused (split-K merge by the last-arriving attention workgroup,
+    sc1 hand-off) generates exactly what the two-launch form generates, graphed, static
+    and paged KV, over contexts that span several 256-key splits."""
+    m = Llama(get_config("tiny-d128"), device=gpu, seed=3).eval()
+    prompts = [list(range(1 + i, 300 + 97 * i)) for i in range(5)]
+    outs = {}
+    for mode in ("kernel", "fused"):
+        monkeypatch.setenv("MXLLM_DECODE_COMBINE", mode)
+        for pool in (None, 4096):
+            eng = Engine(m, max_batch=4, max_seq=1024, kv_pool_tokens=pool)
+            assert (eng._attn_cnt is not None) == (mode == "fused")
+            outs[(mode, pool)] = eng.generate(prompts, max_new_tokens=24)
+            if eng._attn_cnt is not None:
+                assert int(eng._attn_cnt.abs().sum()) == 0  # every counter back at zero
+    assert outs[("fused", None)] == outs[("kernel", None)]
+    assert outs[("fused", 4096)] == outs[("kernel", 4096)]

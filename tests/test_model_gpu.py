@@ -66,9 +66,15 @@ def test_decode_kernels(gpu, D, Hq, Hkv):
     kc_ref, vc_ref = kc.clone(), vc.clone()
     q = native().rope_append(qkv, cos, sin, pos, slots, kc, vc, Hq, Hkv, D)
     out = native().decode_attn(q, kc, vc, pos, slots, max(lens) + 1, 1.0 / math.sqrt(D), 1)
-    # the split merge runs in the attention kernel (last-arriving split): its arrival counters
-    # must be back at zero for the next call -> identical output
     assert torch.equal(native().decode_attn(q, kc, vc, pos, slots, max(lens) + 1, 1.0 / math.sqrt(D), 1), out)
+    # with arrival counters the split merge runs inside the attention launch (last-arriving
+    # workgroup, sc1 hand-off): bit-identical to the combine kernel, and the counters are
+    # back at zero after every call
+    cnt = torch.zeros(B * Hkv + 5, dtype=torch.int32, device=gpu)
+    for _ in range(3):
+        o2 = native().decode_attn(q, kc, vc, pos, slots, max(lens) + 1, 1.0 / math.sqrt(D), 1, None, cnt)
+        assert torch.equal(o2, out)
+        assert int(cnt.abs().sum()) == 0
     x = qkv.float().view(B, Hq + 2 * Hkv, D)
     for i in range(B):
         p, s = lens[i], int(slots[i])
