@@ -158,6 +158,13 @@ at::Tensor transpose2d(const at::Tensor& in) {
   return out;
 }
 
+// read `t` once on the current stream (cache warm-up of a weight ahead of its consumer; misc.hip)
+void prefetch(const at::Tensor& t, int64_t wgs) {
+  MX_CHECK(t.is_cuda() && t.is_contiguous(), "prefetch: contiguous GPU tensor");
+  DevGuard g(t.device());
+  MX_OK(mx_prefetch(t.data_ptr(), t.numel() * t.element_size(), (int)wgs, cur_stream()));
+}
+
 at::Tensor segmented_mean(const at::Tensor& codes, const at::Tensor& offsets) {
   MX_CHECK(codes.is_cuda() && codes.scalar_type() == at::kInt, "codes must be int32 GPU");
   MX_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kLong, "offsets must be int64 GPU");
@@ -854,6 +861,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
@@ -892,6 +900,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("segmented_mean", &segmented_mean);
   m.impl("copy2d_batched", &copy2d_batched);
   m.impl("transpose2d", &transpose2d);
+  m.impl("prefetch", &prefetch);
   m.impl("sqnorm", &sqnorm);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);

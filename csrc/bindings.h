@@ -18,6 +18,7 @@ int mx_segmented_mean_i32(const int32_t* codes, const int64_t* offs, float* out,
                           hipStream_t stream);
 int mx_sqnorm(const void* x, int bf16, int64_t n, float* out, float* work, hipStream_t stream);
 int mx_copy2d_batched(const int64_t* desc, int n, int64_t total_blocks, hipStream_t stream);
+int mx_prefetch(const void* p, int64_t bytes, int wgs, hipStream_t stream);
 int mx_transpose16(const void* in, void* out, int64_t R, int64_t C, int64_t ld_in, int64_t ld_out,
                    hipStream_t stream);
 }

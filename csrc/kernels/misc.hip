@@ -191,3 +191,31 @@ extern "C" int mx_transpose16(const void* in, void* out, int64_t R, int64_t C, i
       reinterpret_cast<const uint16_t*>(in), reinterpret_cast<uint16_t*>(out), R, C, ld_in, ld_out);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------ cache prefetch
+// Read a weight tensor once so its lines sit in the memory-side Infinity Cache (and the
+// readers' L2s) when the consumer kernel streams it: issued on a side stream beside a
+// latency-bound kernel that leaves HBM idle (batch-1 decode attention), so the next
+// weight-streaming GEMM reads from the cache instead of HBM.  The loaded values feed an
+// XOR that is stored only when `never` (a runtime 0) is set, which keeps every load.
+namespace mx {
+__global__ void __launch_bounds__(256) prefetch_kernel(const uint4* __restrict__ p, int64_t n16, int never,
+                                                       uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {  // four 16-B loads in flight per lane
+    const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+    acc ^= a.x ^ b.y ^ c.z ^ d.w;
+  }
+  for (; i < n16; i += stride) acc ^= p[i].x;
+  if (never) sink[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+}  // namespace mx
+
+extern "C" int mx_prefetch(const void* p, int64_t bytes, int wgs, hipStream_t stream) {
+  if (bytes < 16 || wgs <= 0) return 0;
+  if ((uintptr_t)p % 16) return -1;
+  prefetch_kernel<<<wgs, 256, 0, stream>>>(reinterpret_cast<const uint4*>(p), bytes / 16, 0, nullptr);
+  return (int)hipGetLastError();
+}

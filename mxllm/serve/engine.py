@@ -51,6 +51,11 @@ _ROPE_FUSED = os.environ.get("MXLLM_ROPE_FUSED", "1") != "0"  # A/B switch: RoPE
 # 3.841 ms (the prologue slows the weight stream more than the combine launch costs;
 # profiles/r3d_decode_merge_ab.md).  MXLLM_MERGE_FUSED=1 turns it on.
 _MERGE_FUSED = os.environ.get("MXLLM_MERGE_FUSED", "0") == "1"
+# Small-batch decode: while the (latency-bound) attention runs, a side-stream kernel reads
+# the layer's o-projection weight so the o-projection GEMM streams it from the Infinity
+# Cache instead of HBM (MXLLM_DECODE_PREFETCH=1; up to PREFETCH_MAX_B rows)
+_PREFETCH = os.environ.get("MXLLM_DECODE_PREFETCH", "0") == "1"
+PREFETCH_MAX_B = 8
 log = logging.getLogger("mxllm.engine")
 
 
@@ -144,6 +149,7 @@ class Engine:
         if self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_COMBINE", "kernel") == "fused":
             self._attn_cnt = torch.zeros((n_slots + 64) * self.kv.k[0].shape[1], dtype=torch.int32,
                                          device=self.device)
+        self._pf_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" and _PREFETCH else None
         self.eos_ids = tuple(eos_ids) if eos_ids else (c.eos_id,)
         self.free_slots = list(range(max_batch))
         self.active: dict[int, Request] = {}
@@ -333,7 +339,23 @@ class Engine:
         if cnt is not None and B * self.kv.k[0].shape[1] > cnt.numel():
             cnt = None
 
+        pf = self._pf_stream if B <= PREFETCH_MAX_B else None
+
         def attn(i, qkv, q=None):
+            if pf is None:
+                return attn_(i, qkv, q)
+            wo = getattr(m.layers[i].wo, "weight", None)
+            if wo is None or not wo.is_contiguous():
+                return attn_(i, qkv, q)
+            cur = torch.cuda.current_stream(self.device)
+            pf.wait_stream(cur)
+            with torch.cuda.stream(pf):
+                ops.native().prefetch(wo, 128)
+            out = attn_(i, qkv, q)
+            cur.wait_stream(pf)  # joins the side branch before the o-projection
+            return out
+
+        def attn_(i, qkv, q=None):
             if q is not None:  # RoPE and the cache append already done by the QKV GEMM
                 wo = m.layers[i].wo
                 K = q.shape[1] * 128  # this rank's heads (tensor parallel: a shard)

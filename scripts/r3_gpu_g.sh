@@ -16,6 +16,11 @@ for r in 1 2; do
   done
 done
 for r in 1 2; do
+  for v in 1 0; do
+    MXLLM_DECODE_PREFETCH=$v timeout -k 10 300 python bench/serve_bench.py --model llama3.1-8b --batches 1,4 --requests 0 --json-out $O/serve8b_pf${v}_$r.json > $O/serve8b_pf${v}_$r.log 2>&1
+  done
+done
+for r in 1 2; do
   for v in lds reg; do
     MXLLM_LORA_XWT=$v timeout -k 10 300 python bench.py --steps 12 --warmup 4 --config2 off --config3 off --config4 off --json-out $O/70b_xwt_${v}_$r.json > $O/70b_xwt_${v}_$r.log 2>&1
   done

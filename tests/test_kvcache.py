@@ -163,3 +163,19 @@ def test_engine_in_launch_decode_merge_matches_combine_kernel(gpu, monkeypatch):
                 assert int(eng._attn_cnt.abs().sum()) == 0  # every counter back at zero
     assert outs[("fused", None)] == outs[("kernel", None)]
     assert outs[("fused", 4096)] == outs[("kernel", 4096)]
+
+
+@pytest.mark.gpu
+def test_engine_decode_prefetch_is_transparent(gpu, monkeypatch):
+    """MXLLM_DECODE_PREFETCH=1 (a side-stream read of each o-projection weight during the
+    decode attention, joined before the GEMM, captured into the decode graph) changes no token."""
+    import mxllm.serve.engine as E
+
+    m = Llama(get_config("tiny-d128"), device=gpu, seed=5).eval()
+    prompts = [list(range(1 + i, 60 + 31 * i)) for i in range(3)]
+    base = Engine(m, max_batch=4, max_seq=1024).generate(prompts, max_new_tokens=16)
+    monkeypatch.setattr(E, "_PREFETCH", True)
+    eng = Engine(m, max_batch=4, max_seq=1024)
+    assert eng._pf_stream is not None and eng.use_graphs
+    assert eng.generate(prompts, max_new_tokens=16) == base
+
