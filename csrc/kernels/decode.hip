@@ -225,24 +225,28 @@ __device__ __forceinline__ int dswz(int row) { return ((row & 3) << 2) | ((row >
 // write-through (sc1, relaxed agent-scope atomic store), so no release fence (an L2
 // write-back per workgroup) is needed, and loads that bypass this CU's L1 (guide
 // §6 Guideline 16, the sc1 hand-off form)
-template <bool SC1>
-__device__ __forceinline__ void st_part(float* p, float v) {
-  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// st: 0 = plain store, 1 = agent-scope relaxed atomic store (sc1 write-through),
+// 2 = system-scope relaxed atomic store; ld: 0 = plain load, 1 = agent, 2 = system
+__device__ __forceinline__ void st_part(float* p, float v, int st) {
+  if (st == 1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if (st == 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   else *p = v;
 }
-__device__ __forceinline__ float ld_part(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ float ld_part(const float* p, int ld) {
+  float* q = const_cast<float*>(p);
+  if (ld == 1) return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ld == 2) return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return *p;
 }
 
 // one split of decode_attn_mfma_kernel: (m, l, o) partial of 256 keys for every
 // q-head of the GQA group (see the kernel's header comment)
-template <bool SC1>
 __device__ __forceinline__ void decode_split_body(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                   const uint16_t* __restrict__ vc, float* __restrict__ part_o,
                                                   float* __restrict__ pml, char* smem, float (*mls)[2][16], int b,
                                                   int hk, int rep, int Hq, int split, int nsplit, int k_lo, int k_hi,
                                                   int slot, int max_seq, float sl, const int32_t* __restrict__ bt,
-                                                  int maxb, int Hkv) {
+                                                  int maxb, int Hkv, int st) {
   constexpr int D = 128, ROWB = 256, WKEYS = 64, WTILE = WKEYS * ROWB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -359,15 +363,21 @@ __device__ __forceinline__ void decode_split_body(const uint16_t* __restrict__ q
       L += f * mls[ww][1][h];
       acc += f * reinterpret_cast<const float*>(smem + ww * WTILE)[d * 16 + h];
     }
-    st_part<SC1>(&part_o[(((int64_t)b * Hq + hk * rep + h) * nsplit + split) * D + d], acc);
+    st_part(&part_o[(((int64_t)b * Hq + hk * rep + h) * nsplit + split) * D + d], acc, st);
     if (d == 0) {
-      st_part<SC1>(&pml[(int64_t)h * nsplit * 2], M);
-      st_part<SC1>(&pml[(int64_t)h * nsplit * 2 + 1], L);
+      st_part(&pml[(int64_t)h * nsplit * 2], M, st);
+      st_part(&pml[(int64_t)h * nsplit * 2 + 1], L, st);
     }
   }
 }
 
-template <bool FUSED>
+// proto (fused split merge, cnt != nullptr; 0 = partials only / combine kernel):
+//   1 = partials stored with agent-scope (sc1, write-through) atomic stores, read back with
+//       agent-scope atomic loads, no fences;
+//   2 = the same at system scope;
+//   3 = agent-scope stores, an agent-scope acquire fence in the merger, plain loads;
+//   4 = plain stores, one agent-scope release fence per workgroup (lane 0, after every wave's
+//       vmcnt drain), acquire fence in the merger, plain loads (guide §5 in-launch split-K recipe).
 __global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t* __restrict__ q,
                                                                   const uint16_t* __restrict__ kc,
                                                                   const uint16_t* __restrict__ vc,
@@ -378,7 +388,7 @@ __global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t
                                                                   int max_seq, int nsplit, float sl,
                                                                   const int32_t* __restrict__ bt, int maxb,
                                                                   uint16_t* __restrict__ out,
-                                                                  unsigned int* __restrict__ cnt) {
+                                                                  unsigned int* __restrict__ cnt, int proto) {
   constexpr int D = 128, WTILE = 64 * 256;  // 16 KiB per wave
   __shared__ __attribute__((aligned(16))) char smem[4 * WTILE];
   __shared__ float mls[4][2][16];
@@ -390,50 +400,60 @@ __global__ void __launch_bounds__(256, 2) decode_attn_mfma_kernel(const uint16_t
   const int k_lo = split * kSplit;
   const int k_hi = min(len, k_lo + kSplit);
   const int tid = threadIdx.x;
+  const bool fused = cnt != nullptr;
+  const int st = !fused ? 0 : proto == 2 ? 2 : proto == 4 ? 0 : 1;  // store mode of the partials
   float* pml = part_ml + (((int64_t)b * Hq + hk * rep) * nsplit + split) * 2;
   if (k_lo >= k_hi) {  // empty split (workgroup-uniform): neutral partial
     if (tid < rep) {
-      st_part<FUSED>(&pml[(int64_t)tid * nsplit * 2], -INFINITY);
-      st_part<FUSED>(&pml[(int64_t)tid * nsplit * 2 + 1], 0.f);
+      st_part(&pml[(int64_t)tid * nsplit * 2], -INFINITY, st);
+      st_part(&pml[(int64_t)tid * nsplit * 2 + 1], 0.f, st);
     }
   } else {
-    decode_split_body<FUSED>(q, kc, vc, part_o, pml, smem, mls, b, hk, rep, Hq, split, nsplit, k_lo, k_hi, slot,
-                             max_seq, sl, bt, maxb, Hkv);
+    decode_split_body(q, kc, vc, part_o, pml, smem, mls, b, hk, rep, Hq, split, nsplit, k_lo, k_hi, slot, max_seq,
+                      sl, bt, maxb, Hkv, st);
   }
-  if constexpr (FUSED) {
-    // In-launch combine: the last of the nsplit workgroups of this (seq, kv-head) to
-    // arrive merges the partials.  Partials were stored write-through (sc1) and every
-    // storing wave drains them before the barrier -> the relaxed agent-scope ticket
-    // publishes them; the merger reads them with sc1 loads (no L1 copy) and resets
-    // the counter, so it is zero again for the next call.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      unsigned int* c = cnt + (int64_t)b * Hkv + hk;
-      const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == (unsigned)(nsplit - 1);
-      if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = last;
+  if (!fused) return;
+  // In-launch combine: the last of the nsplit workgroups of this (seq, kv-head) to arrive
+  // merges the partials and resets the counter (zero again for the next call).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its partial stores done
+  __syncthreads();
+  if (tid == 0) {
+    unsigned int* c = cnt + (int64_t)b * Hkv + hk;
+    if (proto == 4) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    if (!s_last) return;
-    // the same arithmetic, in the same order, as decode_combine_kernel
-    for (int idx = tid; idx < rep * D; idx += 256) {
-      const int h = idx / D, d = idx % D;
-      const int64_t bh = (int64_t)b * Hq + hk * rep + h;
-      const float* ml = part_ml + bh * nsplit * 2;
-      float M = -INFINITY;
-      for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, ld_part(ml + 2 * sp));
-      float L = 0.f, acc = 0.f;
-      for (int sp = 0; sp < nsplit; ++sp) {
-        const float m = ld_part(ml + 2 * sp);
-        if (m == -INFINITY) continue;
-        const float wgt = __builtin_amdgcn_exp2f(m - M);
-        L += wgt * ld_part(ml + 2 * sp + 1);
-        acc += wgt * ld_part(part_o + (bh * nsplit + sp) * D + d);
+    const unsigned prev = proto == 2 ? __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                     : __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(nsplit - 1);
+    if (last) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (proto >= 3) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      out[bh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
     }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int ld = proto == 1 ? 1 : proto == 2 ? 2 : 0;
+  // the same arithmetic, in the same order, as decode_combine_kernel
+  for (int idx = tid; idx < rep * D; idx += 256) {
+    const int h = idx / D, d = idx % D;
+    const int64_t bh = (int64_t)b * Hq + hk * rep + h;
+    const float* ml = part_ml + bh * nsplit * 2;
+    float M = -INFINITY;
+    for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, ld_part(ml + 2 * sp, ld));
+    float L = 0.f, acc = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) {
+      const float m = ld_part(ml + 2 * sp, ld);
+      if (m == -INFINITY) continue;
+      const float wgt = __builtin_amdgcn_exp2f(m - M);
+      L += wgt * ld_part(ml + 2 * sp + 1, ld);
+      acc += wgt * ld_part(part_o + (bh * nsplit + sp) * D + d, ld);
+    }
+    out[bh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
   }
 }
 
@@ -607,14 +627,14 @@ extern "C" int mx_decode_attn(const uint16_t* q, const uint16_t* kc, const uint1
   const float sl = scale * 1.4426950408889634f;
   if (D == 128) {  // out == nullptr: partials only (the o-projection merges them: skinny_gemm.hip MERGE)
     // cnt (zeroed [B * Hkv] counters, owned by the caller): the splits merge in-launch
-    if (out && cnt) {
-      decode_attn_mfma_kernel<true><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq,
-                                                              Hkv, max_seq, nsplit, sl, bt, maxb, out, cnt);
-    } else {
-      decode_attn_mfma_kernel<false><<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq,
-                                                               Hkv, max_seq, nsplit, sl, bt, maxb, out, nullptr);
-      if (out) decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
-    }
+    // MXLLM_DECODE_HANDOFF: hand-off protocol of the in-launch merge (see the kernel; read per call)
+    const char* pe = getenv("MXLLM_DECODE_HANDOFF");
+    const int proto = pe && *pe ? atoi(pe) : 4;
+    const bool fused = out && cnt && proto >= 1 && proto <= 4;
+    decode_attn_mfma_kernel<<<grid, 256, 0, stream>>>(q, kc, vc, lens, len_off, slots, part_ml, part_o, Hq, Hkv,
+                                                      max_seq, nsplit, sl, bt, maxb, out, fused ? cnt : nullptr,
+                                                      proto);
+    if (out && !fused) decode_combine_kernel<128><<<B * Hq, 128, 0, stream>>>(part_ml, part_o, out, nsplit);
     return (int)hipGetLastError();
   }
   if (!out) return -1;

@@ -53,7 +53,8 @@ _ROPE_FUSED = os.environ.get("MXLLM_ROPE_FUSED", "1") != "0"  # A/B switch: RoPE
 _MERGE_FUSED = os.environ.get("MXLLM_MERGE_FUSED", "0") == "1"
 # Small-batch decode: while the (latency-bound) attention runs, a side-stream kernel reads
 # the layer's o-projection weight so the o-projection GEMM streams it from the Infinity
-# Cache instead of HBM (MXLLM_DECODE_PREFETCH=1; up to PREFETCH_MAX_B rows)
+# Cache instead of HBM (MXLLM_DECODE_PREFETCH=1; up to PREFETCH_MAX_B rows).  Measured
+# slower (fork/join + competing reads; profiles/r3g/README.md): off by default.
 _PREFETCH = os.environ.get("MXLLM_DECODE_PREFETCH", "0") == "1"
 PREFETCH_MAX_B = 8
 log = logging.getLogger("mxllm.engine")
@@ -142,9 +143,10 @@ class Engine:
         self.kv = KVCache(c.n_layers, c.n_kv_heads, c.head_dim, dt, self.device, n_slots, self.max_seq,
                           pool_tokens=kv_pool_tokens, block=kv_block,
                           scratch_slot=self.scratch_slot if self.use_graphs else None)
-        # decode attention: the split-K partials merge inside the attention launch (the last
-        # workgroup of each (seq, kv-head) combines; these counters stay zero between calls),
-        # no separate combine kernel; MXLLM_DECODE_COMBINE=kernel keeps the two-launch form
+        # MXLLM_DECODE_COMBINE=fused: the split-K partials merge inside the attention launch (the
+        # last workgroup of each (seq, kv-head) combines; these counters stay zero between calls)
+        # instead of the combine kernel -- measured slower in the graphed step at every batch
+        # (profiles/r3g/README.md), so off by default
         self._attn_cnt = None
         if self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_COMBINE", "kernel") == "fused":
             self._attn_cnt = torch.zeros((n_slots + 64) * self.kv.k[0].shape[1], dtype=torch.int32,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU pass G: in-launch decode split merge (sc1 hand-off) — numerics, engine
+# Round-3 GPU pass G: in-launch decode split merge (hand-off protocols) — numerics, engine
 # tests, 8B serve A/B vs the combine kernel; lora_xwt in-launch split reduction A/B;
 # LDS-staged lora_xwt A/B on the 70B headline.
 set -e
@@ -7,6 +7,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $ROOT
 O=gpurun_out/r3g
 mkdir -p $O
+timeout -k 10 300 python -u bench/decode_handoff_stress.py > $O/handoff_stress.log 2>&1
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_model_gpu.py tests/test_kvcache.py tests/test_serve.py tests/test_sampling.py > $O/tests.log 2>&1
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k lora > $O/lora_tests.log 2>&1
 timeout -k 10 300 python -u bench/lora_xwt_ab.py > $O/xwt_ab2.log 2>&1
