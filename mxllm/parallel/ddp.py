@@ -31,13 +31,14 @@ log = logging.getLogger("mxllm.ddp")
 
 
 class Bucket:
-    __slots__ = ("start", "end", "pending", "expected", "work", "index", "seen")
+    __slots__ = ("start", "end", "pending", "expected", "work", "index", "seen", "fired")
 
     def __init__(self, index: int, start: int, end: int, expected: int):
         self.index, self.start, self.end, self.expected = index, start, end, expected
         self.pending = expected
         self.work = None
         self.seen = set()
+        self.fired = False  # all-reduce launched / on_ready called this step
 
 
 class DDP:
@@ -68,13 +69,28 @@ class DDP:
         self._timing = self.enabled
         self._last_events = None
         self._hooks = []
+        self.on_ready = None  # callback(bucket) once a bucket's gradient is final (set_on_ready)
         if self.enabled:
-            for p, bi in zip(flat.param_list, self._param_bucket):
-                hook = self._make_hook(bi)
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                p._mx_on_grad_ready = hook  # ops that accumulate grads themselves (fused LoRA)
+            self._register_hooks()
         log.debug("DDP: %d buckets over %d params (%.1f MB), world=%d", len(self.buckets), len(slots),
                   flat.numel * esz / 2 ** 20, self.world)
+
+    def _register_hooks(self):
+        if self._hooks:
+            return
+        for p, bi in zip(self.flat.param_list, self._param_bucket):
+            hook = self._make_hook(bi)
+            self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+            p._mx_on_grad_ready = hook  # ops that accumulate grads themselves (fused LoRA)
+
+    def set_on_ready(self, fn) -> None:
+        """Call ``fn(bucket)`` as soon as a bucket's gradient is final for the step:
+        right after its all-reduce is issued (``bucket.work``: the pending collective;
+        wait on it on the stream that reads the bucket), or, with no all-reduce
+        (world 1), when its last gradient is written.  Buckets whose hooks did not
+        all fire are handed over in ``finish``."""
+        self.on_ready = fn
+        self._register_hooks()
 
     @property
     def bytes_per_step(self) -> int:
@@ -97,8 +113,12 @@ class DDP:
         return hook
 
     def _launch(self, b: Bucket):
-        g = self.flat.grads[b.start:b.end]
-        b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self.enabled:
+            g = self.flat.grads[b.start:b.end]
+            b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        b.fired = True
+        if self.on_ready is not None:
+            self.on_ready(b)
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -113,11 +133,14 @@ class DDP:
     def finish(self) -> float:
         """Wait for every bucket (launching any whose hooks did not all fire, e.g.
         unused params) and return the gradient scale (1/world) to apply."""
-        if not self.enabled:
+        if not self.enabled and self.on_ready is None:
             return 1.0
         for b in self.buckets:
-            if b.work is None and self._sync:
+            if not b.fired and self._sync:
                 self._launch(b)
+        if not self.enabled:
+            self.reset()
+            return 1.0
         timing = self._timing and torch.cuda.is_available() and self.flat.grads.is_cuda
         if timing:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -126,6 +149,7 @@ class DDP:
             if b.work is not None:
                 b.work.wait()
             b.work = None
+            b.fired = False
             b.pending = b.expected
             b.seen.clear()
         if timing:
@@ -146,6 +170,7 @@ class DDP:
     def reset(self):
         for b in self.buckets:
             b.work = None
+            b.fired = False
             b.pending = b.expected
             b.seen.clear()
 

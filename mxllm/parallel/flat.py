@@ -126,20 +126,25 @@ class FlatParams:
         self.grads.zero_()
         self.attach_grads()
 
-    def sync_grads_from_params(self):
+    def sync_grads_from_params(self) -> list[int]:
         """If autograd replaced a .grad (dtype mismatch / detached), copy it back
-        (fp32 mode: fold any ``.grad`` left behind into the fp32 buffer)."""
-        for p, s in zip(self._plist, self.slots):
+        (fp32 mode: fold any ``.grad`` left behind into the fp32 buffer).  Returns
+        the indices of the slots written here."""
+        changed = []
+        for k, (p, s) in enumerate(zip(self._plist, self.slots)):
             g = p.grad
             if g is None:
                 continue
             if self.grad32:
                 self._fold_hook(p)
+                changed.append(k)
                 continue
             flat = self.grads[s.offset:s.offset + s.numel]
             if g.data_ptr() != flat.data_ptr():
                 flat.copy_(g.reshape(-1))
                 p.grad = flat.view(s.shape)
+                changed.append(k)
+        return changed
 
     def state_dict(self):
         return {"slots": [(s.name, s.offset, s.numel, list(s.shape)) for s in self.slots], "numel": self.numel}

@@ -115,6 +115,17 @@ class Trainer:
         self.fresh_grads = (os.environ.get("MXLLM_FRESH_GRADS", "1") != "0" and self.flat.device.type == "cuda"
                             and self.zero1 is None and not getattr(model, "lora", False)
                             and not any(getattr(p, "_mx_no_direct", False) for p in self.flat.param_list))
+        # ---- gradient-norm overlap: each DDP bucket's sum of squares is taken on a side
+        # stream as soon as the bucket is final (after its all-reduce), under the rest of
+        # the backward, instead of one pass over the whole gradient after it (8B full:
+        # 16 GB, ~3 ms on the critical path); a fixed-order sum of the per-bucket values
+        # gives the clip coefficient (deterministic, identical on every rank)
+        self._norm_side = None
+        if (self.opt.grad_clip and self.opt.grad_clip > 0 and self.zero1 is None
+                and self.flat.device.type == "cuda" and os.environ.get("MXLLM_NORM_OVERLAP", "1") != "0"):
+            self._norm_side = torch.cuda.Stream(self.flat.device)
+            self._bsq = torch.zeros(len(self.ddp.buckets), dtype=torch.float32, device=self.flat.device)
+            self.ddp.set_on_ready(self._bucket_sq_norm)
 
     @property
     def lowp(self):
@@ -218,6 +229,15 @@ class Trainer:
                 ev.record(side)
                 self._pending[k] = ev
 
+    def _bucket_sq_norm(self, b) -> None:
+        """DDP on_ready callback: sum of squares of bucket ``b`` on the norm stream."""
+        side = self._norm_side
+        side.wait_stream(torch.cuda.current_stream(self.flat.device))
+        with torch.cuda.stream(side):
+            if b.work is not None:
+                b.work.wait()  # this stream waits for the bucket's all-reduce
+            self._bsq[b.index:b.index + 1].copy_(ops.sq_norm(self.flat.grads[b.start:b.end]))
+
     def train_step(self, micro_batches: list[tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """One optimizer step over ``micro_batches`` [(ids, labels), ...].
         Returns the mean loss as a device tensor (no host sync)."""
@@ -249,11 +269,17 @@ class Trainer:
                 with range_("backward"):
                     (loss / n if n > 1 else loss).backward()
             total = loss.detach() if total is None else total + loss.detach()
-        self.flat.sync_grads_from_params()
+        fired = [b.fired for b in self.ddp.buckets]
+        changed = self.flat.sync_grads_from_params()
         if self.fresh_grads:
             self.flat.zero_unwritten_()
         with range_("grad_allreduce_wait"):
             scale = self.ddp.finish() / n if n > 1 else self.ddp.finish()
+        if self._norm_side is not None and changed:
+            # a gradient folded into the flat buffer after its bucket's norm was taken
+            for bi in sorted({self.ddp._param_bucket[k] for k in changed}):
+                if fired[bi]:
+                    self._bucket_sq_norm(self.ddp.buckets[bi])
         return total, scale
 
     def _optimizer_step(self, scale: float):
@@ -263,7 +289,11 @@ class Trainer:
         if o.grad_clip and o.grad_clip > 0:
             # global grad norm on device; the clip coefficient is applied inside
             # the fused AdamW kernel via grad_scale (host read only for logging)
-            sq = ops.sq_norm(grads)
+            if self._norm_side is not None:  # per-bucket partials taken during the backward
+                torch.cuda.current_stream(self.flat.device).wait_stream(self._norm_side)
+                sq = self._bsq.sum(0, keepdim=True)
+            else:
+                sq = ops.sq_norm(grads)
             if z is not None:
                 from ..parallel.runtime import all_reduce_small_
 

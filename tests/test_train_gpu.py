@@ -235,3 +235,33 @@ def test_split_master_adamw_kernel_bitwise(gpu, gbf16, zero):
     assert torch.equal(m1, m2) and torch.equal(v1, v2)
     bits = p32.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     assert torch.equal(sm.hi.view(torch.int16).to(torch.int64) & 0xFFFF, ((bits + 0x8000) >> 16) & 0xFFFF)
+
+
+@pytest.mark.parametrize("gdt", [None, torch.float32])
+@pytest.mark.parametrize("accum", [1, 2])
+def test_bucketed_grad_norm_overlap(gpu, gdt, accum, monkeypatch):
+    """The clip norm from per-bucket sums of squares taken on a side stream during the
+    backward (MXLLM_NORM_OVERLAP, default) equals the one-pass norm after the backward
+    (to fp32 summation order), with and without micro-batch accumulation; small
+    first bucket so the model spans several buckets."""
+    from mxllm.train.trainer import Trainer  # noqa: F401
+
+    cfg = _cfg()
+    g = torch.Generator(device=gpu).manual_seed(5)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=g) for _ in range(2 * accum)]
+    norms, masters = {}, {}
+    for ov in ("1", "0"):
+        monkeypatch.setenv("MXLLM_NORM_OVERLAP", ov)
+        tr = _ddp_trainer(gpu, cfg, 13, grad_dtype=gdt, bucket_mb=1.0, first_bucket_mb=0.25)
+        assert (tr._norm_side is not None) == (ov == "1")
+        if ov == "1":
+            assert len(tr.ddp.buckets) > 3
+        ns = []
+        for i in range(2):
+            tr.train_step([(b, b) for b in batches[i * accum:(i + 1) * accum]])
+            ns.append(float(tr.last_grad_norm))
+        norms[ov], masters[ov] = ns, _masters(tr)
+    for a, b in zip(norms["1"], norms["0"]):
+        assert abs(a - b) <= 1e-5 * b, (norms)
+    for n, w in masters["0"].items():
+        assert (masters["1"][n] - w).abs().max().item() <= 1e-6, n
