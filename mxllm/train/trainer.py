@@ -105,7 +105,16 @@ class Trainer:
             if self._chunks is not None:
                 self._side = torch.cuda.Stream(self.flat.device) if self.flat.device.type == "cuda" else None
                 model.param_wait = self._param_wait
+                if self._side is not None and os.environ.get("MXLLM_STEP_PRIORITY", "0") == "1":
+                    # forward/backward on a HIGH-priority stream, the overlapped AdamW on the
+                    # lowest: as AdamW workgroups retire, the dispatcher hands the freed CUs to
+                    # the step's kernels first (AdamW fills the gaps instead of delaying them)
+                    least, greatest = torch.cuda.Stream.priority_range()
+                    self._side = torch.cuda.Stream(self.flat.device, priority=least)
+                    self._main = torch.cuda.Stream(self.flat.device, priority=greatest)
         self.overlap_optimizer = self._chunks is not None
+        if not hasattr(self, "_main"):
+            self._main = None
         # "fresh" gradients: every gradient of the step is formed by an op that can
         # OVERWRITE its flat slot (dW GEMMs with beta 0, the RMSNorm / embedding
         # kernels' accum_grad), so AdamW need not zero the gradient buffer behind
@@ -122,7 +131,7 @@ class Trainer:
         # gives the clip coefficient (deterministic, identical on every rank)
         self._norm_side = None
         if (self.opt.grad_clip and self.opt.grad_clip > 0 and self.zero1 is None
-                and self.flat.device.type == "cuda" and os.environ.get("MXLLM_NORM_OVERLAP", "1") != "0"):
+                and self.flat.device.type == "cuda" and os.environ.get("MXLLM_NORM_OVERLAP", "0") == "1"):
             self._norm_side = torch.cuda.Stream(self.flat.device)
             self._bsq = torch.zeros(len(self.ddp.buckets), dtype=torch.float32, device=self.flat.device)
             self.ddp.set_on_ready(self._bucket_sq_norm)
@@ -241,6 +250,16 @@ class Trainer:
     def train_step(self, micro_batches: list[tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """One optimizer step over ``micro_batches`` [(ids, labels), ...].
         Returns the mean loss as a device tensor (no host sync)."""
+        if self._main is not None:  # MXLLM_STEP_PRIORITY: the step on the high-priority stream
+            cur = torch.cuda.current_stream(self.flat.device)
+            self._main.wait_stream(cur)
+            with torch.cuda.stream(self._main):
+                out = self._train_step(micro_batches)
+            cur.wait_stream(self._main)
+            return out
+        return self._train_step(micro_batches)
+
+    def _train_step(self, micro_batches):
         total, scale = self.compute_grads(micro_batches)
         self.step_num += 1
         with range_("optimizer"):

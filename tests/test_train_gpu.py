@@ -241,7 +241,7 @@ def test_split_master_adamw_kernel_bitwise(gpu, gbf16, zero):
 @pytest.mark.parametrize("accum", [1, 2])
 def test_bucketed_grad_norm_overlap(gpu, gdt, accum, monkeypatch):
     """The clip norm from per-bucket sums of squares taken on a side stream during the
-    backward (MXLLM_NORM_OVERLAP, default) equals a one-pass norm of the final gradient
+    backward (MXLLM_NORM_OVERLAP=1; measured neutral, off by default) equals a one-pass norm of the final gradient
     buffer at every step (fp32 summation order aside), with and without micro-batch
     accumulation, and the first step's norm equals the non-overlapped trainer's; small
     buckets so the model spans several."""
