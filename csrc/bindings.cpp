@@ -148,13 +148,20 @@ void copy2d_batched(const at::Tensor& desc, int64_t total_blocks) {
 }
 
 // out[C, R] = in[R, C]^T for a row-major (row-strided) 16-bit 2-D GPU tensor
-at::Tensor transpose2d(const at::Tensor& in) {
+// scale: optional f32 device scalar (bf16 input): out = bf16(in^T * scale)
+at::Tensor transpose2d(const at::Tensor& in, const c10::optional<at::Tensor>& scale) {
   MX_CHECK(in.is_cuda() && in.dim() == 2 && in.element_size() == 2, "in must be a 2-D 16-bit GPU tensor");
   MX_CHECK(in.stride(1) == 1 && in.stride(0) >= in.size(1), "in must be a row-major (row-strided) view");
+  const float* sc = nullptr;
+  if (scale.has_value()) {
+    MX_CHECK(in.scalar_type() == at::kBFloat16 && scale->scalar_type() == at::kFloat && scale->numel() == 1 &&
+                 scale->device() == in.device(), "transpose2d scale: f32 scalar on the device, bf16 input");
+    sc = scale->data_ptr<float>();
+  }
   DevGuard g(in.device());
   const int64_t R = in.size(0), C = in.size(1);
   auto out = at::empty({C, R}, in.options());
-  MX_OK(mx_transpose16(in.data_ptr(), out.data_ptr(), R, C, in.stride(0), R, cur_stream()));
+  MX_OK(mx_transpose16(in.data_ptr(), out.data_ptr(), R, C, in.stride(0), R, sc, cur_stream()));
   return out;
 }
 
@@ -308,6 +315,22 @@ at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V)
   auto dw = at::zeros({V, H}, dy.options().dtype(at::kFloat));
   MX_OK(mx_embedding_bwd(idc.data_ptr<int64_t>(), bf(dy), dw.data_ptr<float>(), T, (int)H, V, cur_stream()));
   return dw;
+}
+
+// out[V, H] (bf16 or f32, contiguous) += the batch's rows of dW, computed from the stably
+// sorted ids (sid) and their positions (perm): only touched rows read / written.
+void embedding_bwd_sorted(const at::Tensor& dy, const at::Tensor& sid, const at::Tensor& perm, at::Tensor out) {
+  check_bf16(dy, "dy");
+  MX_CHECK(sid.scalar_type() == at::kLong && perm.scalar_type() == at::kLong && sid.is_contiguous() &&
+               perm.is_contiguous() && sid.numel() == perm.numel(), "sid / perm: int64, same length");
+  MX_CHECK(out.is_contiguous() && (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16) &&
+               out.dim() == 2 && out.size(1) == dy.size(-1) && dy.is_contiguous() &&
+               dy.numel() == sid.numel() * dy.size(-1) && out.device() == dy.device(),
+           "embedding_bwd_sorted: out [V, H] f32/bf16 contiguous, dy [T, H] contiguous");
+  DevGuard g(dy.device());
+  MX_OK(mx_embedding_bwd_sorted(bf(dy), sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), sid.numel(),
+                                (int)out.size(1), out.size(0), out.data_ptr(), out.scalar_type() == at::kFloat ? 1 : 0,
+                                cur_stream()));
 }
 
 // ---------------------------------------------------------------- cross-entropy
@@ -860,7 +883,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, bool need_dw, int out_pad=0) -> (Tensor, Tensor)");
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
-  m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("transpose2d(Tensor x, Tensor? scale=None) -> Tensor");
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
@@ -870,6 +893,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("join_master(Tensor hi, Tensor lo, Tensor(a!) out) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor w) -> Tensor");
   m.def("embedding_bwd(Tensor dy, Tensor ids, int V) -> Tensor");
+  m.def("embedding_bwd_sorted(Tensor dy, Tensor sid, Tensor perm, Tensor(a!) out) -> ()");
   m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
   m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
@@ -909,6 +933,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("join_master", &join_master);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("embedding_bwd_sorted", &embedding_bwd_sorted);
   m.impl("ce_fwd_bwd", &ce_fwd_bwd);
   m.impl("rope_split", &rope_split);
   m.impl("rope_merge_bwd", &rope_merge_bwd);

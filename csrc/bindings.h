@@ -20,7 +20,7 @@ int mx_sqnorm(const void* x, int bf16, int64_t n, float* out, float* work, hipSt
 int mx_copy2d_batched(const int64_t* desc, int n, int64_t total_blocks, hipStream_t stream);
 int mx_prefetch(const void* p, int64_t bytes, int wgs, hipStream_t stream);
 int mx_transpose16(const void* in, void* out, int64_t R, int64_t C, int64_t ld_in, int64_t ld_out,
-                   hipStream_t stream);
+                   const float* scale, hipStream_t stream);
 }
 
 extern "C" {
@@ -35,6 +35,8 @@ int mx_split_master(const float* x, uint16_t* hi, int16_t* lo, int64_t n, hipStr
 int mx_join_master(const uint16_t* hi, const int16_t* lo, float* x, int64_t n, hipStream_t stream);
 int mx_embedding_fwd(const int64_t* ids, const uint16_t* w, uint16_t* out, int64_t T, int H, int64_t V,
                      hipStream_t stream);
+int mx_embedding_bwd_sorted(const uint16_t* dy, const int64_t* sid, const int64_t* perm, int64_t T, int H,
+                            int64_t V, void* out, int out_f32, hipStream_t stream);
 int mx_embedding_bwd(const int64_t* ids, const uint16_t* dy, float* dw, int64_t T, int H, int64_t V,
                      hipStream_t stream);
 // cross_entropy.hip

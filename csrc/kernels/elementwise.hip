@@ -183,9 +183,59 @@ __global__ void __launch_bounds__(256) embedding_bwd_kernel(const int64_t* __res
   for (int c = threadIdx.x; c < H; c += 256) atomicAdd(dst + c, bf2f(src[c]));
 }
 
+// Sparse, deterministic embedding backward into the parameter's own gradient buffer:
+// sid = the batch's token ids sorted (stable), perm = their positions.  A workgroup per
+// segment START (first position of each distinct id) sums that id's dy rows in sorted
+// order in fp32 and adds the sum into row sid[i] of `out` (fp32, or bf16 with one
+// rounding) -- only the rows the batch touched are read or written, instead of
+// zero-filling and casting a full [V, H] fp32 accumulator.  Grid-stride over positions.
+template <bool F32>
+__global__ void __launch_bounds__(256) embedding_bwd_sorted_kernel(const uint16_t* __restrict__ dy,
+                                                                   const int64_t* __restrict__ sid,
+                                                                   const int64_t* __restrict__ perm, int64_t T,
+                                                                   int H, int64_t V, void* __restrict__ out) {
+  for (int64_t i = blockIdx.x; i < T; i += gridDim.x) {
+    const int64_t row = sid[i];
+    if ((i > 0 && sid[i - 1] == row) || row < 0 || row >= V) continue;  // workgroup-uniform
+    int64_t end = i + 1;
+    while (end < T && sid[end] == row) ++end;
+    for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int64_t j = i; j < end; ++j) {
+        const u16x8 v = *reinterpret_cast<const u16x8*>(dy + perm[j] * H + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+      }
+      if constexpr (F32) {
+        float* o = reinterpret_cast<float*>(out) + row * H + c;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += acc[e];
+      } else {
+        uint16_t* o = reinterpret_cast<uint16_t*>(out) + row * H + c;
+        u16x8 cur = *reinterpret_cast<const u16x8*>(o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cur[e] = f2bf(bf2f(cur[e]) + acc[e]);
+        *reinterpret_cast<u16x8*>(o) = cur;
+      }
+    }
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
+
+extern "C" int mx_embedding_bwd_sorted(const uint16_t* dy, const int64_t* sid, const int64_t* perm, int64_t T, int H,
+                                       int64_t V, void* out, int out_f32, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8) return -1;
+  const unsigned grid = (unsigned)(T < 8192 ? T : 8192);
+  if (out_f32)
+    embedding_bwd_sorted_kernel<true><<<grid, 256, 0, stream>>>(dy, sid, perm, T, H, V, out);
+  else
+    embedding_bwd_sorted_kernel<false><<<grid, 256, 0, stream>>>(dy, sid, perm, T, H, V, out);
+  return (int)hipGetLastError();
+}
 
 static int grid_for(int64_t items) {
   int64_t b = (items + 255) / 256;

@@ -142,9 +142,14 @@ extern "C" int mx_sqnorm(const void* x, int bf16, int64_t n, float* out, float* 
 namespace mx {
 constexpr int kTrTile = 64;
 
+// scale != nullptr (bf16 data): out = bf16(in * *scale), the scalar read on the device (the
+// cross-entropy backward's upstream gradient folded into the dW operand's transpose)
 __global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                          int64_t R, int64_t C, int64_t ld_in, int64_t ld_out) {
+                                                          int64_t R, int64_t C, int64_t ld_in, int64_t ld_out,
+                                                          const float* __restrict__ scale) {
   __shared__ uint16_t tile[kTrTile][kTrTile + 2];
+  const float sc = scale ? *scale : 1.f;
+  auto cv = [&](uint16_t x) -> uint16_t { return scale ? f2bf(bf2f(x) * sc) : x; };
   const int64_t r0 = (int64_t)blockIdx.y * kTrTile, c0 = (int64_t)blockIdx.x * kTrTile;
   const int t = threadIdx.x, sub = t & 7, row = t >> 3;  // 8 threads x 8 elements per row
   const bool full = (r0 + kTrTile <= R) && (c0 + kTrTile <= C) && (ld_in % 8 == 0) && (ld_out % 8 == 0);
@@ -169,26 +174,26 @@ __global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __rest
       const int c = row + 32 * p;  // output row (input column)
       u16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = tile[sub * 8 + j][c];
+      for (int j = 0; j < 8; ++j) v[j] = cv(tile[sub * 8 + j][c]);
       *reinterpret_cast<u16x8*>(out + (c0 + c) * ld_out + r0 + sub * 8) = v;
     }
   } else {
     for (int e = t; e < kTrTile * kTrTile; e += 256) {
       const int c = e / kTrTile, r = e % kTrTile;
-      if (r0 + r < R && c0 + c < C) out[(c0 + c) * ld_out + r0 + r] = tile[r][c];
+      if (r0 + r < R && c0 + c < C) out[(c0 + c) * ld_out + r0 + r] = cv(tile[r][c]);
     }
   }
 }
 }  // namespace mx
 
 extern "C" int mx_transpose16(const void* in, void* out, int64_t R, int64_t C, int64_t ld_in, int64_t ld_out,
-                              hipStream_t stream) {
+                              const float* scale, hipStream_t stream) {
   if (R <= 0 || C <= 0) return 0;
   if (ld_in < C || ld_out < R) return -1;
   const int64_t gx = (C + kTrTile - 1) / kTrTile, gy = (R + kTrTile - 1) / kTrTile;
   if (gy > 65535 || gx > 0x7fffffff) return -1;
   transpose16_kernel<<<dim3((unsigned)gx, (unsigned)gy), 256, 0, stream>>>(
-      reinterpret_cast<const uint16_t*>(in), reinterpret_cast<uint16_t*>(out), R, C, ld_in, ld_out);
+      reinterpret_cast<const uint16_t*>(in), reinterpret_cast<uint16_t*>(out), R, C, ld_in, ld_out, scale);
   return (int)hipGetLastError();
 }
 

@@ -1,18 +1,26 @@
 """Token embedding gather / scatter-add.
 
-GPU: csrc/kernels/embedding.hip — forward is a 16-B-vectorised row gather
-(one wave per token row); backward adds rows into an f32 [V, H] accumulator
-with no-return f32 atomics shaped as full 256-B wave instructions (the chip's
-atomic path runs at ~1.3 TB/s, far above what 4k-token steps need), then
-casts to the parameter dtype.
+GPU: csrc/kernels/elementwise.hip — forward is a 16-B-vectorised row gather
+(one wave per token row).  Backward, when the parameter's owner exposes its
+gradient buffer (DDP flat grads, bf16 or fp32): the batch's ids are stably
+sorted and one workgroup per distinct id sums its dy rows in fp32 and adds them
+into that row of the buffer (touched rows only, deterministic).  Otherwise: rows
+added into an f32 [V, H] accumulator with no-return f32 atomics (256-B wave
+instructions), then cast to the parameter dtype.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
-from ..parallel.grad_ready import accum_grad, deliver_grad
+import os
+
+from ..parallel.grad_ready import accum_grad, deliver_grad, direct_grad, direct_grad32, mark_ready
 from ._ext import native, use_native
+
+# sparse backward straight into the owner's gradient buffer (touched rows only); 0 = the
+# dense f32 accumulator path (A/B)
+_SPARSE_BWD = os.environ.get("MXLLM_EMB_SPARSE_BWD", "1") != "0"
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -30,6 +38,21 @@ class _EmbeddingFn(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         if not ctx.needs_input_grad[1]:
             return None, None
+        if ctx.nat and _SPARSE_BWD and ctx.wp is not None:
+            # the owner's buffer (fp32 accumulation target, else the preallocated .grad):
+            # zero it when this is the step's first write, then add only the rows of the
+            # batch's tokens, each summed over its occurrences in a fixed order
+            t = direct_grad32(ctx.wp)
+            if t is None:
+                t = direct_grad(ctx.wp)
+            if t is not None and t.is_contiguous() and t.dim() == 2:
+                if getattr(ctx.wp, "_mx_grad_fresh", False):
+                    t.zero_()
+                    ctx.wp._mx_grad_fresh = False
+                sid, perm = torch.sort(ids.reshape(-1), stable=True)
+                native().embedding_bwd_sorted(dy.reshape(-1, dy.shape[-1]).contiguous(), sid, perm, t)
+                mark_ready(ctx.wp)
+                return None, None
         if ctx.nat:
             dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab)  # f32 accumulator
         else:

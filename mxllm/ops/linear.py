@@ -223,20 +223,23 @@ def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: tor
     return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt, wa)
 
 
-def transpose2d(t: torch.Tensor) -> torch.Tensor:
+def transpose2d(t: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:
     """Contiguous ``t.T`` of a 2-D row-major (row-strided) 16-bit tensor: the
-    LDS-tiled HIP transpose on GPU (csrc/kernels/misc.hip), torch on CPU."""
+    LDS-tiled HIP transpose on GPU (csrc/kernels/misc.hip), torch on CPU.
+    ``scale``: optional 1-element f32 device tensor multiplied in (bf16 ``t``)."""
     if use_native(t):
         if t.stride(-1) != 1:
             t = t.contiguous()
-        return native().transpose2d(t)
-    return t.t().contiguous()
+        return native().transpose2d(t, scale)
+    out = t.t().contiguous()
+    return out if scale is None else (out * scale.to(out.dtype))
 
 
 _DW_TN = os.environ.get("MXLLM_DW_TN", "1") != "0"
 
 
-def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
+def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, beta: float = 1.0,
+                 dy_scale: torch.Tensor | None = None) -> torch.Tensor:
     """dW = dy^T x (reduction over the token dimension), accumulated into
     ``out`` (``out = beta * out + dW``; beta 0 ignores whatever ``out`` held)
     when given.
@@ -247,16 +250,20 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, be
     token-contiguous images by the HIP transpose (4.4-6.4 TB/s) and the GEMM
     runs in the reduction-contiguous form the forward uses: dW = dyT @ xT^T,
     12-20 % faster including the transposes
-    (bench/dw_layout_probe.py, profiles/r1e_dw_layout_probe.md)."""
+    (bench/dw_layout_probe.py, profiles/r1e_dw_layout_probe.md).
+    ``dy_scale``: 1-element device tensor multiplying dy (folded into dy's
+    transpose on that path; the cross-entropy's upstream gradient)."""
     f32 = out is not None and out.dtype == torch.float32 and dy.dtype != torch.float32
     if _DW_TN and use_native(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
         xt = transpose2d(x)
-        dyt = transpose2d(dy)
+        dyt = transpose2d(dy, None if dy_scale is None else dy_scale.reshape(1).float())
         if out is None:
             return torch.mm(dyt, xt.t())
         if f32:  # bf16 operands, fp32 accumulate-into output (hipBLASLt D = C in fp32)
             return torch.ops.aten.addmm.dtype_out(out, dyt, xt.t(), torch.float32, beta=beta, out=out)
         return out.addmm_(dyt, xt.t(), beta=beta)
+    if dy_scale is not None:
+        dy = dy * dy_scale.to(dy.dtype)
     if out is None:
         return torch.mm(dy.t(), x)
     if f32:
@@ -266,7 +273,8 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, be
     return out.addmm_(dy.t(), x, beta=beta)
 
 
-def param_weight_grad(wp: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor | None:
+def param_weight_grad(wp: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor,
+                      dy_scale: torch.Tensor | None = None) -> torch.Tensor | None:
     """Weight gradient of parameter ``wp`` for a backward pass.
 
     When an owner pre-attached ``wp.grad`` (the trainer's flat grad buffer, or a
@@ -280,9 +288,9 @@ def param_weight_grad(wp: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor
     if g is None and wp is not None:
         g = direct_grad32(wp)  # fp32 gradient accumulation: the GEMM writes fp32
     if g is None:
-        return weight_grad_(None, dy, x)
+        return weight_grad_(None, dy, x, dy_scale=dy_scale)
     fresh = getattr(wp, "_mx_grad_fresh", False)
-    weight_grad_(g, dy, x, beta=0.0 if fresh else 1.0)
+    weight_grad_(g, dy, x, beta=0.0 if fresh else 1.0, dy_scale=dy_scale)
     if fresh:
         wp._mx_grad_fresh = False
     mark_ready(wp)

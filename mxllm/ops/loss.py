@@ -31,19 +31,17 @@ class _LinearCEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl):
         # the upstream scalar gradient ``gl`` stays on device (no host read to
-        # test for 1.0): it scales dlogits once when the head's weight gradient
-        # is formed too (both GEMMs then read the scaled logits), else only the
-        # small [T, H] dh
+        # test for 1.0): it scales the small [T, H] dh, and the head's dW through
+        # the transpose that forms dlogits' token-contiguous image (no extra pass
+        # over the [T, V] dlogits)
         h, w, dlogits = ctx.saved_tensors
         dh = dw = None
-        if ctx.needs_input_grad[1]:
-            dlogits.mul_(gl.to(dlogits.dtype))
         if ctx.needs_input_grad[0]:
             dh = torch.matmul(dlogits, w)
-            if not ctx.needs_input_grad[1]:
-                dh.mul_(gl.to(dh.dtype))
+            dh.mul_(gl.to(dh.dtype))  # [T, H]: cheap, unlike scaling the [T, V] dlogits
         if ctx.needs_input_grad[1]:
-            dw = param_weight_grad(ctx.wp, dlogits, h)
+            # the head's dW: gl folded into dlogits' transpose (token-contiguous operand image)
+            dw = param_weight_grad(ctx.wp, dlogits, h, dy_scale=gl)
         return dh, dw, None, None
 
 
