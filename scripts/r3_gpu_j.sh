@@ -9,6 +9,7 @@ cd $ROOT
 O=gpurun_out/r3j
 mkdir -p $O
 MXLLM_STEP_PRIORITY=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_train_gpu.py -k "overlapped or bench" > $O/tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "embedding or transpose" tests/test_train_gpu.py tests/test_model_gpu.py > $O/tests2.log 2>&1
 B="python bench.py --model llama3.1-8b --finetune full --steps 10 --warmup 3 --config2 off --config3 off --config4 off"
 for r in 1 2; do
   timeout -k 10 200 $B --json-out $O/8b_base_$r.json > $O/8b_base_$r.log 2>&1
