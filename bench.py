@@ -306,6 +306,37 @@ def run_config4(a, world: int) -> dict:
     return res
 
 
+# peak HBM RESERVED by the caching allocator for a world-1 run of a configuration (driver record
+# BENCH_r02.json / profiles/r3h/bench_default.json), and the activation memory one checkpointed
+# layer gives back (70B, 2 x 2048 tokens: ~150 GB of activations over 80 layers)
+RESERVED_GB = {("llama3.1-70b", "lora", 2, 2048): (294.3, 1.7)}
+RCCL_ALLOWANCE_GB = 3.0  # communicator buffers + DDP bucket slack at world > 1
+
+
+def memory_guard(a, env) -> dict | None:
+    """At world > 1 the headline runs beside RCCL's buffers with ~15 GB of HBM to spare at
+    world 1.  If the smallest free HBM over the ranks is below the world-1 reserved peak plus
+    an RCCL allowance, checkpoint just enough layers to fit (every rank takes the same decision
+    from the all-reduced minimum) instead of risking an out-of-memory error mid-step, which
+    would strand the other ranks in a collective.  Returns the record of that decision, or
+    None when the configuration fits as is."""
+    from mxllm.parallel import runtime
+
+    key = (a.model, a.finetune, a.micro_batch, a.seq_len)
+    if env.device.type != "cuda" or env.world_size == 1 or a.act_ckpt or a.layers or key not in RESERVED_GB:
+        return None
+    need, per_layer = RESERVED_GB[key]
+    need += RCCL_ALLOWANCE_GB
+    free = runtime.all_reduce_scalars([torch.cuda.mem_get_info(env.device)[0] / 1e9], op="min")[0]
+    if free >= need:
+        return None
+    import math
+
+    n = math.ceil((need - free) / per_layer) + 2
+    a.act_ckpt, a.act_ckpt_layers = True, n
+    return {"min_free_hbm_gb": round(free, 1), "need_gb": round(need, 1), "checkpointed_layers": n}
+
+
 def run(a, env) -> dict:
     """Build the trainer, run W warm-up + K timed steps, return the JSON dict."""
     from mxllm.models import Llama, get_config
@@ -317,6 +348,7 @@ def run(a, env) -> dict:
     from mxllm.utils import gemm_tuning
 
     tuned = gemm_tuning.enable() if not a.no_gemm_table else False
+    guard = memory_guard(a, env)
     cfg = get_config(a.model)
     if a.layers:
         cfg = cfg.replace(n_layers=a.layers)
@@ -462,6 +494,8 @@ def run(a, env) -> dict:
                                   if k in gpu_sample},
         "trainable_params": (cfg.n_params() if a.parallel == "zero3" else model.num_params(trainable_only=True)),
     }
+    if guard is not None:
+        out["memory_guard"] = guard
     if emulated:
         out["emulated_world"] = emulated
         out["note"] = ("PROXY: one GPU holding one rank's world-%d shards; value/ms exclude all collective "

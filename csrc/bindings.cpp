@@ -166,6 +166,20 @@ at::Tensor transpose2d(const at::Tensor& in, const c10::optional<at::Tensor>& sc
 }
 
 // read `t` once on the current stream (cache warm-up of a weight ahead of its consumer; misc.hip)
+// A HIP stream confined to a subset of the device's CUs (hipExtStreamCreateWithCUMask):
+// ``mask`` = one int per 32 CUs (bit i of word w = CU 32 w + i).  Returns the stream handle
+// for torch.cuda.ExternalStream; the stream lives for the process (never destroyed).
+int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
+  MX_CHECK(!mask.empty(), "cu_masked_stream: empty mask");
+  DevGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  std::vector<uint32_t> w(mask.size());
+  for (size_t i = 0; i < mask.size(); ++i) w[i] = (uint32_t)(mask[i] & 0xffffffffLL);
+  hipStream_t s = nullptr;
+  hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)(w.size() * 32), w.data());
+  MX_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return (int64_t)reinterpret_cast<intptr_t>(s);
+}
+
 void prefetch(const at::Tensor& t, int64_t wgs) {
   MX_CHECK(t.is_cuda() && t.is_contiguous(), "prefetch: contiguous GPU tensor");
   DevGuard g(t.device());
@@ -885,6 +899,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
   m.def("transpose2d(Tensor x, Tensor? scale=None) -> Tensor");
   m.def("prefetch(Tensor t, int wgs) -> ()");
+  m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");

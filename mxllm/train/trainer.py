@@ -104,6 +104,10 @@ class Trainer:
             self._chunks = self._forward_chunks()
             if self._chunks is not None:
                 self._side = torch.cuda.Stream(self.flat.device) if self.flat.device.type == "cuda" else None
+                cus = os.environ.get("MXLLM_ADAMW_CUS", "")
+                if self._side is not None and cus:
+                    # the overlapped AdamW confined to a CU subset (the forward keeps the rest)
+                    self._side = cu_masked_stream(self.flat.device, cus)
                 model.param_wait = self._param_wait
                 if self._side is not None and os.environ.get("MXLLM_STEP_PRIORITY", "0") == "1":
                     # forward/backward on a HIGH-priority stream, the overlapped AdamW on the
@@ -113,6 +117,11 @@ class Trainer:
                     self._side = torch.cuda.Stream(self.flat.device, priority=least)
                     self._main = torch.cuda.Stream(self.flat.device, priority=greatest)
         self.overlap_optimizer = self._chunks is not None
+        # MXLLM_ADAMW_LAG=L > 0: only chunks [0, L) are issued at the end of the step; the next
+        # forward issues chunk k + L when it reaches group k, ordered after its own progress, so
+        # the update is spread over the forward instead of saturating HBM under its first layers
+        self._lag = int(os.environ.get("MXLLM_ADAMW_LAG", "0") or 0)
+        self._deferred: list = []
         if not hasattr(self, "_main"):
             self._main = None
         # "fresh" gradients: every gradient of the step is formed by an op that can
@@ -194,6 +203,8 @@ class Trainer:
         k = self._group_chunk.get(id(group))
         if k is None or k >= len(self._pending):
             return
+        if self._deferred:
+            self._issue_deferred(k + self._lag, after_current=True)
         ev = self._pending[k]
         if ev is not None:
             torch.cuda.current_stream(self.flat.device).wait_event(ev)
@@ -205,6 +216,8 @@ class Trainer:
         parameters outside a forward (checksums, checkpoints, export)."""
         if self.zero1 is not None:
             self.zero1.wait_params()
+        if self._deferred:
+            self._issue_deferred(len(self._pending), after_current=False)
         for k, ev in enumerate(self._pending):
             if ev is not None:
                 torch.cuda.current_stream(self.flat.device).wait_event(ev)
@@ -229,14 +242,36 @@ class Trainer:
         self._hold = gscale  # read on the side stream: keep it alive until the next step
         if len(self._pending) != len(self._chunks):
             self._pending = [None] * len(self._chunks)
+        n_now = len(self._chunks) if self._lag <= 0 else min(self._lag, len(self._chunks))
+        self._deferred = [(k, gscale, kw) for k in range(n_now, len(self._chunks))]
         with torch.cuda.stream(side):
-            for k, (lo, hi) in enumerate(self._chunks):
-                ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
-                                None if lowp is None else lowp[lo:hi], grad_scale=gscale,
-                                zero_grad=not self.fresh_grads, **kw)
-                ev = torch.cuda.Event()
-                ev.record(side)
-                self._pending[k] = ev
+            for k in range(n_now):
+                self._adamw_chunk(k, gscale, kw, side)
+
+    def _adamw_chunk(self, k, gscale, kw, side):
+        lo, hi = self._chunks[k]
+        lowp = self.lowp
+        ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
+                        None if lowp is None else lowp[lo:hi], grad_scale=gscale,
+                        zero_grad=not self.fresh_grads, **kw)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        self._pending[k] = ev
+
+    def _issue_deferred(self, upto: int, after_current: bool):
+        """Issue the deferred AdamW chunks with index < ``upto`` (MXLLM_ADAMW_LAG);
+        ``after_current``: the side stream first waits for the compute stream's
+        current position (the forward has reached that layer)."""
+        todo = [d for d in self._deferred if d[0] < upto]
+        if not todo:
+            return
+        self._deferred = [d for d in self._deferred if d[0] >= upto]
+        side = self._side
+        if after_current:
+            side.wait_stream(torch.cuda.current_stream(self.flat.device))
+        with torch.cuda.stream(side):
+            for k, gscale, kw in todo:
+                self._adamw_chunk(k, gscale, kw, side)
 
     def _bucket_sq_norm(self, b) -> None:
         """DDP on_ready callback: sum of squares of bucket ``b`` on the norm stream."""
@@ -288,6 +323,8 @@ class Trainer:
                 with range_("backward"):
                     (loss / n if n > 1 else loss).backward()
             total = loss.detach() if total is None else total + loss.detach()
+        if self._deferred:  # a forward that skipped parameter groups: nothing may stay un-updated
+            self._issue_deferred(len(self._pending), after_current=False)
         fired = [b.fired for b in self.ddp.buckets]
         changed = self.flat.sync_grads_from_params()
         if self.fresh_grads:
@@ -379,6 +416,40 @@ class Trainer:
         elif self.flat.master is not self.flat.params and not isinstance(self.flat.master, ops.SplitMaster):
             self.flat.params.copy_(self.flat.master)
         self._sync_adapters()
+
+
+_MASKED: dict = {}
+
+
+def cu_masked_stream(device: torch.device, spec: str) -> torch.cuda.ExternalStream:
+    """A stream confined to a CU subset (csrc/bindings.cpp ``cu_masked_stream``).
+    ``spec``: ``first:K`` (CU bits 0..K-1), ``mod8:K`` (K of every 8 consecutive
+    bits), ``stride:K`` (every K-th bit) or a hex mask ``0x...``."""
+    from ..ops._ext import native
+
+    key = (str(device), spec)
+    if key in _MASKED:  # one HIP stream (and hardware queue) per mask for the process
+        return _MASKED[key]
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    if spec.startswith("0x"):
+        bits = int(spec, 16)
+        on = [i for i in range(ncu) if (bits >> i) & 1]
+    else:
+        kind, k = spec.split(":")
+        k = int(k)
+        pick = {"first": lambda i: i < k, "mod8": lambda i: i % 8 < k, "stride": lambda i: i % k == 0}[kind]
+        on = [i for i in range(ncu) if pick(i)]
+    if not on:
+        raise ValueError(f"CU mask {spec!r} selects no CU")
+    words = [0] * ((ncu + 31) // 32)
+    for i in on:
+        words[i // 32] |= 1 << (i % 32)
+    words = [w - (1 << 32) if w >= 1 << 31 else w for w in words]  # int64 schema, low 32 bits used
+    ptr = native().cu_masked_stream(device.index if device.index is not None else torch.cuda.current_device(),
+                                    words)
+    log.info("AdamW stream on %d of %d CUs (%s)", len(on), ncu, spec)
+    _MASKED[key] = torch.cuda.ExternalStream(ptr, device=device)
+    return _MASKED[key]
 
 
 class _null:

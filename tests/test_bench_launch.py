@@ -93,3 +93,29 @@ def test_world8_rehearsal_with_config3_and_config4():
     assert "error" not in c4, c4
     assert c4["config"]["parallelism"] == "zero3-dp8" and c4["config"]["grad_reduce_dtype"] == "fp32"
     assert "tiny" in c4["label"] and "70B" not in c4["label"]
+
+
+def test_memory_guard_checkpoints_only_when_short(monkeypatch):
+    """At world > 1 the 70B headline checkpoints just enough layers when the smallest free HBM
+    over the ranks is below the world-1 reserved peak + the RCCL allowance; never otherwise."""
+    sys.path.insert(0, ROOT)
+    import types
+
+    import torch
+
+    import bench
+    from mxllm.parallel import runtime
+
+    env = types.SimpleNamespace(device=torch.device("cuda", 0), world_size=8)
+    need = bench.RESERVED_GB[("llama3.1-70b", "lora", 2, 2048)][0] + bench.RCCL_ALLOWANCE_GB
+    for free, expect in ((need + 5.0, None), (need - 10.0, 10)):
+        monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d, f=free: (int(f * 1e9), int(309.2e9)))
+        monkeypatch.setattr(runtime, "all_reduce_scalars", lambda xs, op="sum": list(xs))
+        a = bench.parse([])
+        g = bench.memory_guard(a, env)
+        if expect is None:
+            assert g is None and not a.act_ckpt
+        else:
+            assert g["checkpointed_layers"] >= 10 * 1 / 1.7 and a.act_ckpt and a.act_ckpt_layers == g["checkpointed_layers"]
+    a = bench.parse([])
+    assert bench.memory_guard(a, types.SimpleNamespace(device=torch.device("cuda", 0), world_size=1)) is None

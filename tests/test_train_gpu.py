@@ -45,15 +45,27 @@ def _masters(tr):
     return {s.name: tr.flat.master[s.offset:s.offset + s.numel].view(s.shape).clone() for s in tr.flat.slots}
 
 
-@pytest.mark.parametrize("gdt", [None, torch.float32])
-def test_overlapped_adamw_bitwise(gpu, gdt):
+@pytest.mark.parametrize("gdt,sched", [(None, ""), (torch.float32, ""), (None, "lag"), (None, "cus")])
+def test_overlapped_adamw_bitwise(gpu, gdt, sched, monkeypatch):
+    """``sched``: "lag" = chunks issued one group ahead of the forward (MXLLM_ADAMW_LAG=1);
+    "cus" = the AdamW side stream confined to a CU subset (MXLLM_ADAMW_CUS)."""
     cfg = _cfg()
     g = torch.Generator(device=gpu).manual_seed(1)
     batches = [torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=g) for _ in range(3)]
     out = {}
     for ovl in (False, True):
+        monkeypatch.delenv("MXLLM_ADAMW_LAG", raising=False)
+        monkeypatch.delenv("MXLLM_ADAMW_CUS", raising=False)
+        if ovl and sched == "lag":
+            monkeypatch.setenv("MXLLM_ADAMW_LAG", "1")
+        if ovl and sched == "cus":
+            monkeypatch.setenv("MXLLM_ADAMW_CUS", "mod8:2")
         tr = _ddp_trainer(gpu, cfg, 11, overlap_optimizer=ovl, grad_dtype=gdt)
         assert tr.overlap_optimizer == ovl
+        if ovl and sched == "lag":
+            assert tr._lag == 1
+        if ovl and sched == "cus":
+            assert isinstance(tr._side, torch.cuda.ExternalStream)
         losses = [float(tr.train_step([(b, b)])) for b in batches]
         out[ovl] = (losses, _masters(tr))
     assert out[False][0] == out[True][0]
