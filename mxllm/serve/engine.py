@@ -546,13 +546,17 @@ class Engine:
         self.tp_sync = True
         self._tp_stop = False
 
-    def _sync_admit(self, admit: list) -> list:
+    def _sync_admit(self, admit: list, stopping: bool = False) -> list:
+        """``stopping`` (rank 0): broadcast the stop sentinel instead of admissions.  It is
+        an argument, not a read of ``self._stop``: a stop() arriving mid-step must not turn
+        this step's broadcast into the sentinel while rank 0 still runs the step's
+        collectives (the followers would have left them)."""
         import torch.distributed as dist
 
         src = dist.get_global_rank(self.tp.group, 0)
         dev = self.device if dist.get_backend(self.tp.group) == "nccl" else torch.device("cpu")
         if self.tp.rank == 0:
-            payload = [None if self._stop else [(r.prompt, r.params) for r in admit]]
+            payload = [None if stopping else [(r.prompt, r.params) for r in admit]]
             dist.broadcast_object_list(payload, src=src, group=self.tp.group, device=dev)
             return admit
         payload = [None]
@@ -677,7 +681,7 @@ class Engine:
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
             sync = getattr(self, "tp_sync", False)
-            while not self._stop:
+            while True:  # leaves only through the stop branch, which always tells the followers
                 with self._cv:
                     while not self._stop and not self.waiting and not self.active and not self._tasks:
                         self._cv.wait(timeout=0.5)
@@ -687,7 +691,7 @@ class Engine:
                     self._run_tasks()
                 if self._stop:
                     if sync:
-                        self._sync_admit([])  # tells the followers to stop
+                        self._sync_admit([], stopping=True)  # tells the followers to stop
                     break
                 try:
                     self.step()
