@@ -28,6 +28,8 @@ extern "C" {
 int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream);
 int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
                   hipStream_t stream);
+int mx_dw_gemm(const uint16_t* dy, int64_t lda, const uint16_t* x, int64_t ldb, void* out, int64_t ldc, int out_f32,
+               int M, int N, int T, float beta, const float* alpha_t, float alpha_f, hipStream_t stream);
 int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int16_t* lo, int64_t n,
              float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t,
              float scale_f, int zero_grad, hipStream_t stream);
