@@ -65,6 +65,10 @@ def main():
                 os.environ["MXLLM_DW_GEMM"] = "ring"
                 assert native().dw_gemm(dy, x, out_k, beta, None)
 
+            def w8():
+                os.environ["MXLLM_DW_GEMM"] = "w8"
+                assert native().dw_gemm(dy, x, out_k, beta, None)
+
             def tn():
                 xt, dyt = transpose2d(x), transpose2d(dy)
                 if a.f32:
@@ -79,11 +83,11 @@ def main():
                     out_n.addmm_(dy.t(), x, beta=beta)
 
             res = {}
-            for name, fn in (("kernel", kern), ("ring", ring), ("tn_total", tn), ("nt", nt)):
+            for name, fn in (("kernel", kern), ("ring", ring), ("w8", w8), ("tn_total", tn), ("nt", nt)):
                 res[name] = timeit(fn)
             # numerics after one call each from zero
             err = {}
-            for name, fn in (("kernel", kern), ("ring", ring)):
+            for name, fn in (("kernel", kern), ("ring", ring), ("w8", w8)):
                 out_k.zero_(), out_t.zero_()
                 fn(), tn()
                 torch.cuda.synchronize()

@@ -34,7 +34,6 @@
 namespace mx {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int CH>
 __device__ __forceinline__ int swz(int row) {
@@ -57,7 +56,7 @@ __device__ __forceinline__ u16x4 tr_read(const char* p) {
 // NW waves per workgroup = 32 NW query rows sharing every streamed K/V tile (2 waves per SIMD
 // either way).  4 by default; 8 halves the K/V tile traffic per FLOP but measured the same
 // (0.259 vs 0.257 ms at B2 S2048 Hq64 Hkv8 D128 causal: the stream is not the limiter)
-template <int D, bool CAUSAL, int NW, bool PROF = false, bool PK = true>
+template <int D, bool CAUSAL, int NW, bool PROF = false>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
@@ -268,35 +267,16 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         for (int d = 0; d < DB; ++d) o[d] *= alpha;
       }
       const float nm = -m_i;
-      if constexpr (PK) {
-        // exp2 arguments and row sums on packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two elements
-        // per VALU instruction); two independent packed partial sums
-        const f32x2 sl2 = {sl, sl}, nm2 = {nm, nm};
-        f32x2 lp2[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+      float lp[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent partial sums
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < 2; ++n)
 #pragma unroll
-          for (int j = 0; j < 16; j += 2) {
-            const f32x2 arg = __builtin_elementwise_fma(f32x2{sacc[n][j], sacc[n][j + 1]}, sl2, nm2);
-            const f32x2 p2 = {__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};
-            sacc[n][j] = p2[0];
-            sacc[n][j + 1] = p2[1];
-            lp2[(j >> 1) & 1] += p2;
-          }
-        const f32x2 t = lp2[0] + lp2[1];
-        l_i += t[0] + t[1];
-      } else {
-        float lp[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent partial sums
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][j], sl, nm));
-            sacc[n][j] = p;
-            lp[j & 3] += p;
-          }
-        l_i += (lp[0] + lp[1]) + (lp[2] + lp[3]);
-      }
+        for (int j = 0; j < 16; ++j) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][j], sl, nm));
+          sacc[n][j] = p;
+          lp[j & 3] += p;
+        }
+      l_i += (lp[0] + lp[1]) + (lp[2] + lp[3]);
       if constexpr (PROF) asm volatile("" ::"v"(l_i));
       mark(1);
 #pragma unroll
@@ -756,20 +736,9 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_FWD_FLAGS");   // (B2 0.192 -> 0.186 ms, B16 1.372 -> 1.357 ms)
     return e && *e ? atoi(e) : 1;
   }();
-  static const bool fpk = [] {  // MXLLM_ATTN_FWD_PK=1: packed-fp32 softmax arithmetic (A/B; default off until measured)
-    const char* e = getenv("MXLLM_ATTN_FWD_PK");
-    return e && e[0] == '1';
-  }();
-#define FWD(DD, C, NWV)                                                                                       \
-  do {                                                                                                        \
-    const unsigned grid_ = ((S + 32 * NWV - 1) / (32 * NWV)) * B * Hq;                                        \
-    if (fpk)                                                                                                  \
-      attn_fwd_kernel<DD, C, NWV, false, true><<<grid_, 64 * NWV, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, \
-                                                                               Sk, off, sl, ldo, fflags);     \
-    else                                                                                                      \
-      attn_fwd_kernel<DD, C, NWV, false, false><<<grid_, 64 * NWV, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv,  \
-                                                                                S, Sk, off, sl, ldo, fflags); \
-  } while (0)
+#define FWD(DD, C, NWV)                                                                                  \
+  attn_fwd_kernel<DD, C, NWV><<<((S + 32 * NWV - 1) / (32 * NWV)) * B * Hq, 64 * NWV, 0, stream>>>(     \
+      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
   static const bool fprof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report (D = 128, 4 waves; stderr)
     const char* e = getenv("MXLLM_ATTN_PROF");
     return e && e[0] == '1';

@@ -51,19 +51,19 @@ constexpr int kDwNB = 4;                  // stage ring: 128 KiB of LDS
 
 // lane holds C[m0 + 128 wm + 32 i + 8 (r / 4) + 4 hh + r % 4][n0 + 128 wn + 32 j + lane % 32]; per m-block
 // the 64 old values (beta) are loaded before any store (independent loads in flight)
-template <bool OUT_F32, bool BETA>
-__device__ __forceinline__ void dw_epilogue(const f32x16 (&acc)[4][4], void* __restrict__ C, int64_t ldc, int m0,
+template <bool OUT_F32, bool BETA, int NJ = 4>
+__device__ __forceinline__ void dw_epilogue(const f32x16 (&acc)[4][NJ], void* __restrict__ C, int64_t ldc, int m0,
                                             int n0, int wm, int wn, int hh, int lane, float alpha) {
-  const int ncol = n0 + 128 * wn + (lane & 31);
+  const int ncol = n0 + 32 * NJ * wn + (lane & 31);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    float old[4][16];
+    float old[NJ][16];
     if constexpr (BETA) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t m = m0 + 128 * wm + 32 * i + 8 * (r >> 2) + 4 * hh + (r & 3);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const int64_t idx = m * ldc + ncol + 32 * j;
           if constexpr (OUT_F32)
             old[j][r] = reinterpret_cast<const float*>(C)[idx];
@@ -76,7 +76,7 @@ __device__ __forceinline__ void dw_epilogue(const f32x16 (&acc)[4][4], void* __r
     for (int r = 0; r < 16; ++r) {
       const int64_t m = m0 + 128 * wm + 32 * i + 8 * (r >> 2) + 4 * hh + (r & 3);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         float v = acc[i][j][r] * alpha;
         if constexpr (BETA) v += old[j][r];
         const int64_t idx = m * ldc + ncol + 32 * j;
@@ -385,6 +385,146 @@ dw_gemm_dbuf_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
   dw_epilogue<OUT_F32, BETA>(acc, C, ldc, m0, n0, wm, wn, hh, lane, alpha_f * (alpha_t ? alpha_t[0] : 1.f));
 }
 
+
+// 8-wave form (MXLLM_DW_GEMM=w8): 2 waves per SIMD (guide §5 template geometry), each wave
+// 128 (m) x 64 (n) = 4 x 2 blocks (128 accumulators), the same 4-stage BK-32 ring as the 4-wave
+// ring form; while one wave of a SIMD waits on its transposed reads the other issues MFMAs.
+template <bool OUT_F32, bool BETA>
+__global__ void __launch_bounds__(512, 1)
+dw_gemm_w8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+                  void* __restrict__ C, int64_t ldc, int M, int N, int T, const float* __restrict__ alpha_t,
+                  float alpha_f) {
+  __shared__ __attribute__((aligned(1024))) char smem[kDwNB * kDwStage];
+  const int nM = M / kDwBM, nN = N / kDwBN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int pm, pn;
+  {
+    constexpr int GM = 4;
+    const int per = GM * nN, grp = L / per, first = grp * GM;
+    const int rows = min(GM, nM - first), in = L - grp * per;
+    pm = first + in % rows;
+    pn = in / rows;
+  }
+  const int m0 = pm * kDwBM, n0 = pn * kDwBN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  // per stage and operand 16 pieces; wave w stores pieces 2 w, 2 w + 1 of both (4 glds)
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 2 * (2 * w + i) + (lane >> 5), pc = lane & 31;
+    const int lc = dphys(pc, row);
+    aoff[i] = row * (int)lda + 8 * lc;
+    boff[i] = row * (int)ldb + 8 * lc;
+  }
+  const uint16_t* Ab = A + m0;
+  const uint16_t* Bb = B + n0;
+  auto issue = [&](int kt) __attribute__((always_inline)) {
+    const uint16_t* a = Ab + (int64_t)kt * kDwBK * lda;
+    const uint16_t* b = Bb + (int64_t)kt * kDwBK * ldb;
+    char* da = smem + (kt % kDwNB) * kDwStage;
+    char* db = da + kDwHalf;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_global_load_lds((dgptr_t)(a + aoff[i]), (dlptr_t)(da + (2 * w + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((dgptr_t)(b + boff[i]), (dlptr_t)(db + (2 * w + i) * 1024), 16, 0, 0);
+    }
+  };
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3, hh = lane >> 5;
+  const int rA = 4 * hh + tq, rB = 8 + 4 * hh + tq;
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t abase[4][2], bbase[2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int la = wm * 16 + 4 * i + 2 * (g & 1) + (tp >> 1);
+    abase[i][0] = lds0 + rA * kDwRowB + 16 * dphys(la, rA) + 8 * (tp & 1);
+    abase[i][1] = lds0 + rB * kDwRowB + 16 * dphys(la, rB) + 8 * (tp & 1);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int lb = wn * 8 + 4 * j + 2 * (g & 1) + (tp >> 1);
+    bbase[j][0] = lds0 + kDwHalf + rA * kDwRowB + 16 * dphys(lb, rA) + 8 * (tp & 1);
+    bbase[j][1] = lds0 + kDwHalf + rB * kDwRowB + 16 * dphys(lb, rB) + 8 * (tp & 1);
+  }
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = T / kDwBK;
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2);
+    const uint32_t so = (uint32_t)(kt % kDwNB) * kDwStage;
+    uint32_t ab[4][2], bb[2][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ab[i][0] = abase[i][0] + so;
+      ab[i][1] = abase[i][1] + so;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bb[j][0] = bbase[j][0] + so;
+      bb[j][1] = bbase[j][1] + so;
+    }
+    u16x4 fa[2][4][2], fb[2][2][2];
+    auto read = [&](int p, int ks) __attribute__((always_inline)) {  // 12 reads (<= 15 outstanding)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        fb[p][j][0] = trd_off(bb[j][0], ks * 16 * kDwRowB);
+        fb[p][j][1] = trd_off(bb[j][1], ks * 16 * kDwRowB);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[p][i][0] = trd_off(ab[i][0], ks * 16 * kDwRowB);
+        fa[p][i][1] = trd_off(ab[i][1], ks * 16 * kDwRowB);
+      }
+    };
+    read(0, 0);
+    lds_wait();
+#pragma unroll
+    for (int ks = 0; ks < kDwBK / 16; ++ks) {
+      const int p = ks & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pin(fa[p][i][0]);
+        pin(fa[p][i][1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        pin(fb[p][j][0]);
+        pin(fb[p][j][1]);
+      }
+      const bool nxt = ks + 1 < kDwBK / 16;
+      if (nxt) read(p ^ 1, ks + 1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const u16x8 a = u16x8{fa[p][i][0][0], fa[p][i][0][1], fa[p][i][0][2], fa[p][i][0][3],
+                              fa[p][i][1][0], fa[p][i][1][1], fa[p][i][1][2], fa[p][i][1][3]};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const u16x8 b = u16x8{fb[p][j][0][0], fb[p][j][0][1], fb[p][j][0][2], fb[p][j][0][3],
+                                fb[p][j][1][0], fb[p][j][1][1], fb[p][j][1][2], fb[p][j][1][3]};
+          acc[i][j] = mfma32d(a, b, acc[i][j]);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (nxt) lds_wait();
+    }
+  }
+  dw_epilogue<OUT_F32, BETA, 2>(acc, C, ldc, m0, n0, wm, wn, hh, lane, alpha_f * (alpha_t ? alpha_t[0] : 1.f));
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -401,14 +541,16 @@ extern "C" int mx_dw_gemm(const uint16_t* dy, int64_t lda, const uint16_t* x, in
   if (beta != 0.f && beta != 1.f) return -1;
   const int grid = (M / kDwBM) * (N / kDwBN);
   const bool acc = beta != 0.f;
-  // MXLLM_DW_GEMM=ring: the 4-stage ring form (BK 32, two stages in flight across barriers); default:
-  // the double-buffered BK-64 form (read per call: same-process A/B)
+  // MXLLM_DW_GEMM (read per call: same-process A/B): w8 (default, fastest: profiles/r3m) = 8 waves on
+  // the 4-stage BK-32 ring; ring = 4 waves on that ring; dbuf = 4 waves, two BK-64 buffers
   const char* fe = getenv("MXLLM_DW_GEMM");
-  const bool ring = fe && fe[0] == 'r';
-  if (!ring && T % kD1BK) return -1;
+  const bool ring = fe && fe[0] == 'r', w8 = !(fe && (fe[0] == 'r' || fe[0] == 'd'));
+  if (!ring && !w8 && T % kD1BK) return -1;
 #define DW_LAUNCH(F, BT)                                                                                        \
   do {                                                                                                          \
-    if (ring)                                                                                                   \
+    if (w8)                                                                                                     \
+      dw_gemm_w8_kernel<F, BT><<<grid, 512, 0, stream>>>(dy, lda, x, ldb, out, ldc, M, N, T, alpha_t, alpha_f);  \
+    else if (ring)                                                                                              \
       dw_gemm_kernel<F, BT><<<grid, 256, 0, stream>>>(dy, lda, x, ldb, out, ldc, M, N, T, alpha_t, alpha_f);     \
     else                                                                                                        \
       dw_gemm_dbuf_kernel<F, BT><<<grid, 256, 0, stream>>>(dy, lda, x, ldb, out, ldc, M, N, T, alpha_t, alpha_f); \

@@ -9,5 +9,3 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k dw_gemm -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 timeout -k 10 300 python -u bench/dw_gemm_probe.py > $O/probe_bf16.jsonl 2> $O/probe_bf16.err
 timeout -k 10 300 python -u bench/dw_gemm_probe.py --f32 --models 70b > $O/probe_f32.jsonl 2> $O/probe_f32.err
-timeout -k 10 600 python -u bench/adamw_overlap_ab.py --rounds 2 --json-out $O/ab.jsonl \
-  tn= kernel=MXLLM_DW_KERNEL=1 > $O/ab.log 2>&1

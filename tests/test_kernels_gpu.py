@@ -666,7 +666,7 @@ def test_embedding_sparse_backward(gpu, target, fresh):
     (4096, 1024, 512, 0, True, 0.0, False),
     (320, 768, 256, 8, False, 1.0, True),
 ])
-@pytest.mark.parametrize("form", ["dbuf", "ring"])
+@pytest.mark.parametrize("form", ["dbuf", "ring", "w8"])
 def test_dw_gemm_token_major(gpu, T, M, N, ldpad, f32, beta, scaled, form, monkeypatch):
     """csrc/kernels/dw_gemm.hip: out = beta out + s dy^T x on token-major operands (row-strided views,
     fp32 / bf16 output) vs an fp32 PyTorch reference; both pipeline forms (MXLLM_DW_GEMM)."""
