@@ -610,13 +610,8 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         for (int y = 0; y < 4; ++y) pin(x[y]);
         sa = mfma32b(x[0], x[1], sa);
         dp = mfma32b(x[2], x[3], dp);
-        if (prio & 128) {  // early spread: pieces at k steps 0-3, lse / delta at step 4 (more slack)
-          if (spread && st < 4 && more) glds_piece(nx_hj, nx_it, buf ^ 1, st);
-          if (spread && st == 4 && more) glds_piece(nx_hj, nx_it, buf ^ 1, 4);
-        } else {
-          if (spread && (st & 1) == 0 && more) glds_piece(nx_hj, nx_it, buf ^ 1, st >> 1);
-          if (spread && st == KS - 1 && more) glds_piece(nx_hj, nx_it, buf ^ 1, 4);
-        }
+        if (spread && (st & 1) == 0 && more) glds_piece(nx_hj, nx_it, buf ^ 1, st >> 1);
+        if (spread && st == KS - 1 && more) glds_piece(nx_hj, nx_it, buf ^ 1, 4);
       }
     }
     mark(1);
@@ -1045,8 +1040,8 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   float* dqk = dq_mode == 1 ? dq : reinterpret_cast<float*>(work);
   const bool bwd8 = attn_bwd8_on();
   // MXLLM_ATTN_BWD8_PRIO (bit flags, default 17): 1 = s_setprio 1 for waves 4-7, 16 = spread the
-  // DMA / dS-store issue over the MFMA steps (128: over the first half of them); 2 = timing
-  // ablation (same q tile every step, wrong results)
+  // DMA / dS-store issue over the MFMA steps; 2 = timing ablation (same q tile every step, wrong
+  // results)
   static const int bwd8_prio = [] {
     const char* e = getenv("MXLLM_ATTN_BWD8_PRIO");
     return e && *e ? atoi(e) : 17;
