@@ -1,0 +1,31 @@
+"""Compare the logged losses of an uninterrupted fine-tune with a checkpoint + resume run.
+usage: python scripts/compare_resume.py full.jsonl part1.jsonl part2.jsonl"""
+import json
+import sys
+
+
+def load(p):
+    out = {}
+    for line in open(p):
+        r = json.loads(line)
+        if "loss" in r and "step" in r:
+            out[int(r["step"])] = float(r["loss"])
+    return out
+
+
+def main():
+    full, p1, p2 = (load(p) for p in sys.argv[1:4])
+    resumed = {**p1, **p2}
+    steps = sorted(set(full) & set(resumed))
+    worst = 0.0
+    for s in steps:
+        d = abs(full[s] - resumed[s])
+        worst = max(worst, d)
+        print(f"step {s:4d}  uninterrupted {full[s]:.5f}  resumed {resumed[s]:.5f}  |diff| {d:.2e}")
+    first, last = min(full), max(full)
+    print(f"loss {full[first]:.4f} (step {first}) -> {full[last]:.4f} (step {last}); "
+          f"max |uninterrupted - resumed| over {len(steps)} logged steps: {worst:.3e}")
+
+
+if __name__ == "__main__":
+    main()
