@@ -1,4 +1,5 @@
-"""A/B of the overlapped-AdamW scheduling on the 8B full fine-tune step (BASELINE config 2).
+"""Same-process A/B of env-switched variants of a bench workload (default: the 8B full fine-tune
+step, BASELINE config 2; ``--model llama3.1-70b --finetune lora``: the headline).
 
 Every variant runs ``bench.run`` in THIS process (one model init per variant, rounds
 interleaved so clock/thermal drift hits every variant alike) and prints one JSON line:
@@ -27,6 +28,7 @@ def main():
     ap.add_argument("--model", default="llama3.1-8b")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--finetune", default="full", choices=["full", "lora"])
     ap.add_argument("--json-out", default=None)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
@@ -48,7 +50,7 @@ def main():
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(kv)
-            b = bench.parse(["--model", a.model, "--finetune", "full", "--steps", str(a.steps), "--warmup",
+            b = bench.parse(["--model", a.model, "--finetune", a.finetune, "--steps", str(a.steps), "--warmup",
                              str(a.warmup)])
             t0 = time.time()
             try:

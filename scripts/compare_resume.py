@@ -15,7 +15,7 @@ def load(p):
 
 def main():
     full, p1, p2 = (load(p) for p in sys.argv[1:4])
-    resumed = {**p1, **p2}
+    resumed = {**p1, **p2}  # steps logged again after the resume (150..159) come from the resumed run
     steps = sorted(set(full) & set(resumed))
     worst = 0.0
     for s in steps:
