@@ -53,8 +53,15 @@ class _EmbeddingFn(torch.autograd.Function):
                 native().embedding_bwd_sorted(dy.reshape(-1, dy.shape[-1]).contiguous(), sid, perm, t)
                 mark_ready(ctx.wp)
                 return None, None
-        if ctx.nat:
-            dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab)  # f32 accumulator
+        if ctx.nat and _SPARSE_BWD:
+            # no owner buffer (e.g. tied embeddings: autograd sums this with the head's gradient):
+            # the same sorted, fixed-order row sums into a zeroed f32 [V, H] -- deterministic, unlike
+            # the atomic accumulator below (its fp32 add order varies run to run)
+            dw = torch.zeros(ctx.vocab, dy.shape[-1], dtype=torch.float32, device=dy.device)
+            sid, perm = torch.sort(ids.reshape(-1), stable=True)
+            native().embedding_bwd_sorted(dy.reshape(-1, dy.shape[-1]).contiguous(), sid, perm, dw)
+        elif ctx.nat:
+            dw = native().embedding_bwd(dy.contiguous(), ids, ctx.vocab)  # f32 accumulator (atomics)
         else:
             dy2 = dy.reshape(-1, dy.shape[-1])
             dw = torch.zeros(ctx.vocab, dy2.shape[1], dtype=torch.float32, device=dy.device)

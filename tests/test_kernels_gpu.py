@@ -660,6 +660,28 @@ def test_embedding_sparse_backward(gpu, target, fresh):
     assert torch.equal(again, first)
 
 
+def test_embedding_backward_tied_is_deterministic(gpu):
+    """No owner buffer (tied embeddings: autograd sums the embedding and head gradients): the
+    embedding gradient comes from the same sorted, fixed-order kernel into a zeroed fp32 [V, H]
+    -- equal to an fp32 index_add reference and bitwise the same on every call (the atomic
+    accumulator it replaces made tied-embedding training differ run to run)."""
+    from mxllm.ops.embedding import embedding
+
+    torch.manual_seed(3)
+    V, H = 5000, 512
+    ids = torch.randint(0, 64, (2048,), device=gpu)  # flat token ids (as the model passes them), heavy repetition
+    dy = torch.randn(2048, H, device=gpu).bfloat16()
+    grads = []
+    for _ in range(3):
+        w = torch.nn.Parameter(torch.zeros(V, H, device=gpu).bfloat16())
+        w._mx_no_direct = True
+        embedding(ids, w).backward(dy)
+        grads.append(w.grad.float().clone())
+    ref = torch.zeros(V, H, device=gpu).index_add_(0, ids.reshape(-1), dy.reshape(-1, H).float())
+    assert rel_err(grads[0], ref) < 1e-2
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
 @pytest.mark.parametrize("T,M,N,ldpad,f32,beta,scaled", [
     (64, 256, 256, 0, False, 0.0, False),
     (192, 512, 768, 64, True, 1.0, True),
