@@ -101,6 +101,12 @@ def parse(argv=None):
     ap.add_argument("--config3", choices=["auto", "on", "off"], default="auto",
                     help="also measure BASELINE config 3 (Llama-3.1-8B FULL fine-tune, DDP over all N GPUs) "
                          "in-process after the headline; auto = when the headline runs on 8 GPUs")
+    ap.add_argument("--config3-timeout", type=float, default=300.0,
+                    help="hard limit for the config-3 child job; the headline line is printed either way")
+    ap.add_argument("--config2-mb4", choices=["auto", "on", "off"], default="auto",
+                    help="with config 2: also measure it at micro-batch 4 (the reference's batch of 4)")
+    ap.add_argument("--no-calibrate", dest="calibrate", action="store_false",
+                    help="skip the box calibration (8192^3 bf16 GEMM TF/s, 4 GiB copy TB/s) after the timed steps")
     ap.add_argument("--full-model", default="llama3.1-8b", help=argparse.SUPPRESS)  # tests: tiny models
     ap.add_argument("--full-steps", type=int, default=10)
     ap.add_argument("--full-warmup", type=int, default=3)
@@ -179,32 +185,71 @@ def main(argv=None):
     env = runtime.init()
     out = run(a, env)
     cuda = env.device.type == "cuda"
+    if cuda and a.calibrate:
+        # box speed next to the number: fixed GEMM + copy after the timed steps
+        from mxllm.utils.calibrate import calibrate
+
+        _free_gpu_memory(env)
+        out["calibration"] = calibrate(env.device)
     headline = a.model == "llama3.1-70b" and a.finetune == "lora" and a.parallel == "ddp" and not a.layers
     c2 = a.config2 == "on" or (a.config2 == "auto" and env.world_size == 1 and headline and cuda)
     c3 = a.config3 == "on" or (a.config3 == "auto" and env.world_size == 8 and headline and cuda)
-    if (c2 and env.world_size == 1) or (c3 and env.world_size > 1):
-        key = "config2_8b_full" if env.world_size == 1 else f"config3_8b_full_dp{env.world_size}"
-        out[key] = run_full(a, env)
     c4 = a.config4 == "on" or (a.config4 == "auto" and env.world_size == 8 and headline and cuda)
-    if not c4:
+    if c2 and env.world_size == 1:
+        # single process: an exception (e.g. out of memory) is caught and recorded, nothing can strand
+        out["config2_8b_full"] = run_full(a, env)
+        if a.config2_mb4 == "on" or (a.config2_mb4 == "auto" and cuda):
+            # the reference's batch of 4 sequences per rank (/root/reference/src/distributed_inference.py:59)
+            out["config2_8b_full_mb4"] = run_full(a, env, micro_batch=4)
+    children = []
+    if c3 and env.world_size > 1:
+        children.append(("config3", f"config3_8b_full_dp{env.world_size}"))
+    if c4:
+        children.append(("config4", "config4_full_zero3"))
+    if not children:
         if env.is_main:
             emit(out, a.json_out)
         runtime.cleanup()
         return 0
-    # BASELINE config 4 in a fresh job: this job's ranks free the GPUs (non-zero
-    # ranks exit; the launcher waits for rank 0), local rank 0 runs the child.
-    # Every rank first reports the HBM it can hand over; too little -> skipped with the reason
+    # Multi-rank phases run as FRESH child jobs (an exception on one rank of an in-process
+    # DDP phase would strand the others in a collective): this job's ranks free their HBM, report the
+    # smallest free HBM and their PIDs, non-zero ranks exit, and local rank 0 confirms every other
+    # rank's process has exited (its HBM released) before it starts a child.
     _free_gpu_memory(env)
     free_gb = _min_free_gb(env)
+    import socket
+
+    pids = runtime.all_gather_objects((socket.gethostname(), os.getpid()))
     runtime.cleanup()
-    if env.is_main:
-        if free_gb is not None and free_gb < a.config4_need_gb:
-            out["config4_full_zero3"] = {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < "
-                                                    f"{a.config4_need_gb:.0f} GB the config-4 child needs"}
+    if not env.is_main:
+        return 0
+    host = socket.gethostname()
+    released = _wait_exited([p for h, p in pids if h == host and p != os.getpid()], timeout_s=120.0)
+    out["child_phases"] = {"headline_ranks_exited_s": released, "min_free_hbm_gb_before": (
+        round(free_gb, 1) if free_gb is not None else None)}
+    for kind, key in children:
+        if kind == "config4" and free_gb is not None and free_gb < a.config4_need_gb:
+            out[key] = {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < "
+                                   f"{a.config4_need_gb:.0f} GB the config-4 child needs"}
+        elif kind == "config4":
+            out[key] = run_config4(a, env.world_size)
         else:
-            out["config4_full_zero3"] = run_config4(a, env.world_size)
-        emit(out, a.json_out)
+            out[key] = run_config3(a, env.world_size)
+    emit(out, a.json_out)
     return 0
+
+
+def _wait_exited(pids: list[int], timeout_s: float) -> float | None:
+    """Seconds until every PID in ``pids`` has exited (same node), None on timeout."""
+    import psutil
+
+    t0 = time.time()
+    while time.time() - t0 < timeout_s:
+        alive = [p for p in pids if psutil.pid_exists(p) and psutil.Process(p).status() != psutil.STATUS_ZOMBIE]
+        if not alive:
+            return round(time.time() - t0, 2)
+        time.sleep(0.1)
+    return None
 
 
 def _free_gpu_memory(env):
@@ -227,7 +272,7 @@ def _min_free_gb(env) -> float | None:
     return runtime.all_reduce_scalars([free], op="min")[0]
 
 
-def run_full(a, env) -> dict:
+def run_full(a, env, micro_batch: int | None = None) -> dict:
     """BASELINE config 2 (1 GPU) / config 3 (N GPUs): Llama-3.1-8B FULL-parameter
     fine-tune with plain DDP, in this process after the headline (whose model and
     caches are released first).  Same timing contract as the headline.  A failure
@@ -240,6 +285,8 @@ def run_full(a, env) -> dict:
     b.steps, b.warmup, b.layers = a.full_steps, a.full_warmup, None
     b.act_ckpt, b.act_ckpt_layers, b.sp, b.cp, b.emulate_world = False, None, 1, 1, 0
     b.grad_accum = 1
+    if micro_batch is not None:
+        b.micro_batch = micro_batch
     try:
         res = run(b, env)
     except Exception as e:  # noqa: BLE001  (e.g. out of memory): report, keep the headline
@@ -249,7 +296,8 @@ def run_full(a, env) -> dict:
     cfg = b.model
     res["metric"] = f"fine-tune tokens/sec (whole node) {PRETTY.get(cfg, cfg)} FULL-parameter DDP"
     res["label"] = (f"BASELINE config {2 if env.world_size == 1 else 3}: {PRETTY.get(cfg, cfg)} full-parameter "
-                    f"fine-tune, DDP over {env.world_size} GPU(s), measured in-process after the headline")
+                    f"fine-tune, DDP over {env.world_size} GPU(s), micro-batch {b.micro_batch}, measured "
+                    f"in-process after the headline")
     return res
 
 
@@ -261,32 +309,28 @@ def emit(out: dict, json_out: str | None):
             f.write(line + "\n")
 
 
-def run_config4(a, world: int) -> dict:
-    """70B full-parameter ZeRO-3 fine-tune (activation checkpointing) on ``world``
-    GPUs as a child torchrun job; returns its parsed JSON (or the error)."""
+def _run_child(a, world: int, argv: list[str], timeout_s: float) -> dict:
+    """Run bench.py ``argv`` as a fresh ``world``-rank torchrun child job (rendezvous on
+    127.0.0.1) and return its parsed JSON line (or the error)."""
+    import contextlib
+    import io
     import tempfile
 
     if a.device != "cpu" and torch.cuda.device_count() < world:
         return {"skipped": f"this process sees {torch.cuda.device_count()} GPU(s), the child job needs {world}"}
-
-    fd, path = tempfile.mkstemp(suffix=".json", prefix="mxllm_c4_")
+    fd, path = tempfile.mkstemp(suffix=".json", prefix="mxllm_child_")
     os.close(fd)
-    argv = ["--gpus", str(world), "--model", a.config4_model, "--finetune", "full", "--parallel", "zero3",
-            "--act-ckpt", "--micro-batch", str(a.config4_micro_batch), "--seq-len", str(a.seq_len),
-            "--act-ckpt-layers", str(a.config4_act_ckpt_layers),
-            "--steps", str(a.config4_steps), "--warmup", str(a.config4_warmup), "--config4", "off",
-            "--json-out", path] + (["--device", a.device] if a.device else [])
+    argv = ["--gpus", str(world)] + argv + ["--config2", "off", "--config3", "off", "--config4", "off",
+                                            "--no-calibrate", "--json-out", path] + (
+        ["--device", a.device] if a.device else [])
     keep = {k: v for k, v in os.environ.items()
             if not (k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                           "ROLE_WORLD_SIZE", "ROLE_NAME", "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
                     or k.startswith("TORCHELASTIC_") or k.startswith("TORCH_ELASTIC"))}
     t0 = time.time()
-    import contextlib
-    import io
-
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):  # the child's own JSON line must not become a second output line
-        rc = launch_ranks(world, argv, timeout_s=a.config4_timeout, env=keep)
+        rc = launch_ranks(world, argv, timeout_s=timeout_s, env=keep)
     res = {"error": f"child job exit code {rc}", "wall_s": round(time.time() - t0, 1)}
     try:
         with open(path) as f:
@@ -300,6 +344,31 @@ def run_config4(a, world: int) -> dict:
         with contextlib.suppress(OSError):
             os.remove(path)
     res.pop("vs_baseline", None)
+    return res
+
+
+def run_config3(a, world: int) -> dict:
+    """BASELINE config 3: Llama-3.1-8B FULL fine-tune, plain DDP over ``world`` GPUs, as a
+    fresh child job after the headline."""
+    argv = ["--model", a.full_model, "--finetune", "full", "--parallel", "ddp", "--micro-batch",
+            str(a.micro_batch), "--seq-len", str(a.seq_len), "--steps", str(a.full_steps), "--warmup",
+            str(a.full_warmup)]
+    res = _run_child(a, world, argv, a.config3_timeout)
+    name = PRETTY.get(a.full_model, a.full_model)
+    res["metric"] = f"fine-tune tokens/sec (whole node) {name} FULL-parameter DDP"
+    res["label"] = (f"BASELINE config 3: {name} full-parameter fine-tune, DDP over {world} GPUs, "
+                    f"measured after the headline in a separate job")
+    return res
+
+
+def run_config4(a, world: int) -> dict:
+    """70B full-parameter ZeRO-3 fine-tune (activation checkpointing) on ``world``
+    GPUs as a child torchrun job; returns its parsed JSON (or the error)."""
+    argv = ["--model", a.config4_model, "--finetune", "full", "--parallel", "zero3",
+            "--act-ckpt", "--micro-batch", str(a.config4_micro_batch), "--seq-len", str(a.seq_len),
+            "--act-ckpt-layers", str(a.config4_act_ckpt_layers),
+            "--steps", str(a.config4_steps), "--warmup", str(a.config4_warmup)]
+    res = _run_child(a, world, argv, a.config4_timeout)
     name = PRETTY.get(a.config4_model, a.config4_model)
     res["label"] = (f"BASELINE config 4: {name} FULL-parameter fine-tune, ZeRO-3 sharded over "
                     f"{world} GPUs, activation checkpointing, measured after the headline in a separate job")

@@ -192,6 +192,36 @@ bool dw_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, double 
   return true;
 }
 
+// out[M, N] = beta * out + alpha * op(a) op(b) on the 8-phase MFMA GEMM (csrc/kernels/gemm8.hip).
+// a: [M, K] when a_kc (k-contiguous) else [K, M]; b: [N, K] when b_kc else [K, N]; all row-strided
+// bf16 views, out fp32 or bf16; alpha = alpha_f * (the optional f32 device scalar alpha_t).
+// Returns false (nothing launched) for shapes the kernel does not take.
+bool gemm8(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::Tensor& out, double beta,
+           const c10::optional<at::Tensor>& alpha_t, double alpha_f) {
+  MX_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm8: GPU tensors");
+  MX_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm8: bf16 operands");
+  MX_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "gemm8: fp32 / bf16 output");
+  MX_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm8: 2-D operands");
+  const int64_t M = a_kc ? a.size(0) : a.size(1), K = a_kc ? a.size(1) : a.size(0);
+  const int64_t N = b_kc ? b.size(0) : b.size(1), Kb = b_kc ? b.size(1) : b.size(0);
+  MX_CHECK(K == Kb && out.size(0) == M && out.size(1) == N, "gemm8: shape mismatch");
+  if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1) return false;
+  if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return false;
+  const float* sc = nullptr;
+  if (alpha_t.has_value()) {
+    MX_CHECK(alpha_t->scalar_type() == at::kFloat && alpha_t->numel() == 1 && alpha_t->device() == a.device(),
+             "gemm8 alpha_t: f32 scalar on the device");
+    sc = alpha_t->data_ptr<float>();
+  }
+  DevGuard g(a.device());
+  const int rc = mx_gemm8(bf(a), a.stride(0), a_kc ? 1 : 0, bf(b), b.stride(0), b_kc ? 1 : 0, out.data_ptr(),
+                          out.stride(0), out.scalar_type() == at::kFloat ? 1 : 0, (int)M, (int)N, (int)K, (float)beta,
+                          sc, (float)alpha_f, cur_stream());
+  if (rc == -1) return false;
+  MX_OK(rc);
+  return true;
+}
+
 // A HIP stream confined to a subset of the device's CUs (hipExtStreamCreateWithCUMask):
 // ``mask`` = one int per 32 CUs (bit i of word w = CU 32 w + i).  Returns the stream handle
 // for torch.cuda.ExternalStream; the stream lives for the process (never destroyed).
@@ -389,6 +419,33 @@ std::tuple<at::Tensor, at::Tensor> ce_fwd_bwd(at::Tensor logits, const at::Tenso
   MX_OK(mx_ce_fwd_bwd(bfm(logits), lab.data_ptr<int64_t>(), losses.data_ptr<float>(), ws.data_ptr<float>(),
                       loss.data_ptr<float>(), T, (int)V, ignore, cur_stream()));
   return {loss, losses};
+}
+
+// 1 / (number of labels != ignore) as a 1-element f32 device tensor (0 when none)
+at::Tensor ce_inv_count(const at::Tensor& labels, int64_t ignore) {
+  MX_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong, "labels must be int64 GPU");
+  DevGuard g(labels.device());
+  auto lab = labels.contiguous();
+  auto inv = at::empty({1}, labels.options().dtype(at::kFloat));
+  MX_OK(mx_ce_inv_count(lab.data_ptr<int64_t>(), lab.numel(), ignore, inv.data_ptr<float>(), cur_stream()));
+  return inv;
+}
+
+// one chunk of the chunked LM-head CE: per-row losses, logits <- (softmax - onehot) * inv_n in place
+at::Tensor ce_chunk(at::Tensor logits, const at::Tensor& labels, int64_t ignore, const at::Tensor& inv_n) {
+  check_bf16(logits, "logits");
+  MX_CHECK(logits.is_contiguous(), "ce_chunk: contiguous logits");
+  MX_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong, "labels must be int64 GPU");
+  MX_CHECK(inv_n.scalar_type() == at::kFloat && inv_n.numel() == 1 && inv_n.device() == logits.device(),
+           "ce_chunk: inv_n f32 device scalar");
+  DevGuard g(logits.device());
+  const int64_t V = logits.size(-1), T = logits.numel() / V;
+  MX_CHECK(labels.numel() == T, "labels size mismatch");
+  auto lab = labels.contiguous();
+  auto losses = at::empty({T}, logits.options().dtype(at::kFloat));
+  MX_OK(mx_ce_chunk(bfm(logits), lab.data_ptr<int64_t>(), losses.data_ptr<float>(), inv_n.data_ptr<float>(), T,
+                    (int)V, ignore, cur_stream()));
+  return losses;
 }
 
 // ---------------------------------------------------------------- RoPE split / merge
@@ -926,6 +983,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
   m.def("transpose2d(Tensor x, Tensor? scale=None) -> Tensor");
   m.def("dw_gemm(Tensor dy, Tensor x, Tensor(a!) out, float beta, Tensor? scale=None) -> bool");
+  m.def("gemm8(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, float beta, Tensor? alpha_t=None, float alpha=1.0) -> bool");
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
   m.def("sqnorm(Tensor x) -> Tensor");
@@ -938,6 +996,8 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("embedding_bwd(Tensor dy, Tensor ids, int V) -> Tensor");
   m.def("embedding_bwd_sorted(Tensor dy, Tensor sid, Tensor perm, Tensor(a!) out) -> ()");
   m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
+  m.def("ce_inv_count(Tensor labels, int ignore_index) -> Tensor");
+  m.def("ce_chunk(Tensor(a!) logits, Tensor labels, int ignore_index, Tensor inv_n) -> Tensor");
   m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
@@ -968,6 +1028,9 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("copy2d_batched", &copy2d_batched);
   m.impl("transpose2d", &transpose2d);
   m.impl("dw_gemm", &dw_gemm);
+  m.impl("gemm8", &gemm8);
+  m.impl("ce_inv_count", &ce_inv_count);
+  m.impl("ce_chunk", &ce_chunk);
   m.impl("prefetch", &prefetch);
   m.impl("sqnorm", &sqnorm);
   m.impl("swiglu_fwd", &swiglu_fwd);

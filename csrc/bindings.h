@@ -28,6 +28,12 @@ extern "C" {
 int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream);
 int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
                   hipStream_t stream);
+int mx_ce_inv_count(const int64_t* labels, int64_t T, int64_t ignore, float* inv_n, hipStream_t stream);
+int mx_ce_chunk(uint16_t* logits, const int64_t* labels, float* losses, const float* inv_n, int64_t T, int V,
+                int64_t ignore, hipStream_t stream);
+int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc, void* C,
+             int64_t ldc, int out_f32, int M, int N, int K, float beta, const float* alpha_t, float alpha_f,
+             hipStream_t stream);
 int mx_dw_gemm(const uint16_t* dy, int64_t lda, const uint16_t* x, int64_t ldb, void* out, int64_t ldc, int out_f32,
                int M, int N, int T, float beta, const float* alpha_t, float alpha_f, hipStream_t stream);
 int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int16_t* lo, int64_t n,

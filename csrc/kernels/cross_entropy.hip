@@ -112,3 +112,18 @@ extern "C" int mx_ce_fwd_bwd(uint16_t* logits, const int64_t* labels, float* los
   ce_reduce_kernel<<<1, 256, 0, stream>>>(losses, T, inv_n, loss_out);
   return (int)hipGetLastError();
 }
+
+// Chunked LM head + CE (mxllm/ops/loss.py): the valid-token count over ALL chunks first, then one
+// fwd+bwd launch per chunk of rows against that global 1 / n_valid.
+extern "C" int mx_ce_inv_count(const int64_t* labels, int64_t T, int64_t ignore, float* inv_n, hipStream_t stream) {
+  if (T <= 0) return 0;
+  count_valid_kernel<<<1, 256, 0, stream>>>(labels, T, ignore, inv_n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mx_ce_chunk(uint16_t* logits, const int64_t* labels, float* losses, const float* inv_n, int64_t T,
+                           int V, int64_t ignore, hipStream_t stream) {
+  if (V % 8 || T <= 0) return T <= 0 ? 0 : -1;
+  ce_fwd_bwd_kernel<<<(unsigned)T, 256, 0, stream>>>(logits, labels, losses, inv_n, V, ignore);
+  return (int)hipGetLastError();
+}

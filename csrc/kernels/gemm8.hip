@@ -1,0 +1,404 @@
+// 8-phase bf16 GEMM for gfx950 (VERDICT r3 "next round" item 1).
+//
+//   C[M, N] = alpha * op(A) op(B) (+ C when BETA),  fp32 accumulation, C fp32 or bf16,
+//
+// with each operand in either storage order, so the three GEMM forms of a Llama training step
+// run without a transpose pass:
+//   forward  y  = x W^T  : A = x  [T][in]  (k-contiguous), B = W [out][in] (k-contiguous)
+//   input gr dX = dY W   : A = dY [T][out] (k-contiguous), B = W [out][in] = [k][n] (n-contiguous)
+//   weight gr dW = dY^T X: A = dY [T][out] = [k][m] (m-contiguous), B = X [T][in] = [k][n]
+// ("NN"-form dX ran at ~1.32 PF in hipBLASLt; token-major dW needed 6.8 / 73 ms of transposes
+// per 8B / 70B-ZeRO-3 step, profiles/r3o, r3p, r3d).
+//
+// Structure (CDNA guide §5 "The 256² 8-phase template", T1-T5, T10), designed here for the two
+// operand orders:
+//  * workgroup 512 threads = 8 waves as 2 (M) x 4 (N), output tile 256 x 256, each wave 128 x 64 =
+//    8 x 4 blocks of v_mfma_f32_16x16x32_bf16 (16x16x32 rather than 32x32x16: the chip holds a
+//    ~12-15 % higher clock on it on random data, MI355X_MICROARCH "DVFS give-back" item 7);
+//  * the MFMA is issued with the operands swapped (B fragment as the A operand), so each lane's
+//    4 accumulator registers are 4 CONSECUTIVE output columns of one row: 8-B (bf16) / 16-B (fp32)
+//    epilogue stores instead of 2-B / 4-B ones;
+//  * a K-tile (BK 64) is four 16-KiB half-tile images, A0 | A1 | B0 | B1, where A0 holds the rows
+//    of output quadrant a = 0 of BOTH wave rows (and B0 the columns of quadrant b = 0 of all four
+//    wave columns), so each image is read in exactly one phase;
+//  * every image is filled by LDS-DMA (buffer_load ... lds, 16 B per lane, 2 per wave) into a
+//    lane-linear layout; the XOR swizzle that makes the MFMA-operand reads bank-conflict free is
+//    applied by permuting each lane's SOURCE address (guide rule 21):
+//      - k-contiguous operand: [128 rows][64 k] (128-B rows), 16-B chunk c stored at c ^ ((r>>1)&7),
+//        read with ds_read_b128 (lane: row l&15, k chunk l>>4);
+//      - mn-contiguous operand: [64 k][128 cols] (256-B rows), chunk c stored at c ^ 2 t(k),
+//        t(k) = (k&3) | ((k>>3)&1)<<2, read with two ds_read_b64_tr_b16 per 32-k step (T10);
+//  * 8 phases per two K-tiles; phase p: {this phase's LDS reads, one half-tile prefetch,
+//    s_barrier, lgkmcnt(0), 16 MFMAs (one 64x32 quadrant x K 64), s_barrier}; the two wave rows run
+//    one barrier apart (ping-pong: one issues MFMAs while the other reads LDS); counted
+//    vmcnt(6) (three half-tiles in flight across barriers) only in phases 4 and 8, raw s_barrier
+//    (never __syncthreads: its fence would drain the DMA), all LDS in one __shared__ array, LDS
+//    reads as inline asm (hipcc's waitcnt pass cannot see that they miss the in-flight DMA);
+//  * read/restage order (why the schedule is race free): phase 1 reads B0 then A0 of the even
+//    buffer and retires the B0 reads (counted lgkmcnt) before its first barrier, phase 2 B1,
+//    phase 3 A1, phase 4 nothing; the next tile's images are restaged B0 @2, A0 @3, B1 @4, A1 @5,
+//    i.e. >= 2 phases after an image's last read (1 for the early-retired B0), and read >= one
+//    phase after the vmcnt that retires them (guide §5 "Read a staged buffer one phase AFTER the
+//    wait", with the extra barrier of the staggered wave rows);
+//  * workgroup -> tile: XCD-contiguous ranges (T1, bijective) of a grouped order (8 m-tiles x all
+//    n-tiles) so one XCD's co-resident tiles share their A / B panels in its L2.
+// Range-checked buffer descriptors read rows past K (mn-contiguous operands) as zeros, so the
+// weight-gradient form takes any token count; M and N must be multiples of 256.
+#include <cstdio>
+#include <cstdlib>
+
+#include "common.h"
+
+namespace mx {
+
+typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* g8lptr_t;
+
+__device__ __forceinline__ f32x4 g8_mfma(const u16x8& a, const u16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_g, a), __builtin_bit_cast(bf16x8_g, b), c,
+                                                 0, 0, 0);
+}
+
+constexpr int G8_HT = 16384;        // one half-tile image: 128 rows (cols) x 64 k x bf16
+constexpr int G8_TILE = 4 * G8_HT;  // A0 | A1 | B0 | B1
+constexpr int G8_BK = 64;
+
+// image row r' (k-contiguous) / image column (mn-contiguous) -> row / column of the 256 tile
+__device__ __forceinline__ int g8_map_a(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
+__device__ __forceinline__ int g8_map_b(int r, int h) { return (r >> 5) * 64 + h * 32 + (r & 31); }
+__device__ __forceinline__ int g8_t(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// per-lane byte offsets of this wave's two LDS-DMA pieces of half-tile image h of one operand
+template <bool KC, bool IS_A>
+__device__ __forceinline__ void g8_src_offsets(int w, int lane, int64_t ld, int h, uint32_t (&off)[2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pc = 2 * w + j;
+    if constexpr (KC) {
+      const int r = 8 * pc + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int row = IS_A ? g8_map_a(r, h) : g8_map_b(r, h);
+      off[j] = (uint32_t)(((int64_t)row * ld + 8 * c) * 2);
+    } else {
+      const int k = 4 * pc + (lane >> 4);
+      const int c = (lane & 15) ^ (2 * g8_t(k));
+      const int col = IS_A ? g8_map_a(8 * c, h) : g8_map_b(8 * c, h);
+      off[j] = (uint32_t)(((int64_t)k * ld + col) * 2);
+    }
+  }
+}
+
+// lane part of the LDS address of an MFMA-operand read
+//  KC: block rows rb.. (rb % 16 == 0, folded into the immediate), k-step s
+__device__ __forceinline__ uint32_t g8_kc_lane(int lane, int s) {
+  const int i = lane & 15, g = lane >> 4;
+  return (uint32_t)(i * 128 + 16 * ((4 * s + g) ^ ((i >> 1) & 7)));
+}
+//  MN: block columns cb..cb+15 (one base per cb; k-step s and read r are +8192 s + 1024 r)
+__device__ __forceinline__ uint32_t g8_mn_lane(int lane, int cb) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int t = q | ((g & 1) << 2);
+  return (uint32_t)((8 * g + q) * 256 + 16 * (((cb >> 3) ^ (2 * t)) + (p >> 1)) + 8 * (p & 1));
+}
+
+template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA>
+__global__ void __launch_bounds__(512, 1)
+gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+             void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
+             float alpha_f) {
+  // ONE __shared__ array (a second LDS object makes hipcc drain vmcnt before LDS reads: guide §5 item 4a)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * G8_TILE];
+  const int nM = M >> 8, nN = N >> 8;
+  int pm, pn;
+  {
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    constexpr int GM = 8;
+    const int per = GM * nN, grp = L / per, first = grp * GM;
+    const int rows = min(GM, nM - first), in = L - grp * per;
+    pm = first + in % rows;
+    pn = in / rows;
+  }
+  const int m0 = pm << 8, n0 = pn << 8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int nk = (K + G8_BK - 1) / G8_BK;
+
+  // ---- operand descriptors (range-checked: mn-contiguous rows past K read as zeros)
+  const uint16_t* abase = A_KC ? A + (int64_t)m0 * lda : A + m0;
+  const uint16_t* bbase = B_KC ? B + (int64_t)n0 * ldb : B + n0;
+  const uint32_t arec = A_KC ? (uint32_t)((255 * lda + (int64_t)nk * G8_BK) * 2) : (uint32_t)(((int64_t)K * lda - m0) * 2);
+  const uint32_t brec = B_KC ? (uint32_t)((255 * ldb + (int64_t)nk * G8_BK) * 2) : (uint32_t)(((int64_t)K * ldb - n0) * 2);
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)abase, 0, arec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, 0, brec, 0x00020000);
+  const uint32_t astep = A_KC ? G8_BK * 2 : (uint32_t)(G8_BK * lda * 2);  // bytes per K-tile
+  const uint32_t bstep = B_KC ? G8_BK * 2 : (uint32_t)(G8_BK * ldb * 2);
+  uint32_t aoff[2][2], boff[2][2];
+  g8_src_offsets<A_KC, true>(w, lane, lda, 0, aoff[0]);
+  g8_src_offsets<A_KC, true>(w, lane, lda, 1, aoff[1]);
+  g8_src_offsets<B_KC, false>(w, lane, ldb, 0, boff[0]);
+  g8_src_offsets<B_KC, false>(w, lane, ldb, 1, boff[1]);
+
+  // issue half-tile image `img` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile kt into buffer kt & 1
+  auto issue = [&](int kt, int img) __attribute__((always_inline)) {
+    char* dst = smem + (kt & 1) * G8_TILE + img * G8_HT + (2 * w) * 1024;
+    // the K-tile offset rides in voffset: the range check covers voffset + immediate only
+    if (img < 2) {
+      const uint32_t so = (uint32_t)kt * astep;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (g8lptr_t)dst, 16, aoff[img][0] + so, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (g8lptr_t)(dst + 1024), 16, aoff[img][1] + so, 0, 0, 0);
+    } else {
+      const uint32_t so = (uint32_t)kt * bstep;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (g8lptr_t)dst, 16, boff[img - 2][0] + so, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (g8lptr_t)(dst + 1024), 16, boff[img - 2][1] + so, 0, 0, 0);
+    }
+  };
+
+  // ---- LDS read bases (lane parts; + buffer / image offsets at the read)
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t akc[2], amn[4], bmn[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) akc[s] = g8_kc_lane(lane, s);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) amn[i] = g8_mn_lane(lane, wr * 64 + 16 * i);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bmn[j] = g8_mn_lane(lane, wc * 32 + 16 * j);
+
+  u16x8 fa[4][2], fb0[2][2], fb1[2][2];  // [block][k-step]
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A image `img` (0/1) of buffer `buf` -> fa;  KC: ds_read_b128, MN: 2 x ds_read_b64_tr_b16 per block and k-step
+  auto read_a = [&](int buf, int img) __attribute__((always_inline)) {
+    const uint32_t ib = lds0 + buf * G8_TILE + img * G8_HT;
+    if constexpr (A_KC) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t b = ib + akc[s];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i][s] = rd128_off(b, (wr * 64 + 16 * i) * 128);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t b = ib + amn[i];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u16x4 lo = trd_off(b, 8192 * s), hi = trd_off(b, 8192 * s + 1024);
+          fa[i][s] = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+    }
+  };
+  auto read_b = [&](int buf, int img, u16x8(&fb)[2][2]) __attribute__((always_inline)) {
+    const uint32_t ib = lds0 + buf * G8_TILE + (2 + img) * G8_HT;
+    if constexpr (B_KC) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t b = ib + akc[s];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j][s] = rd128_off(b, (wc * 32 + 16 * j) * 128);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t b = ib + bmn[j];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u16x4 lo = trd_off(b, 8192 * s), hi = trd_off(b, 8192 * s + 1024);
+          fb[j][s] = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+    }
+  };
+  auto pin_a = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pin(fa[i][0]);
+      pin(fa[i][1]);
+    }
+  };
+  auto pin_b = [&](u16x8(&fb)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      pin(fb[j][0]);
+      pin(fb[j][1]);
+    }
+  };
+  // quadrant (a, b): 16 MFMAs; swapped operands -> acc holds C^T blocks (4 consecutive columns per lane)
+  auto mma = [&](int qa, int qb, u16x8(&fb)[2][2]) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 * qa + i][2 * qb + j] = g8_mfma(fb[j][s], fa[i][s], acc[4 * qa + i][2 * qb + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  constexpr int NA = A_KC ? 8 : 16;  // LDS reads of one A image
+  auto vm6 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); };
+  auto vm0 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  // ---- prologue: K-tile 0 (all four images) + K-tile 1's B0, A0, B1; retire tile 0
+  issue(0, 2);
+  issue(0, 0);
+  issue(0, 3);
+  issue(0, 1);
+  if (nk > 1) {
+    issue(1, 2);
+    issue(1, 0);
+    issue(1, 3);
+    vm6();
+  } else {
+    vm0();
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+
+  // one phase: reads -> prefetch -> [wait] -> barrier -> lgkmcnt(0) -> MFMA -> barrier
+#define G8_SYNC_MMA(QA, QB, FB) \
+  __builtin_amdgcn_s_barrier(); \
+  lds_wait();                   \
+  pin_a();                      \
+  pin_b(FB);                    \
+  mma(QA, QB, FB);              \
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0;; kt += 2) {
+    // phases 1-4: tile kt in buffer 0
+    read_b(0, 0, fb0);
+    read_a(0, 0);
+    if (kt + 1 < nk) issue(kt + 1, 1);
+    lds_wait_le(NA < 15 ? NA : 15);  // B0 reads retired before the barrier: B0 restageable in phase 2
+    G8_SYNC_MMA(0, 0, fb0)
+    read_b(0, 1, fb1);
+    if (kt + 2 < nk) issue(kt + 2, 2);
+    G8_SYNC_MMA(0, 1, fb1)
+    read_a(0, 1);
+    if (kt + 2 < nk) issue(kt + 2, 0);
+    G8_SYNC_MMA(1, 1, fb1)
+    if (kt + 2 < nk) {
+      issue(kt + 2, 3);
+      vm6();
+    } else {
+      vm0();
+    }
+    G8_SYNC_MMA(1, 0, fb0)
+    if (kt + 1 >= nk) break;
+    // phases 5-8: tile kt + 1 in buffer 1
+    read_b(1, 0, fb0);
+    read_a(1, 0);
+    if (kt + 2 < nk) issue(kt + 2, 1);
+    lds_wait_le(NA < 15 ? NA : 15);
+    G8_SYNC_MMA(0, 0, fb0)
+    read_b(1, 1, fb1);
+    if (kt + 3 < nk) issue(kt + 3, 2);
+    G8_SYNC_MMA(0, 1, fb1)
+    read_a(1, 1);
+    if (kt + 3 < nk) issue(kt + 3, 0);
+    G8_SYNC_MMA(1, 1, fb1)
+    if (kt + 3 < nk) {
+      issue(kt + 3, 3);
+      vm6();
+    } else {
+      vm0();
+    }
+    G8_SYNC_MMA(1, 0, fb0)
+    if (kt + 2 >= nk) break;
+  }
+#undef G8_SYNC_MMA
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the stagger barrier
+
+  // ---- epilogue: lane holds C[m][n .. n+3] per block
+  const float alpha = alpha_f * (alpha_t ? alpha_t[0] : 1.f);
+  const int ml = m0 + wr * 128 + (lane & 15);
+  const int nl = n0 + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa) {
+    f32x4 old[4][4];
+    if constexpr (BETA) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t m = ml + qa * 64 + 16 * i;
+          const int n = nl + 32 * (j >> 1) + 16 * (j & 1);
+          if constexpr (OUT_F32) {
+            old[i][j] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(C) + m * ldc + n);
+          } else {
+            const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(C) + m * ldc + n);
+            old[i][j] = f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                              __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+          }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t m = ml + qa * 64 + 16 * i;
+        const int n = nl + 32 * (j >> 1) + 16 * (j & 1);
+        f32x4 v = acc[4 * qa + i][j] * alpha;
+        if constexpr (BETA) v += old[i][j];
+        if constexpr (OUT_F32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + m * ldc + n) = v;
+        } else {
+          uint2 o;
+          o.x = pack_bf16x2(v[0], v[1]);
+          o.y = pack_bf16x2(v[2], v[3]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + m * ldc + n) = o;
+        }
+      }
+  }
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+// C[M, N] = alpha * op(A) op(B) + beta * C.  a_kc: A stored [M][K] (else [K][M]); b_kc: B stored [N][K]
+// (else [K][N]); row strides in elements.  Takes M, N multiples of 256; K a multiple of 64 when an
+// operand is k-contiguous (any K otherwise: rows past K read as zeros); 16-B aligned rows; beta 0 or 1;
+// every operand's addressed span < 2 GiB.  Returns -1 (nothing launched) for shapes it does not take.
+extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc, void* C,
+                        int64_t ldc, int out_f32, int M, int N, int K, float beta, const float* alpha_t, float alpha_f,
+                        hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (M & 255) || (N & 255)) return -1;
+  if ((a_kc || b_kc) && (K % G8_BK)) return -1;
+  if (lda % 8 || ldb % 8 || ldc % 4 || ((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)C & 15)) return -1;
+  if (a_kc ? lda < K : lda < M) return -1;
+  if (b_kc ? ldb < K : ldb < N) return -1;
+  if (ldc < N || (!out_f32 && ldc % 4)) return -1;
+  if (beta != 0.f && beta != 1.f) return -1;
+  const int64_t kpad = (int64_t)((K + G8_BK - 1) / G8_BK) * G8_BK;
+  const int64_t aspan = a_kc ? 256 * lda : kpad * lda;
+  const int64_t bspan = b_kc ? 256 * ldb : kpad * ldb;
+  if (aspan * 2 >= ((int64_t)1 << 31) || bspan * 2 >= ((int64_t)1 << 31)) return -1;
+  const int grid = (M >> 8) * (N >> 8);
+  const bool acc = beta != 0.f;
+#define G8_L(AK, BK_, F, BT) \
+  gemm8_kernel<AK, BK_, F, BT><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f)
+#define G8_OUT(AK, BK_)                                        \
+  do {                                                         \
+    if (out_f32) {                                             \
+      if (acc) G8_L(AK, BK_, true, true); else G8_L(AK, BK_, true, false);   \
+    } else {                                                   \
+      if (acc) G8_L(AK, BK_, false, true); else G8_L(AK, BK_, false, false); \
+    }                                                          \
+  } while (0)
+  if (a_kc && b_kc)
+    G8_OUT(true, true);
+  else if (a_kc)
+    G8_OUT(true, false);
+  else if (b_kc)
+    G8_OUT(false, true);
+  else
+    G8_OUT(false, false);
+#undef G8_OUT
+#undef G8_L
+  return (int)hipGetLastError();
+}

@@ -44,7 +44,11 @@ class RunConfig:
     # prompts are generated together by continuous batching; results are still
     # logged batch by batch, in order).  0 = one batch at a time, as the reference.
     lookahead_batches: int = 8
-    max_seq: int = 2048
+    # engine context window: long enough for whole IMDB-like reviews (~8k byte tokens at the tail of
+    # the synthetic length distribution); the KV cache is a paged pool sized by kv_pool_tokens, so
+    # the window costs nothing until a long prompt uses it (prompts were truncated at 2k)
+    max_seq: int = 16384
+    kv_pool_tokens: int = 0  # 0 = max_batch x 4096 tokens (or max_seq, whichever is larger)
     tokenizer: str = ""
     checkpoint: str = ""
     request_timeout: float = 120.0

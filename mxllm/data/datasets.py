@@ -84,9 +84,10 @@ def load_text_dataset(name: str = "imdb", split: str = "train[:1%]", n_rows: int
 class SyntheticTokens:
     """Random-token LM batches of a fixed shape, generated on the device.
 
-    labels are the next-token targets of the same stream (shift by one), the
-    last position is ignored (-100).  Seeded per rank so DDP ranks see
-    different data, reproducible across restarts via ``state``.
+    Each row is drawn as seq_len + 1 tokens: ids are the first seq_len, labels
+    the next-token targets (the same stream shifted by one), so every position,
+    the last included, has a real target (no -100).  Seeded per rank so DDP
+    ranks see different data, reproducible across restarts via ``state``.
     """
 
     def __init__(self, vocab: int, batch: int, seq_len: int, device, seed: int = 0, rank: int = 0):

@@ -1,4 +1,4 @@
-"""Fused LM-head + cross-entropy.
+"""Fused LM-head + cross-entropy, chunked over T for long sequences.
 
 MI355X-first sizing: at 4k tokens x 128,256 vocab the bf16 logits are 1 GB —
 cheap against 288 GB of HBM — so the head runs as ONE large hipBLASLt GEMM
@@ -8,15 +8,27 @@ log-sum-exp and overwrites the row IN PLACE with d(loss)/d(logits)
 (softmax - onehot) / n_valid in bf16.  The backward is a single
 ``dlogits @ W`` GEMM (plus ``dlogits^T @ h`` when the head is trainable).
 ``ignore_index`` rows get zero gradient and do not count in the mean.
+
+Long sequences ("chunk over T to avoid materializing"): when the
+[T, V] logits would exceed ``MXLLM_CE_CHUNK_GB`` (default 2 GiB: T > 8k tokens
+at V = 128,256), the forward walks T in chunks of ``MXLLM_CE_CHUNK_TOKENS``
+(default 4096 = 1 GB of bf16 logits) through ONE reused logits buffer: per
+chunk the head GEMM, the CE kernel against the GLOBAL valid-token count, and
+immediately the chunk's dh rows (dlogits @ W) and its dW contribution (dlogits^T
+h into an fp32 accumulator, on the weight-gradient GEMM) — nothing [T, V]-sized
+is kept.  The backward only scales dh / dW by the upstream gradient.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import reference as ref
 from ._ext import native, use_native
-from .linear import param_weight_grad
+from ..parallel.grad_ready import direct_grad, direct_grad32, mark_ready
+from .linear import param_weight_grad, weight_grad_
 
 
 class _LinearCEFn(torch.autograd.Function):
@@ -45,9 +57,93 @@ class _LinearCEFn(torch.autograd.Function):
         return dh, dw, None, None
 
 
+def _ce_chunk_torch(logits: torch.Tensor, labels: torch.Tensor, inv_n: torch.Tensor, ignore: int) -> torch.Tensor:
+    """CPU / reference form of the ce_chunk kernel: per-row losses; ``logits`` <- dlogits * inv_n."""
+    lf = logits.float()
+    valid = labels != ignore
+    lse = torch.logsumexp(lf, dim=-1)
+    tgt = lf.gather(1, labels.clamp(min=0).unsqueeze(1)).squeeze(1)
+    losses = torch.where(valid, lse - tgt, torch.zeros_like(lse))
+    g = torch.softmax(lf, dim=-1)
+    g[torch.arange(g.shape[0]), labels.clamp(min=0)] -= 1.0
+    g = g * valid.unsqueeze(1).to(g.dtype) * inv_n
+    logits.copy_(g.to(logits.dtype))
+    return losses
+
+
+def ce_chunk_tokens(T: int, V: int, elem: int = 2) -> int:
+    """Tokens per LM-head chunk for T tokens (T itself = no chunking)."""
+    limit = float(os.environ.get("MXLLM_CE_CHUNK_GB", "2")) * 2 ** 30
+    if T * V * elem <= limit:
+        return T
+    return max(1, min(T, int(os.environ.get("MXLLM_CE_CHUNK_TOKENS", "4096"))))
+
+
+class _ChunkedLinearCEFn(torch.autograd.Function):
+    """Mean CE of h @ w^T, T walked in chunks (module doc); dh / dW formed in the forward."""
+
+    @staticmethod
+    def forward(ctx, h, w, labels, ignore_index, chunk):
+        T, V = h.shape[0], w.shape[0]
+        nat = use_native(h)
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if nat:
+            inv_n = native().ce_inv_count(labels, ignore_index)
+        else:
+            inv_n = (1.0 / (labels != ignore_index).sum().clamp(min=1).float()).reshape(1)
+        losses = torch.empty(T, dtype=torch.float32, device=h.device)
+        dh = torch.empty_like(h) if need_h else None
+        dwacc = torch.empty(V, h.shape[1], dtype=torch.float32, device=h.device) if need_w else None
+        buf = torch.empty(min(chunk, T), V, dtype=h.dtype, device=h.device)
+        for i, t0 in enumerate(range(0, T, chunk)):
+            t1 = min(T, t0 + chunk)
+            hc, lab = h[t0:t1], labels[t0:t1]
+            lg = buf[: t1 - t0]
+            torch.matmul(hc, w.t(), out=lg)
+            losses[t0:t1] = (native().ce_chunk(lg, lab, ignore_index, inv_n) if nat
+                             else _ce_chunk_torch(lg, lab, inv_n, ignore_index))
+            if need_h:
+                torch.matmul(lg, w, out=dh[t0:t1])
+            if need_w:
+                weight_grad_(dwacc, lg, hc, beta=0.0 if i == 0 else 1.0)
+        loss = losses.sum() * inv_n[0]
+        ctx.save_for_backward(dh, dwacc)
+        ctx.wp = w if w.is_leaf else None
+        ctx.wdtype = w.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        dh, dwacc = ctx.saved_tensors
+        gdh = gdw = None
+        if ctx.needs_input_grad[0]:
+            gdh = dh * gl.to(dh.dtype)
+        if ctx.needs_input_grad[1]:
+            dwacc.mul_(gl)
+            wp = ctx.wp
+            g = direct_grad(wp) if wp is not None else None
+            if g is None and wp is not None:
+                g = direct_grad32(wp)
+            if g is None:
+                gdw = dwacc.to(ctx.wdtype)
+            else:
+                if getattr(wp, "_mx_grad_fresh", False):
+                    g.copy_(dwacc)
+                    wp._mx_grad_fresh = False
+                else:
+                    g.add_(dwacc)
+                mark_ready(wp)
+        return gdh, gdw, None, None, None
+
+
 def linear_cross_entropy(h: torch.Tensor, w: torch.Tensor, labels: torch.Tensor,
-                         ignore_index: int = -100) -> torch.Tensor:
-    """mean CE of ``h @ w.T`` against ``labels`` (h [T,H], w [V,H], labels [T] int64)."""
+                         ignore_index: int = -100, chunk: int | None = None) -> torch.Tensor:
+    """mean CE of ``h @ w.T`` against ``labels`` (h [T,H], w [V,H], labels [T] int64).
+    ``chunk``: tokens per LM-head chunk (default: :func:`ce_chunk_tokens`; T = one piece)."""
+    T, V = h.shape[0], w.shape[0]
+    c = ce_chunk_tokens(T, V) if chunk is None else chunk
+    if c < T:
+        return _ChunkedLinearCEFn.apply(h.contiguous(), w, labels.contiguous(), ignore_index, c)
     if use_native(h):
         return _LinearCEFn.apply(h.contiguous(), w, labels.contiguous(), ignore_index)
     return ref.cross_entropy(F.linear(h, w), labels, ignore_index)

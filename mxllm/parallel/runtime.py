@@ -188,3 +188,12 @@ def all_reduce_small_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         return _SMALL.all_reduce_(t, op)
     dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
     return t
+
+
+def all_gather_objects(obj) -> list:
+    """Gather one picklable object per rank (rank order); ``[obj]`` without a process group."""
+    if not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out

@@ -25,8 +25,13 @@ def preset_for(model_name: str, device: torch.device) -> str:
     return "tiny"
 
 
-def ensure_local_engine(model_name: str, device, engine_model: str = "", max_batch: int = 8, max_seq: int = 2048,
-                        tokenizer_path: str = "", checkpoint: str = "", seed: int = 0, weights: str = "bf16"):
+def ensure_local_engine(model_name: str, device, engine_model: str = "", max_batch: int = 8, max_seq: int = 16384,
+                        tokenizer_path: str = "", checkpoint: str = "", seed: int = 0, weights: str = "bf16",
+                        kv_pool_tokens: int = 0):
+    """Build (once per model name) and register the local engine.  The KV cache is a paged
+    pool of ``kv_pool_tokens`` (0: max(max_batch x 4096, max_seq)) shared by every slot, so a
+    long context window costs HBM only when a long prompt is admitted; prompts are cut to
+    ``max_seq - 64`` tokens (left-truncation) only beyond the window."""
     from ..data.tokenizer import get_tokenizer
     from ..models import build_model, tokenizer_path_for
 
@@ -49,7 +54,9 @@ def ensure_local_engine(model_name: str, device, engine_model: str = "", max_bat
 
         quantize_model_fp8_(model)
     tok = get_tokenizer(cfg.vocab_size, tokenizer_path or None, cfg.bos_id, cfg.eos_id)
-    eng = Engine(model, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id,))
+    max_seq = min(max_seq, cfg.max_seq_len)
+    pool = kv_pool_tokens or max(max_batch * 4096, max_seq)
+    eng = Engine(model, max_batch=max_batch, max_seq=max_seq, eos_ids=(cfg.eos_id,), kv_pool_tokens=pool)
     client.register_local(model_name, eng, _Truncating(tok, max_seq - 64))
     return client._LOCAL[model_name]
 

@@ -196,6 +196,7 @@ def load(ckpt_dir: str, trainer, step: int | None = None) -> dict | None:
     elif kind == "zero1":
         if man["world_size"] != world:
             raise RuntimeError(f"ZeRO-1 checkpoint written with world {man['world_size']}, resuming with {world}")
+        _require_same_layout(man.get("layout"), trainer.flat.state_dict(), "ZeRO-1")
         sd = {k: v.to(trainer._master.device) for k, v in load_file(os.path.join(d, f"rank_{rank}.safetensors")).items()}
         sd["step"] = man["step"]
         trainer.load_state_dict(sd)
@@ -214,10 +215,27 @@ def load(ckpt_dir: str, trainer, step: int | None = None) -> dict | None:
     return man.get("extra", {})
 
 
+def _norm_slots(layout: dict | None):
+    """Slot table as a list of lists (the manifest's JSON lists and the live tuples compare equal)."""
+    return None if not layout else [list(x) for x in layout.get("slots", [])]
+
+
+def _require_same_layout(old: dict | None, new: dict, what: str) -> None:
+    """Sharded optimizer state is a raw copy of flat ranges: it is only valid into the SAME flat
+    layout (the round-3 bucket order moved slots, so an older sharded file would have
+    landed on the wrong parameters without an error)."""
+    if not old:
+        raise RuntimeError(f"{what} checkpoint has no layout record; cannot verify the flat layout")
+    if _norm_slots(old) != _norm_slots(new) or old.get("numel") != new.get("numel"):
+        raise RuntimeError(f"{what} checkpoint was written with a different flat-buffer layout (parameter order / "
+                           "bucketing changed); resume it with the trainer version that wrote it, or re-save it "
+                           "unsharded (DDP) so it can be remapped by parameter name")
+
+
 def _remap_segments(old: dict | None, new: dict) -> list:
     """(old_lo, old_hi, new_lo) flat ranges moving every slot, by name, from the
     checkpoint's layout to the current one (identity when they agree)."""
-    if not old or old.get("slots") == new.get("slots"):
+    if not old or _norm_slots(old) == _norm_slots(new):
         return [(0, new["numel"], 0)]
     where = {name: (off, n) for name, off, n, _ in old["slots"]}
     segs = []
@@ -233,6 +251,8 @@ def _load_v1(d, man, trainer, rank, world):
     src = rank if man.get("sharded") else 0
     if man.get("sharded") and man.get("world_size") != world:
         raise RuntimeError(f"sharded checkpoint written with world {man['world_size']}, resuming with {world}")
+    if man.get("sharded") and hasattr(trainer, "flat"):
+        _require_same_layout(man.get("layout"), trainer.flat.state_dict(), "sharded (v1)")
     tensors = load_file(os.path.join(d, f"rank_{src}.safetensors"))
     dev = trainer.flat.master.device if hasattr(trainer, "flat") else trainer.master.device
     if hasattr(trainer, "flat") and not man.get("sharded") and man.get("layout"):

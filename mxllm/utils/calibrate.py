@@ -1,0 +1,71 @@
+"""Box-speed calibration for benchmark records.
+
+Two boxes of the pool run the same code up to a few percent apart (clock under
+power limit, HBM); a bench number is only comparable across rounds next to a
+measurement of the box itself.  ``calibrate(device)`` times two fixed
+workloads right after a benchmark's timed steps, on the same GPU:
+
+* ``gemm_8192_bf16_tflops``: C = A @ B, 8192^3, bf16 in / bf16 out, uniform
+  random [-1, 1) operands (random data: zero-filled operands read high), via
+  ``torch.matmul`` (hipBLASLt), median of 10 timed calls after 5 warm-up calls;
+* ``copy_4gb_tbps``: a 4 GiB device-to-device ``copy_`` counted as read +
+  write bytes (8 GiB moved per call), median of 6 calls.
+
+Plus the clock / power sample taken right after the GEMM loop.  Nothing here
+changes any GPU setting.
+"""
+from __future__ import annotations
+
+import statistics
+
+import torch
+
+
+def _time_ms(fn, reps: int, warm: int) -> float:
+    for _ in range(warm):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for s, e in ev:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    return statistics.median(s.elapsed_time(e) for s, e in ev)
+
+
+def calibrate(device: torch.device, copy_gib: float = 4.0) -> dict:
+    out: dict = {}
+    if device.type != "cuda":
+        return out
+    with torch.cuda.device(device):
+        try:
+            n = 8192
+            g = torch.Generator(device=device)
+            g.manual_seed(7)
+            a = torch.rand(n, n, device=device, dtype=torch.bfloat16, generator=g) * 2 - 1
+            b = torch.rand(n, n, device=device, dtype=torch.bfloat16, generator=g) * 2 - 1
+            c = torch.empty(n, n, device=device, dtype=torch.bfloat16)
+            ms = _time_ms(lambda: torch.matmul(a, b, out=c), reps=10, warm=5)
+            out["gemm_8192_bf16_tflops"] = round(2 * n ** 3 / (ms * 1e-3) / 1e12, 1)
+            try:
+                from mxllm.utils.gpumon import sample_device
+
+                smp = sample_device(device.index)
+                out["gfx_clock_mhz_under_gemm"] = smp.get("gfx_clock_mhz")
+                out["socket_power_w_under_gemm"] = smp.get("socket_power_w")
+            except Exception:  # noqa: BLE001  (SMI unavailable: the rates still stand)
+                pass
+            del a, b, c
+        except RuntimeError as e:  # out of memory on a loaded device: say so
+            out["gemm_error"] = str(e)[:200]
+        try:
+            nel = int(copy_gib * 2 ** 30) // 4
+            src = torch.empty(nel, device=device, dtype=torch.float32).uniform_()
+            dst = torch.empty_like(src)
+            ms = _time_ms(lambda: dst.copy_(src), reps=6, warm=2)
+            out["copy_4gb_tbps"] = round(2 * nel * 4 / (ms * 1e-3) / 1e12, 2)
+            del src, dst
+        except RuntimeError as e:
+            out["copy_error"] = str(e)[:200]
+        torch.cuda.empty_cache()
+    return out

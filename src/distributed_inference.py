@@ -119,7 +119,7 @@ def _configure_client(device):
 
         ensure_local_engine(CONFIG['MODEL_NAME'], device, RUN.engine_model, RUN.max_batch,
                             RUN.max_seq if device.type == "cuda" else min(RUN.max_seq, 1024), RUN.tokenizer,
-                            RUN.checkpoint, RUN.seed, RUN.engine_weights)
+                            RUN.checkpoint, RUN.seed, RUN.engine_weights, RUN.kv_pool_tokens)
 
 
 def _gather_results(records, rank, world_size):

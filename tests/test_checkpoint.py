@@ -163,3 +163,24 @@ def test_ddp_checkpoint_pieces_and_layout_remap(tmp_path, monkeypatch):
     assert abs(float(t2.train_step([(ids, ids)])) - l_next) < 1e-5
     del flat_mod
     runtime.cleanup()
+
+
+def test_layout_guard_and_json_identity():
+    """sharded optimizer state must only load into the same flat layout; the slot table
+    read back from the JSON manifest (lists) must compare equal to the live one (tuples)."""
+    import json
+
+    import pytest
+
+    from mxllm.train.checkpoint import _remap_segments, _require_same_layout
+
+    live = {"slots": [("a", 0, 4, [2, 2]), ("b", 4, 3, [3])], "numel": 7}
+    man = json.loads(json.dumps(live))
+    assert _remap_segments(man, live) == [(0, 7, 0)]  # identity, not the per-slot path
+    _require_same_layout(man, live, "ZeRO-1")
+    moved = {"slots": [["b", 0, 3, [3]], ["a", 3, 4, [2, 2]]], "numel": 7}
+    with pytest.raises(RuntimeError, match="different flat-buffer layout"):
+        _require_same_layout(moved, live, "ZeRO-1")
+    with pytest.raises(RuntimeError, match="no layout record"):
+        _require_same_layout(None, live, "ZeRO-1")
+    assert _remap_segments(moved, live) == [(3, 7, 0), (0, 3, 4)]

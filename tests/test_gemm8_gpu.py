@@ -1,0 +1,96 @@
+"""8-phase MFMA GEMM (csrc/kernels/gemm8.hip) vs a plain-PyTorch fp32 reference.
+
+All four operand orders (k- / mn-contiguous A and B), bf16 and fp32 output, beta 0 / 1, a
+device-scalar alpha, padded row strides, odd K-tile counts and (for the weight-gradient form,
+both operands token-major) token counts that are not a multiple of the 64-token K-tile: the
+rows past K read as zeros through the range-checked descriptors.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from mxllm.ops import native
+
+    return native()
+
+
+def _mat(rows, cols, dev, pad=0, seed=0):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    buf = (torch.rand(rows, cols + pad, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    return buf[:, :cols]
+
+
+def _check(got, ref, tol):
+    err = ((got.float() - ref).norm() / ref.norm()).item()
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 640), (768, 512, 192)])
+def test_gemm8_orders(gpu, a_kc, b_kc, M, N, K):
+    a = _mat(M, K, gpu, pad=8, seed=1) if a_kc else _mat(K, M, gpu, pad=16, seed=1)
+    b = _mat(N, K, gpu, pad=24, seed=2) if b_kc else _mat(K, N, gpu, pad=8, seed=2)
+    A = a.float() if a_kc else a.float().t()
+    B = b.float().t() if b_kc else b.float()
+    ref = A @ B
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    assert _ops().gemm8(a, a_kc, b, b_kc, out, 0.0, None, 1.0)
+    _check(out, ref, 5e-3)
+    out32 = torch.empty(M, N, device=gpu, dtype=torch.float32)
+    assert _ops().gemm8(a, a_kc, b, b_kc, out32, 0.0, None, 1.0)
+    _check(out32, ref, 1e-5)
+
+
+@pytest.mark.parametrize("f32", [True, False])
+def test_gemm8_beta_alpha(gpu, f32):
+    M, N, K = 512, 1024, 384
+    a, b = _mat(K, M, gpu, seed=3), _mat(K, N, gpu, seed=4)  # token-major dW form
+    c0 = _mat(M, N, gpu, pad=8, seed=5).to(torch.float32 if f32 else torch.bfloat16)
+    out = c0.clone()
+    alpha = torch.tensor([0.37], device=gpu)
+    assert _ops().gemm8(a, False, b, False, out, 1.0, alpha, 2.0)
+    ref = c0.float() + 0.74 * (a.float().t() @ b.float())
+    _check(out, ref, 1e-5 if f32 else 5e-3)
+
+
+@pytest.mark.parametrize("T", [1, 63, 100, 1000, 4097])
+def test_gemm8_weight_grad_odd_tokens(gpu, T):
+    M, N = 256, 512
+    dy, x = _mat(T, M, gpu, pad=8, seed=6), _mat(T, N, gpu, pad=8, seed=7)
+    out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.float32)  # beta 0 must ignore it
+    assert _ops().gemm8(dy, False, x, False, out, 0.0, None, 1.0)
+    _check(out, dy.float().t() @ x.float(), 1e-5)
+
+
+def test_gemm8_odd_ktiles_nn(gpu):
+    """the LoRA-augmented dX shape: K = N_out + 64 (an odd number of 64-deep K-tiles)."""
+    T, N, K = 512, 1024, 1024 + 64
+    dya = _mat(T, K, gpu, seed=8)
+    w = _mat(K, N, gpu, pad=64, seed=9)
+    out = torch.empty(T, N, device=gpu, dtype=torch.bfloat16)
+    assert _ops().gemm8(dya, True, w, False, out, 0.0, None, 1.0)
+    _check(out, dya.float() @ w.float(), 5e-3)
+
+
+def test_gemm8_declines_unsupported(gpu):
+    a, b = _mat(100, 64, gpu), _mat(256, 64, gpu)
+    out = torch.empty(100, 256, device=gpu, dtype=torch.bfloat16)
+    assert not _ops().gemm8(a, True, b, True, out, 0.0, None, 1.0)  # M not a multiple of 256
+    a2 = _mat(256, 100, gpu)
+    out2 = torch.empty(256, 256, device=gpu, dtype=torch.bfloat16)
+    assert not _ops().gemm8(a2, True, _mat(256, 100, gpu), True, out2, 0.0, None, 1.0)  # k-contig K % 64
+
+
+def test_gemm8_identity_asymmetric(gpu):
+    """A = I with an asymmetric B catches a transposed store (guide §3)."""
+    n = 256
+    a = torch.eye(n, device=gpu, dtype=torch.bfloat16)
+    b = (torch.arange(n, device=gpu).view(n, 1) * 3 + torch.arange(n, device=gpu).view(1, n) * 0.5 - 300) / 64
+    b = b.to(torch.bfloat16)
+    out = torch.empty(n, n, device=gpu, dtype=torch.float32)
+    assert _ops().gemm8(a, True, b, False, out, 0.0, None, 1.0)
+    assert torch.equal(out, b.float())

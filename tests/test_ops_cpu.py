@@ -214,3 +214,30 @@ def test_split_master_roundtrip_exact():
         adamw_step_(p32, grad, m1, v1, None, **kw)
         adamw_step_(sp, grad, m2, v2, None, **kw)
     assert torch.equal(sp.float(), p32) and torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
+def test_chunked_linear_cross_entropy_matches_reference():
+    """LM head + CE walked over T in chunks (global valid-token count, dh / dW formed in the
+    forward, scaled by the upstream gradient in the backward) == autograd of the plain form."""
+    import torch.nn.functional as F
+
+    from mxllm.ops.loss import ce_chunk_tokens, linear_cross_entropy
+
+    torch.manual_seed(0)
+    T, H, V = 37, 16, 50
+    h = torch.randn(T, H, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(V, H, dtype=torch.float64, requires_grad=True)
+    lab = torch.randint(0, V, (T,))
+    lab[3] = lab[20] = -100
+    for chunk in (8, 36, 37):
+        l1 = linear_cross_entropy(h, w, lab, chunk=chunk)
+        (l1 * 0.5).backward()
+        g1h, g1w = h.grad.clone(), w.grad.clone()
+        h.grad = w.grad = None
+        l2 = F.cross_entropy(h @ w.t(), lab, ignore_index=-100)
+        (l2 * 0.5).backward()
+        assert abs(float(l1) - float(l2)) < 1e-6
+        assert torch.allclose(g1h, h.grad, atol=1e-7) and torch.allclose(g1w, w.grad, atol=1e-7)
+        h.grad = w.grad = None
+    assert ce_chunk_tokens(4096, 128256) == 4096  # 1 GB of logits: one piece
+    assert ce_chunk_tokens(32768, 128256) == 4096  # 8.4 GB: chunked
