@@ -563,6 +563,17 @@ def run(a, env) -> dict:
                                   if k in gpu_sample},
         "trainable_params": (cfg.n_params() if a.parallel == "zero3" else model.num_params(trainable_only=True)),
     }
+    if a.parallel == "zero3":
+        # which communicator layout / optimizer schedule actually ran
+        c = trainer.comm
+        out["zero3"] = {
+            "comms": ("split: all-gathers and reduce-scatters on two communicators" if c.real and c.rs_pg is not None
+                      and c.rs_pg is not c.ag_pg else "single communicator" if c.real else "none (world 1 / emulated)"),
+            "adamw": "per unit on a side stream, overlapped with the next forward" if trainer.overlap_optimizer
+                     else "one launch after the backward",
+            "rmsnorm_unit": "replicated (all-reduced gradient, no re-gather)",
+            "max_inflight_reduce_scatters": trainer.max_inflight,
+        }
     if guard is not None:
         out["memory_guard"] = guard
     if emulated:

@@ -39,12 +39,14 @@ def main():
     res = {"shape": [B, Hq, Hkv, S, D]}
     res["fwd_ms"] = timeit(lambda: ops.attn_fwd(q, k, v, True, sc))
     res["bwd_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc))  # default (split) mode
-    res["bwd_atomic_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 1))
-    res["bwd_partials_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 2))
-    res["bwd_noatomic_ms"] = timeit(lambda: ops.attn_bwd_ablate(do, q, k, v, o, lse, -1, sc))
+    lite = len(sys.argv) > 6 and sys.argv[6] == "lite"  # long S: default modes only (mode 2's workspace ~ S^2)
+    if not lite:
+        res["bwd_atomic_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 1))
+        res["bwd_partials_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 2))
+        res["bwd_noatomic_ms"] = timeit(lambda: ops.attn_bwd_ablate(do, q, k, v, o, lse, -1, sc))
+        res["bwd_noatomic_TF"] = 2.5 * fl / res["bwd_noatomic_ms"] / 1e9
     res["fwd_TF"] = fl / res["fwd_ms"] / 1e9
     res["bwd_TF"] = 2.5 * fl / res["bwd_ms"] / 1e9
-    res["bwd_noatomic_TF"] = 2.5 * fl / res["bwd_noatomic_ms"] / 1e9
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
     cos = torch.randn(S, D // 2, device=dev)
     res["rope_split_ms"] = timeit(lambda: ops.rope_split(qkv, cos, cos, B, S, Hq, Hkv, D, None))

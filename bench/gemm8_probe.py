@@ -52,6 +52,10 @@ def time_ms(fn, calls):
     return statistics.median(s.elapsed_time(e) for s, e in ev)
 
 
+# the path each form takes without gemm8 (what a table entry must beat)
+DEFAULT = {"nn": "hipblaslt_nn", "tt": "transpose_tn", "tn": "hipblaslt_tn"}
+
+
 def run_case(name, flops, variants, rounds, calls):
     res = {k: [] for k in variants}
     for _ in range(rounds):
@@ -74,6 +78,14 @@ def main():
     ap.add_argument("--forms", default="nn,tt,tt32,tn")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-table", action="store_true", help="hipBLASLt defaults instead of the tuned table")
+    ap.add_argument("--shapes", default="", help="comma list of projection names to run (default all)")
+    ap.add_argument("--aug", action="store_true",
+                    help="also the 70B LoRA headline's augmented shapes (K + 64 pad, padded weight buffers) and head")
+    ap.add_argument("--write-table", default=None,
+                    help="write the shapes where gemm8 beats the default path by >= --margin (JSON for mxllm/ops/gemm.py)")
+    ap.add_argument("--margin", type=float, default=0.01)
+    ap.add_argument("--layout-exp", action="store_true", help="K-parity / row-stride experiment on the o dX shape")
+    ap.add_argument("--layout-exp-only", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     if not a.no_table:
@@ -84,46 +96,115 @@ def main():
     T = a.tokens
     forms = a.forms.split(",")
     models = ["70b", "8b"] if a.model == "both" else [a.model]
+    only = set(filter(None, a.shapes.split(",")))
     results = []
+    wins = []
+    measured = set()
+
+    def record(res, form, M, N, K, out):
+        results.append(res)
+        measured.add((form, M, N, K, out))
+        g, d = res["gemm8"]["ms"], res[DEFAULT[form]]["ms"]
+        if g < d * (1 - a.margin):
+            wins.append({"form": form, "M": M, "N": N, "K": K, "out": out, "gemm8_tflops": res["gemm8"]["tflops"],
+                         "default_tflops": res[DEFAULT[form]]["tflops"], "case": res["case"]})
+
+    if a.layout_exp:
+        # why the 70B LoRA o-projection dX (K = 8192 + 64, padded buffers) runs ~17 % slower than the
+        # plain shape in BOTH kernels: K-tile parity vs row stride of the operands
+        for K, lda, ldb in ((8192, 8192, 8192), (8256, 8256, 8256), (8192, 8256, 8256), (8256, 8256, 8192),
+                            (8256, 8320, 8320), (8320, 8320, 8320), (8192, 8320, 8320)):
+            M, N = T, 8192
+            xa = rnd(M, lda, dev=dev)[:, :K]
+            wb = rnd(K, ldb, dev=dev)[:, :N]
+            o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            record(run_case(f"layout o dX nn K{K} lda{lda} ldb{ldb}", 2.0 * M * N * K, {
+                "gemm8": lambda: ops.gemm8(xa, True, wb, False, o, 0.0, None, 1.0),
+                "hipblaslt_nn": lambda: torch.mm(xa, wb, out=o)}, a.rounds, a.calls), "nn", M, N, K, "bf16")
+            del xa, wb, o
+            torch.cuda.empty_cache()
+        if a.layout_exp_only:
+            return
+    if a.aug:
+        P = 64  # LoRA pad of every 70B projection (n * r rounded up to 64)
+        for name, form, M, N, K, ldb in (("o dX", "nn", T, 8192, 8192 + P, 8192 + P),
+                                         ("gu dX", "nn", T, 8192, 57344 + P, 8192 + P),
+                                         ("down fwd (transposed buffer)", "nn", T, 8192, 28672 + P, 8192 + P),
+                                         ("head dX", "nn", T, 8192, 128256, 8192),
+                                         ("qkv fwd", "tn", T, 10240, 8192 + P, 8192 + P),
+                                         ("o fwd", "tn", T, 8192, 8192 + P, 8192 + P),
+                                         ("gu fwd", "tn", T, 57344, 8192 + P, 8192 + P),
+                                         ("qkv dX (image)", "tn", T, 8192, 10240 + P, 10240 + P),
+                                         ("down dX (transposed buffer)", "tn", T, 28672, 8192 + P, 8192 + P),
+                                         ("head fwd", "tn", T, 128256, 8192, 8192)):
+            xa = rnd(M, K, dev=dev)
+            o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            if form == "nn":
+                wb = rnd(K, ldb, dev=dev)[:, :N]
+                var = {"gemm8": lambda: ops.gemm8(xa, True, wb, False, o, 0.0, None, 1.0),
+                       "hipblaslt_nn": lambda: torch.mm(xa, wb, out=o)}
+            else:
+                wb = rnd(N, K, dev=dev)
+                var = {"gemm8": lambda: ops.gemm8(xa, True, wb, True, o, 0.0, None, 1.0),
+                       "hipblaslt_tn": lambda: torch.mm(xa, wb.t(), out=o)}
+            record(run_case(f"70b-lora {name} {form} M{M} N{N} K{K}", 2.0 * M * N * K, var, a.rounds, a.calls),
+                   form, M, N, K, "bf16")
+            del xa, wb, o
+            torch.cuda.empty_cache()
     for mdl in models:
         for pname, (O, I) in SHAPES[mdl].items():
+            if only and pname not in only:
+                continue
             fl = 2.0 * T * O * I
             w = rnd(O, I, dev=dev)
             dy = rnd(T, O, dev=dev)
             x = rnd(T, I, dev=dev)
             if "nn" in forms and T % 256 == 0 and I % 256 == 0:
                 o = torch.empty(T, I, device=dev, dtype=torch.bfloat16)
-                results.append(run_case(f"{mdl} {pname} dX nn T{T}", fl, {
+                record(run_case(f"{mdl} {pname} dX nn T{T}", fl, {
                     "gemm8": lambda: ops.gemm8(dy, True, w, False, o, 0.0, None, 1.0),
                     "hipblaslt_nn": lambda: torch.mm(dy, w, out=o),
-                }, a.rounds, a.calls))
+                }, a.rounds, a.calls), "nn", T, I, O, "bf16")
             if "tt" in forms and O % 256 == 0 and I % 256 == 0:
                 o = torch.empty(O, I, device=dev, dtype=torch.bfloat16)
-                results.append(run_case(f"{mdl} {pname} dW tt bf16 T{T}", fl, {
+                record(run_case(f"{mdl} {pname} dW tt bf16 T{T}", fl, {
                     "gemm8": lambda: ops.gemm8(dy, False, x, False, o, 0.0, None, 1.0),
                     "transpose_tn": lambda: torch.mm(transpose2d(dy), transpose2d(x).t(), out=o),
                     "hipblaslt_nt": lambda: torch.mm(dy.t(), x, out=o),
-                }, a.rounds, a.calls))
+                }, a.rounds, a.calls), "tt", O, I, T, "bf16")
             if "tt32" in forms and O % 256 == 0 and I % 256 == 0:
                 o32 = torch.zeros(O, I, device=dev, dtype=torch.float32)
-                results.append(run_case(f"{mdl} {pname} dW tt fp32+=  T{T}", fl, {
+                record(run_case(f"{mdl} {pname} dW tt fp32+=  T{T}", fl, {
                     "gemm8": lambda: ops.gemm8(dy, False, x, False, o32, 1.0, None, 1.0),
                     "transpose_tn": lambda: torch.ops.aten.addmm.dtype_out(
                         o32, transpose2d(dy), transpose2d(x).t(), torch.float32, beta=1.0, out=o32),
                     "hipblaslt_nt": lambda: torch.ops.aten.addmm.dtype_out(o32, dy.t(), x, torch.float32, beta=1.0,
                                                                             out=o32),
-                }, a.rounds, a.calls))
+                }, a.rounds, a.calls), "tt", O, I, T, "f32")
             if "tn" in forms and O % 256 == 0:
                 o = torch.empty(T, O, device=dev, dtype=torch.bfloat16)
-                results.append(run_case(f"{mdl} {pname} fwd tn T{T}", fl, {
+                record(run_case(f"{mdl} {pname} fwd tn T{T}", fl, {
                     "gemm8": lambda: ops.gemm8(x, True, w, True, o, 0.0, None, 1.0),
                     "hipblaslt_tn": lambda: torch.mm(x, w.t(), out=o),
-                }, a.rounds, a.calls))
+                }, a.rounds, a.calls), "tn", T, O, I, "bf16")
             del w, dy, x
             torch.cuda.empty_cache()
     if a.json_out:
         with open(a.json_out, "w") as f:
             json.dump(results, f, indent=1)
+    if a.write_table:
+        old = []
+        if os.path.exists(a.write_table):
+            with open(a.write_table) as f:
+                old = json.load(f).get("wins", [])
+        key = lambda e: (e["form"], e["M"], e["N"], e["K"], e["out"])  # noqa: E731
+        # entries of shapes not measured in this run are kept; measured shapes take this run's verdict
+        merged = {key(e): e for e in old if key(e) not in measured}
+        merged.update({key(e): e for e in wins})
+        with open(a.write_table, "w") as f:
+            json.dump({"arch": "gfx950", "source": "bench/gemm8_probe.py", "tokens": T, "margin": a.margin,
+                       "wins": sorted(merged.values(), key=key)}, f, indent=1)
+        print(json.dumps({"table": a.write_table, "wins": len(merged)}), flush=True)
 
 
 if __name__ == "__main__":

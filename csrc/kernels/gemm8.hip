@@ -336,23 +336,44 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
           }
         }
     }
+    if constexpr (OUT_F32) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t m = ml + qa * 64 + 16 * i;
-        const int n = nl + 32 * (j >> 1) + 16 * (j & 1);
-        f32x4 v = acc[4 * qa + i][j] * alpha;
-        if constexpr (BETA) v += old[i][j];
-        if constexpr (OUT_F32) {
+        for (int j = 0; j < 4; ++j) {
+          const int64_t m = ml + qa * 64 + 16 * i;
+          const int n = nl + 32 * (j >> 1) + 16 * (j & 1);
+          f32x4 v = acc[4 * qa + i][j] * alpha;
+          if constexpr (BETA) v += old[i][j];
           *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + m * ldc + n) = v;
-        } else {
-          uint2 o;
-          o.x = pack_bf16x2(v[0], v[1]);
-          o.y = pack_bf16x2(v[2], v[3]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + m * ldc + n) = o;
         }
-      }
+    } else {
+      // bf16: blocks j, j + 1 are 16 columns apart and lanes l, l + 16 hold adjacent 4-column groups
+      // of one row, so one v_permlane16_swap per packed dword pair gives every lane 8 consecutive
+      // columns -> ONE 16-B store per block pair (guide T21, with the 16-lane swap) instead of two 8-B
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          f32x4 va = acc[4 * qa + i][2 * jp] * alpha, vb = acc[4 * qa + i][2 * jp + 1] * alpha;
+          if constexpr (BETA) {
+            va += old[i][2 * jp];
+            vb += old[i][2 * jp + 1];
+          }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(va[0], va[1]), pack_bf16x2(vb[0], vb[1]),
+                                                          false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[2], vb[3]),
+                                                          false, false);
+          const int64_t m = ml + qa * 64 + 16 * i;
+          const int n = n0 + wc * 64 + 32 * jp + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5);
+          uint4 o;
+          o.x = s0[0];
+          o.y = s1[0];
+          o.z = s0[1];
+          o.w = s1[1];
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(C) + m * ldc + n) = o;
+        }
+    }
   }
 }
 
@@ -372,7 +393,7 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
   if (lda % 8 || ldb % 8 || ldc % 4 || ((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)C & 15)) return -1;
   if (a_kc ? lda < K : lda < M) return -1;
   if (b_kc ? ldb < K : ldb < N) return -1;
-  if (ldc < N || (!out_f32 && ldc % 4)) return -1;
+  if (ldc < N || (!out_f32 && ldc % 8)) return -1;  // bf16 epilogue: 16-B stores
   if (beta != 0.f && beta != 1.f) return -1;
   const int64_t kpad = (int64_t)((K + G8_BK - 1) / G8_BK) * G8_BK;
   const int64_t aspan = a_kc ? 256 * lda : kpad * lda;

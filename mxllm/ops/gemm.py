@@ -1,0 +1,110 @@
+"""GEMM dispatch between the hand-written 8-phase MFMA kernel (csrc/kernels/gemm8.hip) and
+hipBLASLt / rocBLAS (``torch.mm`` with the tuned solution table, mxllm/utils/gemm_tuning.py).
+
+Every training GEMM of a Llama step is one of four operand orders over row-major bf16 storage:
+
+  form  A stored   B stored   computes          used for
+  tn    [M][K]     [N][K]     A @ B^T           forward  y = x W^T
+  nn    [M][K]     [K][N]     A @ B             input gradient  dX = dY W
+  tt    [K][M]     [K][N]     A^T @ B           weight gradient dW = dY^T X (token-major operands)
+  nt    [K][M]     [N][K]     A^T @ B^T         (unused; for completeness)
+
+``gemm8`` is selected per (form, M, N, K, output dtype) only where it was measured faster
+(``mxllm/tuning/gemm8_gfx950.json``, written from ``bench/gemm8_probe.py`` runs), or for every
+shape it takes in deterministic mode (``MXLLM_DETERMINISTIC=1``: one workgroup per output tile,
+a fixed K order, no split-K or atomics — the step is bitwise reproducible; vendor stream-K
+solutions are not, profiles/r3aa).  ``MXLLM_GEMM8=0`` disables it, ``=all`` forces it wherever
+it takes the shape (A/B runs).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+
+from ._ext import native, use_native
+
+_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                           "gemm8_gfx950.json")
+_TABLE: dict | None = None
+
+
+def deterministic() -> bool:
+    return os.environ.get("MXLLM_DETERMINISTIC", "0") == "1"
+
+
+def _table() -> dict:
+    global _TABLE
+    if _TABLE is None:
+        _TABLE = {}
+        try:
+            with open(_TABLE_PATH) as f:
+                for e in json.load(f).get("wins", []):
+                    _TABLE[(e["form"], e["M"], e["N"], e["K"], e["out"])] = True
+        except (OSError, ValueError, KeyError):
+            pass
+    return _TABLE
+
+
+def _policy() -> str:
+    return os.environ.get("MXLLM_GEMM8", "table")
+
+
+def takes(form: str, M: int, N: int, K: int) -> bool:
+    """Shape constraints of the kernel (mirrors mx_gemm8)."""
+    if M % 256 or N % 256 or K <= 0:
+        return False
+    return K % 64 == 0 or form == "tt"
+
+
+def want(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> bool:
+    pol = _policy()
+    if pol == "0" or not takes(form, M, N, K):
+        return False
+    if pol == "all" or deterministic():
+        return True
+    return (form, M, N, K, "f32" if out_dtype == torch.float32 else "bf16") in _table()
+
+
+# (A k-contiguous, B k-contiguous) per form
+_KC = {"tn": (True, True), "nn": (True, False), "tt": (False, False), "nt": (False, True)}
+
+
+def _dims(form, a, b):
+    if form == "tn":
+        return a.shape[0], b.shape[0], a.shape[1]
+    if form == "nn":
+        return a.shape[0], b.shape[1], a.shape[1]
+    if form == "tt":
+        return a.shape[1], b.shape[1], a.shape[0]
+    return a.shape[1], b.shape[0], a.shape[0]
+
+
+def mm(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, beta: float = 0.0,
+       alpha_t: torch.Tensor | None = None, out_dtype: torch.dtype | None = None) -> torch.Tensor:
+    """``out = beta * out + alpha_t * op(a) op(b)`` in operand order ``form`` (module doc).
+    ``out`` None: a new [M, N] tensor of ``out_dtype`` (default: a's dtype) and beta is 0.
+    ``alpha_t``: optional 1-element f32 device scalar (no host sync)."""
+    M, N, K = _dims(form, a, b)
+    odt = out.dtype if out is not None else (out_dtype or a.dtype)
+    if out is None:
+        out = torch.empty(M, N, dtype=odt, device=a.device)
+        beta = 0.0
+    if (use_native(a) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and odt in (torch.bfloat16,
+                                                                                              torch.float32)
+            and want(form, M, N, K, odt)):
+        a_kc, b_kc = _KC[form]
+        if native().gemm8(a, a_kc, b, b_kc, out, float(beta), alpha_t, 1.0):
+            return out
+    A = a if form in ("tn", "nn") else a.t()
+    B = b.t() if form in ("tn", "nt") else b
+    if alpha_t is not None:
+        A = A * alpha_t.to(A.dtype)
+    if odt == a.dtype:
+        if beta == 0.0:
+            return torch.mm(A, B, out=out)
+        return out.addmm_(A, B, beta=beta)
+    if a.is_cuda:  # bf16 operands, fp32 output (hipBLASLt D = C in fp32)
+        return torch.ops.aten.addmm.dtype_out(out, A, B, odt, beta=beta, out=out)
+    return out.mul_(beta).add_(A.float() @ B.float()) if beta != 0.0 else out.copy_(A.float() @ B.float())

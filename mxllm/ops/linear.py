@@ -32,6 +32,7 @@ import torch
 import torch.nn.functional as F
 
 from ..parallel.grad_ready import direct_grad, direct_grad32, mark_ready
+from . import gemm
 from ._ext import native, use_native
 
 
@@ -151,7 +152,7 @@ class _LoRAAugFn(torch.autograd.Function):
             native().lora_xwt(x2, amat, xa[:, K:], scaling)  # s t, zero in the pad columns
         else:
             xa[:, K:].addmm_(x2, amat.t(), beta=0.0, alpha=scaling)
-        y = torch.mm(xa, wbuf[:, :N]) if tr else torch.mm(xa, wbuf[:N, :].t())
+        y = gemm.mm("nn", xa, wbuf[:, :N]) if tr else gemm.mm("tn", xa, wbuf[:N, :])
         ctx.save_for_backward(xa, wbuf)
         ctx.lora_a, ctx.lora_b, ctx.wbt, ctx.wxt = a, b, wbt, wxt
         ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat, tr)
@@ -205,11 +206,11 @@ class _LoRAAugFn(torch.autograd.Function):
                 else:
                     db = tgt
         if tr:  # [W; A]^T is the leading K rows of the transposed buffer: TN form
-            dx = torch.mm(dya, wbuf[:K, :].t())
+            dx = gemm.mm("tn", dya, wbuf[:K, :])
         elif ctx.wxt is not None:  # reduction-contiguous image of [W; A]: hipBLASLt "TN"
-            dx = torch.mm(dya, ctx.wxt.t())
-        else:
-            dx = torch.mm(dya, wbuf[:, :K])
+            dx = gemm.mm("tn", dya, ctx.wxt)
+        else:  # the n-contiguous weight itself ("NN": gemm8 where it wins, csrc/kernels/gemm8.hip)
+            dx = gemm.mm("nn", dya, wbuf[:, :K])
         return dx.view(xshape), da, db, None, None, None, None, None, None, None, None
 
 
@@ -260,6 +261,13 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, be
     ``dy_scale``: 1-element device tensor multiplying dy (folded into dy's
     transpose on that path; the cross-entropy's upstream gradient)."""
     f32 = out is not None and out.dtype == torch.float32 and dy.dtype != torch.float32
+    if use_native(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
+        # token-major operands straight into the 8-phase MFMA GEMM (no transposes) where it wins
+        odt = out.dtype if out is not None else dy.dtype
+        if gemm.want("tt", dy.shape[1], x.shape[1], dy.shape[0], odt):
+            sc = None if dy_scale is None else dy_scale.reshape(1).float()
+            return gemm.mm("tt", dy, x, out=out, beta=beta if out is not None else 0.0, alpha_t=sc,
+                           out_dtype=odt)
     if _dw_kernel_on() and use_native(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
         # token-major operands straight into the MFMA kernel (csrc/kernels/dw_gemm.hip): the
         # transposes happen in its LDS reads; False = shape not taken -> the path below
@@ -324,13 +332,13 @@ class _LinearFn(torch.autograd.Function):
         # ZeRO-3 the saved ``w`` unpacks as a view of the re-gathered unit, not the leaf
         ctx.wp = w if w.is_leaf else None
         ctx.xshape = x.shape
-        return torch.mm(x2, w.t()).view(*x.shape[:-1], w.shape[0])
+        return gemm.mm("tn", x2, w).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
-        dx = torch.mm(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = gemm.mm("nn", dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = param_weight_grad(ctx.wp, dy2, x2) if ctx.needs_input_grad[1] else None
         return dx, dw
 

@@ -28,13 +28,14 @@ import torch.nn.functional as F
 from . import reference as ref
 from ._ext import native, use_native
 from ..parallel.grad_ready import direct_grad, direct_grad32, mark_ready
+from . import gemm
 from .linear import param_weight_grad, weight_grad_
 
 
 class _LinearCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, w, labels, ignore_index):
-        logits = torch.matmul(h, w.t())  # [T, V] bf16, hipBLASLt
+        logits = gemm.mm("tn", h, w)  # [T, V] bf16
         loss, _ = native().ce_fwd_bwd(logits, labels, ignore_index)  # logits <- dlogits
         ctx.save_for_backward(h, w, logits)
         ctx.wp = w if w.is_leaf else None
@@ -49,7 +50,7 @@ class _LinearCEFn(torch.autograd.Function):
         h, w, dlogits = ctx.saved_tensors
         dh = dw = None
         if ctx.needs_input_grad[0]:
-            dh = torch.matmul(dlogits, w)
+            dh = gemm.mm("nn", dlogits, w)
             dh.mul_(gl.to(dh.dtype))  # [T, H]: cheap, unlike scaling the [T, V] dlogits
         if ctx.needs_input_grad[1]:
             # the head's dW: gl folded into dlogits' transpose (token-contiguous operand image)
@@ -99,11 +100,11 @@ class _ChunkedLinearCEFn(torch.autograd.Function):
             t1 = min(T, t0 + chunk)
             hc, lab = h[t0:t1], labels[t0:t1]
             lg = buf[: t1 - t0]
-            torch.matmul(hc, w.t(), out=lg)
+            gemm.mm("tn", hc, w, out=lg)
             losses[t0:t1] = (native().ce_chunk(lg, lab, ignore_index, inv_n) if nat
                              else _ce_chunk_torch(lg, lab, inv_n, ignore_index))
             if need_h:
-                torch.matmul(lg, w, out=dh[t0:t1])
+                gemm.mm("nn", lg, w, out=dh[t0:t1])
             if need_w:
                 weight_grad_(dwacc, lg, hc, beta=0.0 if i == 0 else 1.0)
         loss = losses.sum() * inv_n[0]

@@ -166,9 +166,10 @@ class Comm:
             torch.sum(full.view(self.world, -1), dim=0, out=out)
         return None
 
-    def all_reduce(self, t: torch.Tensor):
+    def all_reduce(self, t: torch.Tensor, async_op: bool = False):
         if self.real:
-            dist.all_reduce(t, group=self.rs_pg)
+            return dist.all_reduce(t, group=self.rs_pg, async_op=async_op)
+        return None
 
 
 class Unit:
@@ -184,9 +185,14 @@ class Unit:
             self.offsets.append(off)
             off += n
         self.numel = off
-        chunk = world * ALIGN
+        # the resident unit (every RMSNorm weight, ~1.3 M params at 70B) is REPLICATED, not
+        # sharded: every rank holds and updates all of it (its gradient is all-reduced), so it
+        # never needs a re-gather after the optimizer step (no synchronous regather)
+        self.replicated = resident
+        wsz = 1 if resident else world
+        chunk = wsz * ALIGN
         self.full_numel = (off + chunk - 1) // chunk * chunk
-        self.shard_numel = self.full_numel // world
+        self.shard_numel = self.full_numel // wsz
         self.full: torch.Tensor | None = None
         self.work = None
         self.shard = None  # bf16 view (set by the trainer)
@@ -201,7 +207,7 @@ class Unit:
         self.gdt = None  # gradient dtype (reduce-scatter / accumulation): fp32 or bf16
         # world 1 (not emulated): the shard IS the full unit — no gather copy, and
         # with fp32 gradients the dW GEMMs write straight into the fp32 grad shard
-        self.local = world == 1 and not comm.emulate
+        self.local = (world == 1 and not comm.emulate) or resident
 
     # -------------------------------------------------------------- gather / release
     def gather(self, async_op: bool = True):
@@ -274,12 +280,37 @@ class Unit:
                 p.grad = self.gbuf[o:o + n].view(s)
             p._mx_grad_fresh = fresh
 
+    def reduce_replicated(self):
+        """Replicated unit, once per step: its gradient (summed over the step's
+        micro-batches) into the fp32 ``grad_shard``, then an all-reduce (sum over the
+        ranks) in place.  Returns the work handle (None: nothing in flight)."""
+        direct = self._collect()
+        if not direct:
+            self.grad_shard.copy_(self.gbuf[:self.shard_numel])
+        self.gbuf = None
+        if self.comm.emulate:  # emulated world N: N identical ranks would sum N copies
+            self.grad_shard.mul_(float(self.world))
+        return self.comm.all_reduce(self.grad_shard, async_op=True)
+
     def reduce_async(self, first: bool = True):
         """Launch the reduce-scatter of the unit's gradient buffer; returns
         (work | None, shard | None, fold).  ``fold``: the shard must still be added
         into ``grad_shard`` (bf16 gradients, or a later micro-batch); fp32 on the
         first micro-batch reduce-scatters straight into ``grad_shard``, and world 1
         with fp32 gradients has nothing to reduce (the GEMMs wrote ``grad_shard``)."""
+        direct = self._collect()
+        if direct:
+            self.gbuf = None
+            return None, None, False
+        into = first and self.grad32
+        out = self.grad_shard if into else torch.empty(self.shard_numel, dtype=self.gdt, device=self.device)
+        work = self.comm.reduce_scatter(out, self.gbuf, async_op=True)
+        self.gbuf = None  # RCCL keeps the buffer alive until the collective is done
+        return work, (None if into else out), not into
+
+    def _collect(self) -> bool:
+        """Every parameter's gradient into the unit's gradient buffer (``gbuf``); returns
+        whether that buffer is ``grad_shard`` itself."""
         if self.gbuf is None:
             g0 = self.params[0].grad if len(self.params) == 1 else None
             if (g0 is not None and g0.is_contiguous() and g0.numel() == self.full_numel
@@ -309,14 +340,7 @@ class Unit:
             p._mx_grad32 = None
         self.seen.clear()
         self.reduced = True
-        if direct:
-            self.gbuf = None
-            return None, None, False
-        into = first and self.grad32
-        out = self.grad_shard if into else torch.empty(self.shard_numel, dtype=self.gdt, device=self.device)
-        work = self.comm.reduce_scatter(out, self.gbuf, async_op=True)
-        self.gbuf = None  # RCCL keeps the buffer alive until the collective is done
-        return work, (None if into else out), not into
+        return direct
 
 
 class _PreBackward(torch.autograd.Function):
@@ -455,6 +479,18 @@ class Zero3Trainer:
             if a is not b:
                 self._below[a.uid] = b
         self._B = self._S = 0
+        # ---- optimizer / next-forward overlap: the fused AdamW runs unit by
+        # unit on a side stream in FORWARD order; the next forward waits for unit u's update just
+        # before it gathers / uses u, so the update of the units it has not reached yet runs under
+        # its GEMMs instead of as one serial launch between the steps
+        self._side = (torch.cuda.Stream(dev) if dev.type == "cuda"
+                      and os.environ.get("MXLLM_Z3_ADAMW_OVERLAP", "1") != "0" else None)
+        self._pending: dict[int, torch.cuda.Event] = {}
+        self._hold = None
+        self._fwd_order = [self.units[0], self.units[1]] + [self._units_by_layer[i] for i in range(len(model.layers))]
+        if self._head is not self.units[1]:
+            self._fwd_order.append(self._head)
+        self.overlap_optimizer = self._side is not None
         model._zero3 = self
         log.info("ZeRO-3: %d units, %.2f M params/rank (world %d%s, act-ckpt %s)", len(self.units), total / 1e6,
                  self.world, " emulated" if self.emulated else "", self.act_ckpt)
@@ -477,7 +513,8 @@ class Zero3Trainer:
                 fill(u.names, u.shapes, full)
             else:
                 full = init_unit_full(u.uid, u.names, u.numels, u.full_numel, seed, self.device)
-            u.shard.copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
+            r = 0 if u.replicated else self.rank
+            u.shard.copy_(full[r * u.shard_numel:(r + 1) * u.shard_numel])
             del full
         self.units[0].materialize()  # norms stay resident
 
@@ -564,12 +601,20 @@ class Zero3Trainer:
             return torch.as_strided(u.full, shape, stride, off)
         return obj
 
+    def _wait_update(self, u: Unit):
+        """The compute stream waits for unit u's overlapped AdamW (no host sync)."""
+        ev = self._pending.pop(u.uid, None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
     def _gather(self, u: Unit, async_op=True):
+        self._wait_update(u)  # the gather reads the updated shard (RCCL orders after the current stream)
         u.gather(async_op=async_op)
         if not u.local:  # world 1: the "gathered" unit is the persistent shard, nothing to release
             self._by_storage[u.full.untyped_storage().data_ptr()] = u
 
     def _use(self, u: Unit, prefetch: Unit | None = None):
+        self._wait_update(u)
         if u.full is None:
             self._gather(u)
         if prefetch is not None and prefetch.full is None:
@@ -591,6 +636,7 @@ class Zero3Trainer:
         cfg = m.cfg
         B, S = ids.shape
         self._B, self._S = B, S
+        self._wait_update(self.units[0])  # every layer's RMSNorm reads the replicated unit
         for u in self.units:
             u.seen.clear()
             u.reduced = False
@@ -635,11 +681,9 @@ class Zero3Trainer:
             total = loss.detach() if total is None else total + loss.detach()
         self._drain()
         self._first = True
-        work, out, fold = norms.reduce_async(True)
+        work = norms.reduce_replicated()  # all-reduce of the replicated unit's fp32 gradient
         if work is not None:
             work.wait()
-        if fold:
-            norms.grad_shard.copy_(out)
         for u in self.units[1:]:
             if not u.grad_written:  # no gradient at all this step (unused): a zero update input
                 u.grad_shard.zero_()
@@ -648,21 +692,43 @@ class Zero3Trainer:
         self.step_num += 1
         o = self.opt
         if o.grad_clip and o.grad_clip > 0:
-            sq = ops.sq_norm(self.grads)
+            # sharded units: sum of squares over the ranks; the replicated unit (flat [0, n0),
+            # identical on every rank after its all-reduce) is counted once
+            n0 = norms.shard_numel
+            sq = ops.sq_norm(self.grads[n0:])
             self.comm.all_reduce(sq)
+            sq = sq + ops.sq_norm(self.grads[:n0])
             gnorm = sq.sqrt() * scale
             self.last_grad_norm = gnorm
             gscale = torch.clamp(o.grad_clip / (gnorm + 1e-6), max=1.0) * scale
         else:
             gscale = scale
-        ops.adamw_step_(self.master, self.grads, self.m, self.v, self.shard_params, lr=o.lr_at(self.step_num),
-                        beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay, step=self.step_num,
-                        grad_scale=gscale, zero_grad=False)  # every shard is overwritten by the next step
-        self._refresh_resident()
+        kw = dict(lr=o.lr_at(self.step_num), beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
+                  step=self.step_num, grad_scale=gscale, zero_grad=False)  # every shard is overwritten next step
+        if self._side is None:
+            ops.adamw_step_(self.master, self.grads, self.m, self.v, self.shard_params, **kw)
+        else:
+            self._launch_overlapped(kw)
         return total / n
 
+    def _launch_overlapped(self, kw):
+        """The fused AdamW over each unit's shard on the side stream in forward order, one
+        event per unit (waited in _use / _gather).  Same elementwise kernel over the same
+        slices with the same inputs: bitwise identical to the one-launch update."""
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        self._hold = kw["grad_scale"]  # read on the side stream: keep it alive until the next step
+        with torch.cuda.stream(side):
+            for u in self._fwd_order:
+                off = u.grad_shard.storage_offset() - self.grads.storage_offset()
+                sl = slice(off, off + u.shard_numel)
+                ops.adamw_step_(self.master[sl], self.grads[sl], self.m[sl], self.v[sl], self.shard_params[sl], **kw)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self._pending[u.uid] = ev
+
     def _refresh_resident(self):
-        # the resident unit's gathered copy must follow its updated shards
+        # the replicated unit IS its shard (updated in place by AdamW): re-point its parameters
         norms = self.units[0]
         norms.full = None
         norms.work = None
@@ -671,6 +737,7 @@ class Zero3Trainer:
 
     # ---------------------------------------------------------------- state
     def state_dict(self):
+        self.params_ready()
         return {"step": self.step_num, "master": self.master, "m": self.m, "v": self.v}
 
     def load_state_dict(self, sd):
@@ -688,19 +755,26 @@ class Zero3Trainer:
         self._refresh_resident()
 
     def params_ready(self):
-        """API parity with Trainer: nothing is in flight between steps."""
+        """Order the current stream after every in-flight overlapped unit update: call
+        before reading parameters / optimizer state outside a step (checkpoints, export)."""
+        for u in self.units:
+            self._wait_update(u)
 
     def full_master_state(self) -> dict:
         """Every fp32 master weight, gathered unit by unit (collective: all ranks
         call it; tests / export)."""
+        self.params_ready()
         out = {}
         for u in self.units:
-            full = torch.empty(u.full_numel, dtype=torch.float32, device=self.device)
             src = u.master_view.float().contiguous()
-            if self.comm.real:
-                dist.all_gather_into_tensor(full, src, group=self.pg)
+            if u.replicated:
+                full = src
             else:
-                full.view(self.world, -1).copy_(src.unsqueeze(0).expand(self.world, -1))
+                full = torch.empty(u.full_numel, dtype=torch.float32, device=self.device)
+                if self.comm.real:
+                    dist.all_gather_into_tensor(full, src, group=self.pg)
+                else:
+                    full.view(self.world, -1).copy_(src.unsqueeze(0).expand(self.world, -1))
             for name, o, n, shp in zip(u.names, u.offsets, u.numels, u.shapes):
                 out[name] = full[o:o + n].view(shp).clone()
         return out

@@ -153,7 +153,8 @@ def _save_zero3(d: str, tr, rank: int) -> list:
         _write(os.path.join(d, "z3", f"rank_{rank}", f"unit_{u.uid:04d}.safetensors"),
                {"master": tr.master[sl], "m": tr.m[sl], "v": tr.v[sl]})
         table.append({"uid": u.uid, "names": u.names, "numels": u.numels, "numel": u.numel,
-                      "full_numel": u.full_numel, "shard_numel": u.shard_numel})
+                      "full_numel": u.full_numel, "shard_numel": u.shard_numel,
+                      "replicated": bool(getattr(u, "replicated", False))})
     return table
 
 
@@ -280,11 +281,17 @@ def _load_zero3(d, man, tr, rank, world):
         if e is None or e["names"] != u.names or e["numel"] != u.numel:
             raise RuntimeError(f"checkpoint unit {u.uid} does not match the model ({u.names[:2]}...)")
         S_old = e["shard_numel"]
+        # a replicated unit (every rank holds all of it) was written whole by every rank: read
+        # rank 0's copy; a unit replicated now takes the whole content [0, numel)
+        old_q = 1 if e.get("replicated") else old_world
+        if e.get("replicated"):
+            S_old = e["numel"]
         off = u.master_view.storage_offset() - tr.master.storage_offset()
-        a0, a1 = rank * u.shard_numel, min((rank + 1) * u.shard_numel, u.numel)
+        r = 0 if getattr(u, "replicated", False) else rank
+        a0, a1 = r * u.shard_numel, min((r + 1) * u.shard_numel, u.numel)
         for buf in (tr.master, tr.m, tr.v):
             buf[off:off + u.shard_numel].zero_()
-        for q in range(old_world):
+        for q in range(old_q):
             lo, hi = max(a0, q * S_old), min(a1, (q + 1) * S_old)
             if lo >= hi:
                 continue
@@ -330,7 +337,7 @@ def _load_zero3_weights(d: str, man: dict, named: dict):
         for e in man["units"]:
             S = e["shard_numel"]
             full = torch.cat([load_file(os.path.join(d, "z3", f"rank_{q}", f"unit_{e['uid']:04d}.safetensors"))
-                              ["master"][:S] for q in range(world)])
+                              ["master"][:S] for q in range(1 if e.get("replicated") else world)])
             o = 0
             for name, n in zip(e["names"], e["numels"]):
                 if name in named:

@@ -711,3 +711,50 @@ def test_dw_gemm_declines_untiled_shapes(gpu):
     out = torch.zeros(320, 256, device=gpu, dtype=torch.bfloat16)
     assert not _ops().dw_gemm(dy, x, out, 0.0, None)
     assert not _ops().dw_gemm(dy[:48], x[:48], out, 0.0, None)  # T not a multiple of 64
+
+
+def test_chunked_lm_head_ce_matches_unchunked_gpu(gpu):
+    """Long-sequence LM head + CE walked in token chunks (ce_inv_count + ce_chunk kernels,
+    dh / dW formed per chunk) == the one-piece fused path, loss and gradients."""
+    from mxllm.ops.loss import linear_cross_entropy
+
+    torch.manual_seed(11)
+    T, H, V = 1000, 256, 4096
+    h = (torch.randn(T, H, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(V, H, device=gpu) * 0.05).to(torch.bfloat16).requires_grad_(True)
+    lab = torch.randint(0, V, (T,), device=gpu)
+    lab[::17] = -100
+    res = []
+    for chunk in (None, 256):
+        loss = linear_cross_entropy(h, w, lab) if chunk is None else linear_cross_entropy(h, w, lab, chunk=chunk)
+        (loss * 0.5).backward()
+        res.append((float(loss), h.grad.float().clone(), w.grad.float().clone()))
+        h.grad = w.grad = None
+    (l0, gh0, gw0), (l1, gh1, gw1) = res
+    assert abs(l0 - l1) < 1e-4 * abs(l0)
+    assert rel_err(gh1, gh0) < 1e-2 and rel_err(gw1, gw0) < 1e-2
+
+
+@pytest.mark.parametrize("S", [8192])
+def test_attention_long_context_vs_fp32(gpu, S):
+    """Long context: causal GQA attention at S=8192 through the training
+    kernels (forward + the default split backward) against an fp32 PyTorch reference —
+    output, dQ, dK, dV."""
+    torch.manual_seed(9)
+    B, Hq, Hkv, D = 1, 8, 2, 128
+    q = torch.randn(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    sc = 1.0 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, True, sc)
+    do = torch.randn(B, S, Hq, D, device=gpu, dtype=torch.bfloat16)
+    dq, dkp, dvp = _ops().attn_bwd(do.view(B, S, Hq * D), q, k, v, o, lse, True, sc, 3)
+    dk = dkp.view(B, Hkv, -1, S, D).sum(2)
+    dv = dvp.view(B, Hkv, -1, S, D).sum(2)
+    qf, kf, vf = [t.float().requires_grad_(True) for t in (q, k, v)]
+    orf = ref.attention(qf.transpose(1, 2), kf.transpose(1, 2), vf.transpose(1, 2), causal=True)
+    assert rel_err(o.view(B, S, Hq, D), orf) < 2e-2
+    orf.backward(do.float())
+    assert rel_err(dq, qf.grad) < 3e-2
+    assert rel_err(dk, kf.grad) < 3e-2
+    assert rel_err(dv, vf.grad) < 3e-2

@@ -182,7 +182,9 @@ def test_zero3_emulated_world4_one_step_gpu(gpu, ck):
         full = torch.zeros(u.full_numel, dtype=torch.float32, device=gpu)
         for name, o, n in zip(u.names, u.offsets, u.numels):
             full[o:o + n] = gd[name]
-        exp[off:off + u.shard_numel] = full.view(4, -1).sum(0)
+        # sharded unit: the emulated reduce-scatter sums the 4 slices; the replicated RMSNorm
+        # unit: the emulated all-reduce of 4 identical ranks = 4 x its gradient
+        exp[off:off + u.shard_numel] = full * 4 if u.replicated else full.view(4, -1).sum(0)
         off += u.shard_numel
     z.train_step([(ids, ids)])
     o = z.opt
@@ -197,6 +199,30 @@ def test_zero3_emulated_world4_one_step_gpu(gpu, ck):
     d = (z.master.float() - want).abs()
     # step 1 of AdamW moves every weight by ~lr * sign(g): only near-zero gradients can differ
     assert float(d.mean()) < 2e-5 and int((d > 2e-4).sum()) <= max(8, 2e-3 * d.numel()), float(d.max())
+
+
+@pytest.mark.parametrize("ck", [False, 2])
+def test_zero3_overlapped_adamw_bitwise_gpu(gpu, ck):
+    """ZeRO-3's per-unit AdamW on the side stream, overlapped with the next forward
+    (each unit waited for just before it is used), gives bitwise the same weights and
+    losses as the one-launch update after the step."""
+    cfg = _cfg()
+    g = torch.Generator(device=gpu).manual_seed(6)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=g) for _ in range(3)]
+    res = {}
+    for ov in ("0", "1"):
+        os.environ["MXLLM_Z3_ADAMW_OVERLAP"] = ov
+        try:
+            z = _zero3(gpu, cfg, 21, activation_checkpointing=ck, grad_dtype=torch.float32)
+        finally:
+            os.environ.pop("MXLLM_Z3_ADAMW_OVERLAP", None)
+        assert z.overlap_optimizer == (ov == "1")
+        losses = [z.train_step([(b, b)]) for b in batches]
+        res[ov] = ([float(x) for x in losses], z.full_master_state())
+        del z
+    assert res["0"][0] == res["1"][0]
+    for n, w in res["0"][1].items():
+        assert torch.equal(w, res["1"][1][n]), n
 
 
 def test_bench_config2_field_tiny(gpu, tmp_path):

@@ -34,6 +34,8 @@ def _run(rank, world, port, q, mode, steps):
     # "..._bf16": bf16 gradient reduction in both trainers (default: fp32 in both)
     gdt = torch.bfloat16 if mode.endswith("_bf16") else torch.float32
     mode = mode.removesuffix("_bf16")
+    acc2 = mode.endswith("_acc2")  # two micro-batches per step (gradient accumulation)
+    mode = mode.removesuffix("_acc2")
     cfg = get_config("tiny").replace(n_layers=3, vocab_size=320)
     opt = OptimConfig(lr=3e-3, grad_clip=1.0, weight_decay=0.01)
     if mode.startswith("zero3"):
@@ -54,8 +56,12 @@ def _run(rank, world, port, q, mode, steps):
     ids = torch.randint(0, cfg.vocab_size, (world * 2, 24), generator=g)
     losses = []
     mine = ids.view(world, 2, 24)[rank]  # fixed batch: the loss must go down
+    mbs = [(mine[:1], mine[:1]), (mine[1:], mine[1:])] if acc2 else [(mine, mine)]
     for s in range(steps):
-        losses.append(float(tr.train_step([(mine, mine)])))
+        losses.append(float(tr.train_step(mbs)))
+    if mode.startswith("zero3") and world > 1:
+        # the default runs gathers and reduce-scatters on two communicators (split RCCL streams)
+        assert tr.comm.rs_pg is not None and tr.comm.rs_pg is not tr.comm.ag_pg
     tot = runtime.all_reduce_scalars(losses, "sum")
     if mode.startswith("zero3"):
         master = tr.full_master_state()
@@ -90,11 +96,14 @@ def _launch(mode, world, steps=3):
     return res
 
 
-@pytest.mark.parametrize("world,gd", [(1, ""), (2, ""), (4, ""), (2, "_bf16")])
+@pytest.mark.parametrize("world,gd", [(1, ""), (2, ""), (4, ""), (2, "_bf16"), (8, "_acc2")])
 def test_zero3_matches_ddp_per_parameter(world, gd):
+    """world 8 (BASELINE config 4's world) with gradient accumulation 2: plain and
+    selective checkpointing (first 2 of 3 layers), split gather / reduce-scatter communicators."""
     ddp_loss, ddp_w = _launch("ddp" + gd, world)
-    modes = {1: ["zero3", "zero3_ckpt", "zero3_ckpt2"], 2: ["zero3", "zero3_ckpt2"]}.get(world, ["zero3", "zero3_ckpt"])
-    if gd:
+    modes = {1: ["zero3", "zero3_ckpt", "zero3_ckpt2"], 2: ["zero3", "zero3_ckpt2"],
+             8: ["zero3", "zero3_ckpt2"]}.get(world, ["zero3", "zero3_ckpt"])
+    if gd == "_bf16":
         modes = ["zero3"]
     got = {}
     for mode in modes:
@@ -131,7 +140,9 @@ def test_zero3_emulated_world_shards():
     z1 = Zero3Trainer(cfg, env, OptimConfig(lr=1e-3), seed=3)
     z4 = Zero3Trainer(cfg, env, OptimConfig(lr=1e-3), seed=3, emulate_world=4, activation_checkpointing=True)
     assert z4.world == 4 and z4.emulated
-    assert z4.master.numel() * 4 == sum(u.full_numel for u in z4.units)
+    # sharded units hold 1/4 of their content; the replicated RMSNorm unit all of it
+    assert z4.units[0].replicated and not any(u.replicated for u in z4.units[1:])
+    assert z4.master.numel() == sum(u.full_numel // (1 if u.replicated else 4) for u in z4.units)
     assert z4.master.numel() < z1.master.numel() // 3
     ids = torch.randint(0, cfg.vocab_size, (2, 16))
     for _ in range(2):
