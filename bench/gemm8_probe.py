@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--margin", type=float, default=0.01)
     ap.add_argument("--layout-exp", action="store_true", help="K-parity / row-stride experiment on the o dX shape")
     ap.add_argument("--layout-exp-only", action="store_true")
+    ap.add_argument("--ablate", action="store_true", help="timing-only ablation builds of the NN kernel")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     if not a.no_table:
@@ -109,6 +110,23 @@ def main():
             wins.append({"form": form, "M": M, "N": N, "K": K, "out": out, "gemm8_tflops": res["gemm8"]["tflops"],
                          "default_tflops": res[DEFAULT[form]]["tflops"], "case": res["case"]})
 
+    if a.ablate:
+        # timing-only ablations of the NN kernel (results wrong): doubled MFMA per phase, no barriers
+        M, N, K = T, 8192, 8192
+        xa, wb = rnd(M, K, dev=dev), rnd(K, N, dev=dev)
+        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+        def var(v):
+            def f():
+                os.environ["MXLLM_GEMM8_ABLATE"] = str(v)
+                ops.gemm8(xa, True, wb, False, o, 0.0, None, 1.0)
+            return f
+        res = run_case("ablate o dX nn (v0 real, v1 2x MFMA, v2 no barriers, v3 both)", 2.0 * M * N * K,
+                       {f"v{v}": var(v) for v in range(4)}, a.rounds, a.calls)
+        os.environ.pop("MXLLM_GEMM8_ABLATE", None)
+        results.append(res)
+        if a.layout_exp_only:
+            return
     if a.layout_exp:
         # why the 70B LoRA o-projection dX (K = 8192 + 64, padded buffers) runs ~17 % slower than the
         # plain shape in BOTH kernels: K-tile parity vs row stride of the operands

@@ -101,7 +101,10 @@ __device__ __forceinline__ uint32_t g8_mn_lane(int lane, int cb) {
   return (uint32_t)((8 * g + q) * 256 + 16 * (((cb >> 3) ^ (2 * t)) + (p >> 1)) + 8 * (p & 1));
 }
 
-template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA>
+// V != 0: timing-only ablation builds (bench/gemm8_probe.py --ablate; results are WRONG):
+//   V & 1: every phase issues its 16 MFMAs twice (MFMA time per barrier doubled)
+//   V & 2: no barriers in the K loop and no wave-row stagger (no LDS ordering at all)
+template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA, int V = 0>
 __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
              void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
@@ -257,16 +260,17 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     vm0();
   }
   __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+  if (!(V & 2) && wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
 
   // one phase: reads -> prefetch -> [wait] -> barrier -> lgkmcnt(0) -> MFMA -> barrier
-#define G8_SYNC_MMA(QA, QB, FB) \
-  __builtin_amdgcn_s_barrier(); \
-  lds_wait();                   \
-  pin_a();                      \
-  pin_b(FB);                    \
-  mma(QA, QB, FB);              \
-  __builtin_amdgcn_s_barrier();
+#define G8_SYNC_MMA(QA, QB, FB)                   \
+  if constexpr (!(V & 2)) __builtin_amdgcn_s_barrier(); \
+  lds_wait();                                     \
+  pin_a();                                        \
+  pin_b(FB);                                      \
+  mma(QA, QB, FB);                                \
+  if constexpr (V & 1) mma(QA, QB, FB);           \
+  if constexpr (!(V & 2)) __builtin_amdgcn_s_barrier();
 
   for (int kt = 0;; kt += 2) {
     // phases 1-4: tile kt in buffer 0
@@ -311,7 +315,7 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
     if (kt + 2 >= nk) break;
   }
 #undef G8_SYNC_MMA
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the stagger barrier
+  if (!(V & 2) && wr == 0) __builtin_amdgcn_s_barrier();  // match the stagger barrier
 
   // ---- epilogue: lane holds C[m][n .. n+3] per block
   const float alpha = alpha_f * (alpha_t ? alpha_t[0] : 1.f);
@@ -411,6 +415,18 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
       if (acc) G8_L(AK, BK_, false, true); else G8_L(AK, BK_, false, false); \
     }                                                          \
   } while (0)
+  if (const char* ab = getenv("MXLLM_GEMM8_ABLATE")) {  // timing-only variants, NN bf16 beta 0 (results wrong)
+    const int v = atoi(ab);
+    if (a_kc && !b_kc && !out_f32 && !acc && v >= 1 && v <= 3) {
+      if (v == 1)
+        gemm8_kernel<true, false, false, false, 1><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f);
+      else if (v == 2)
+        gemm8_kernel<true, false, false, false, 2><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f);
+      else
+        gemm8_kernel<true, false, false, false, 3><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f);
+      return (int)hipGetLastError();
+    }
+  }
   if (a_kc && b_kc)
     G8_OUT(true, true);
   else if (a_kc)

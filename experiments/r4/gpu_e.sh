@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 4 pass E: gemm8 ablations (barrier / MFMA-per-barrier share), then re-probe with the
+# permlane16 bf16 epilogue (nn / tt forms) and rewrite the win table
+OUT=gpurun_out/r4e; mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 200 python -u -m pytest tests/test_gemm8_gpu.py -q --timeout 120 --timeout-method thread > $OUT/tests.txt 2>&1
+rc=$?; tail -2 $OUT/tests.txt; case $rc in 0) ;; *) exit $rc;; esac
+timeout -k 10 200 python -u bench/gemm8_probe.py --ablate --layout-exp-only --rounds 5 > $OUT/ablate.txt 2>&1 || { echo "ablate rc=$?"; exit 1; }
+grep ablate $OUT/ablate.txt
+cp mxllm/tuning/gemm8_gfx950.json $OUT/gemm8_gfx950.json
+timeout -k 10 500 python -u bench/gemm8_probe.py --aug --forms nn,tt,tt32 --rounds 3 --write-table $OUT/gemm8_gfx950.json --json-out $OUT/probe.json > $OUT/probe.txt 2>&1 || { echo "probe rc=$?"; exit 1; }
+tail -1 $OUT/probe.txt

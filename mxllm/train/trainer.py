@@ -48,6 +48,18 @@ def _overlap_default() -> bool:
     return os.environ.get("MXLLM_OVERLAP_ADAMW", "1") != "0"
 
 
+def _fresh_guard(p):
+    """Tensor hook (runs before AccumulateGrad adds ``g`` into ``p.grad``): a slot still
+    flagged fresh holds last step's gradient -> zero it first (fp32 mode: the flat fold in
+    ``sync_grads_from_params`` already copies instead of adding)."""
+    def hook(g):
+        if getattr(p, "_mx_grad_fresh", False) and getattr(p, "_mx_grad32", None) is None and p.grad is not None:
+            p.grad.zero_()
+            p._mx_grad_fresh = False
+        return g
+    return hook
+
+
 class Trainer:
     def __init__(self, model: torch.nn.Module, env: DistEnv, optim: OptimConfig | None = None, *,
                  bucket_mb: float = 128.0, first_bucket_mb: float = 16.0, broadcast_init: bool = False,
@@ -133,6 +145,13 @@ class Trainer:
         self.fresh_grads = (os.environ.get("MXLLM_FRESH_GRADS", "1") != "0" and self.flat.device.type == "cuda"
                             and self.zero1 is None and not getattr(model, "lora", False)
                             and not any(getattr(p, "_mx_no_direct", False) for p in self.flat.param_list))
+        if self.fresh_grads:
+            # enforce the invariant: a gradient that reaches a parameter through
+            # autograd's AccumulateGrad (not an op honouring _mx_grad_fresh) would be ADDED onto
+            # last step's stale slot -- zero the slot first, once, right before that accumulation
+            for p in self.flat.param_list:
+                if p.requires_grad:
+                    p.register_hook(_fresh_guard(p))
         # ---- gradient-norm overlap: each DDP bucket's sum of squares is taken on a side
         # stream as soon as the bucket is final (after its all-reduce), under the rest of
         # the backward, instead of one pass over the whole gradient after it (8B full:

@@ -193,6 +193,18 @@ def main(argv=None):
         loader.close()
         if monitor is not None:
             monitor.stop()
+        if run.metrics_file and hasattr(trainer, "master_fp32"):
+            # bit-level digest of the final fp32 master weights (exact integer sums of the bit
+            # patterns): equal digests <=> (almost surely) bitwise-equal weights -- deterministic
+            # mode / resume comparisons (scripts/compare_resume.py)
+            m = trainer.master_fp32().reshape(-1).view(torch.int32)
+            s1 = s2 = 0
+            for lo in range(0, m.numel(), 1 << 26):
+                c = m[lo:lo + (1 << 26)].to(torch.int64)
+                s1 += int(c.sum())
+                s2 += int((c * torch.arange(lo, lo + c.numel(), device=c.device, dtype=torch.int64).remainder_(
+                    1000003)).sum())
+            metrics.write(kind="final", step=total, master_bits_sum=s1, master_bits_wsum=s2, numel=m.numel())
         if run.save_hf:
             export_hf(run, trainer, rank)
         runtime.barrier()

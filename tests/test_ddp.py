@@ -109,3 +109,18 @@ def test_ddp_matches_single_process(full, bucket_mb, accum, world):
     tol = 2e-2 if ref.dtype == torch.bfloat16 else 1e-5
     assert err <= tol * max(1.0, ref.float().abs().max().item()), err
     assert same, "ranks diverged after the optimizer step"
+
+
+def test_fresh_guard_zeroes_stale_slot_before_autograd_accumulates():
+    """ADVICE r3 (fresh gradients): a parameter whose gradient arrives through autograd's
+    AccumulateGrad while its flat slot is still flagged fresh must not be added onto last
+    step's stale gradient: the guard hook zeroes the slot first, once."""
+    from mxllm.train.trainer import _fresh_guard
+
+    p = torch.nn.Parameter(torch.ones(4))
+    p.grad = torch.full((4,), 7.0)  # stale slot content from the previous step
+    p._mx_grad_fresh = True
+    p.register_hook(_fresh_guard(p))
+    ((p * 2).sum() + (p * 3).sum()).backward()  # two contributions: zero once, then both accumulate
+    assert torch.equal(p.grad, torch.full((4,), 5.0))
+    assert p._mx_grad_fresh is False
