@@ -197,7 +197,7 @@ bool dw_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, double 
 // bf16 views, out fp32 or bf16; alpha = alpha_f * (the optional f32 device scalar alpha_t).
 // Returns false (nothing launched) for shapes the kernel does not take.
 bool gemm8(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::Tensor& out, double beta,
-           const c10::optional<at::Tensor>& alpha_t, double alpha_f) {
+           const c10::optional<at::Tensor>& alpha_t, double alpha_f, int64_t ph) {
   MX_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm8: GPU tensors");
   MX_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm8: bf16 operands");
   MX_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "gemm8: fp32 / bf16 output");
@@ -216,7 +216,7 @@ bool gemm8(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::T
   DevGuard g(a.device());
   const int rc = mx_gemm8(bf(a), a.stride(0), a_kc ? 1 : 0, bf(b), b.stride(0), b_kc ? 1 : 0, out.data_ptr(),
                           out.stride(0), out.scalar_type() == at::kFloat ? 1 : 0, (int)M, (int)N, (int)K, (float)beta,
-                          sc, (float)alpha_f, cur_stream());
+                          sc, (float)alpha_f, (int)ph, cur_stream());
   if (rc == -1) return false;
   MX_OK(rc);
   return true;
@@ -983,7 +983,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
   m.def("transpose2d(Tensor x, Tensor? scale=None) -> Tensor");
   m.def("dw_gemm(Tensor dy, Tensor x, Tensor(a!) out, float beta, Tensor? scale=None) -> bool");
-  m.def("gemm8(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, float beta, Tensor? alpha_t=None, float alpha=1.0) -> bool");
+  m.def("gemm8(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, float beta, Tensor? alpha_t=None, float alpha=1.0, int ph=8) -> bool");
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
   m.def("sqnorm(Tensor x) -> Tensor");

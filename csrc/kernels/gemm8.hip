@@ -104,7 +104,10 @@ __device__ __forceinline__ uint32_t g8_mn_lane(int lane, int cb) {
 // V != 0: timing-only ablation builds (bench/gemm8_probe.py --ablate; results are WRONG):
 //   V & 1: every phase issues its 16 MFMAs twice (MFMA time per barrier doubled)
 //   V & 2: no barriers in the K loop and no wave-row stagger (no LDS ordering at all)
-template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA, int V = 0>
+// PH = 4: the same images and registers on a 4-phase schedule (two quadrants = 32 MFMAs per phase,
+// half the barriers; every phase retires its LDS reads before its first barrier so each image is
+// restaged one phase after its last read; two half-tiles in flight across barriers, vmcnt(4))
+template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA, int V = 0, int PH = 8>
 __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
              void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
@@ -246,16 +249,17 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   auto vm6 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); };
   auto vm0 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
-  // ---- prologue: K-tile 0 (all four images) + K-tile 1's B0, A0, B1; retire tile 0
+  auto vm4 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); };
+  // ---- prologue: K-tile 0 (all four images) + K-tile 1's B0, A0, B1 (PH 4: B0, B1); retire tile 0
   issue(0, 2);
   issue(0, 0);
   issue(0, 3);
   issue(0, 1);
   if (nk > 1) {
     issue(1, 2);
-    issue(1, 0);
+    if constexpr (PH == 8) issue(1, 0);
     issue(1, 3);
-    vm6();
+    if constexpr (PH == 8) vm6(); else vm4();
   } else {
     vm0();
   }
@@ -272,6 +276,63 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   if constexpr (V & 1) mma(QA, QB, FB);           \
   if constexpr (!(V & 2)) __builtin_amdgcn_s_barrier();
 
+  if constexpr (PH == 4) {
+#define G8_SYNC_MMA2(QA, QB0, FB0, QB1, FB1)              \
+  __builtin_amdgcn_s_barrier();                           \
+  pin_a();                                                \
+  pin_b(FB0);                                             \
+  pin_b(FB1);                                             \
+  mma(QA, QB0, FB0);                                      \
+  mma(QA, QB1, FB1);                                      \
+  __builtin_amdgcn_s_barrier();
+    for (int kt = 0;; kt += 2) {
+      // phase 1: buffer 0 (tile kt) B0, B1, A0; tile kt + 1's A0, A1 -> buffer 1
+      read_b(0, 0, fb0);
+      read_b(0, 1, fb1);
+      read_a(0, 0);
+      if (kt + 1 < nk) {
+        issue(kt + 1, 0);
+        issue(kt + 1, 1);
+      }
+      lds_wait();  // retired before the barrier: these images are restageable next phase
+      G8_SYNC_MMA2(0, 0, fb0, 1, fb1)
+      // phase 2: buffer 0 A1; tile kt + 2's B0, B1 -> buffer 0; retire tile kt + 1
+      read_a(0, 1);
+      if (kt + 2 < nk) {
+        issue(kt + 2, 2);
+        issue(kt + 2, 3);
+        vm4();
+      } else {
+        vm0();
+      }
+      lds_wait();
+      G8_SYNC_MMA2(1, 1, fb1, 0, fb0)
+      if (kt + 1 >= nk) break;
+      // phase 3: buffer 1 (tile kt + 1) B0, B1, A0; tile kt + 2's A0, A1 -> buffer 0
+      read_b(1, 0, fb0);
+      read_b(1, 1, fb1);
+      read_a(1, 0);
+      if (kt + 2 < nk) {
+        issue(kt + 2, 0);
+        issue(kt + 2, 1);
+      }
+      lds_wait();
+      G8_SYNC_MMA2(0, 0, fb0, 1, fb1)
+      // phase 4: buffer 1 A1; tile kt + 3's B0, B1 -> buffer 1; retire tile kt + 2
+      read_a(1, 1);
+      if (kt + 3 < nk) {
+        issue(kt + 3, 2);
+        issue(kt + 3, 3);
+        vm4();
+      } else {
+        vm0();
+      }
+      lds_wait();
+      G8_SYNC_MMA2(1, 1, fb1, 0, fb0)
+      if (kt + 2 >= nk) break;
+    }
+#undef G8_SYNC_MMA2
+  } else
   for (int kt = 0;; kt += 2) {
     // phases 1-4: tile kt in buffer 0
     read_b(0, 0, fb0);
@@ -391,7 +452,7 @@ using namespace mx;
 // every operand's addressed span < 2 GiB.  Returns -1 (nothing launched) for shapes it does not take.
 extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc, void* C,
                         int64_t ldc, int out_f32, int M, int N, int K, float beta, const float* alpha_t, float alpha_f,
-                        hipStream_t stream) {
+                        int ph, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || (M & 255) || (N & 255)) return -1;
   if ((a_kc || b_kc) && (K % G8_BK)) return -1;
   if (lda % 8 || ldb % 8 || ldc % 4 || ((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)C & 15)) return -1;
@@ -405,8 +466,15 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
   if (aspan * 2 >= ((int64_t)1 << 31) || bspan * 2 >= ((int64_t)1 << 31)) return -1;
   const int grid = (M >> 8) * (N >> 8);
   const bool acc = beta != 0.f;
-#define G8_L(AK, BK_, F, BT) \
-  gemm8_kernel<AK, BK_, F, BT><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f)
+  const char* phs = getenv("MXLLM_GEMM8_PH");  // read per call: overrides `ph` (same-process A/B)
+  const bool ph4 = phs && *phs ? atoi(phs) == 4 : ph == 4;
+#define G8_L(AK, BK_, F, BT)                                                                                        \
+  do {                                                                                                              \
+    if (ph4)                                                                                                        \
+      gemm8_kernel<AK, BK_, F, BT, 0, 4><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f); \
+    else                                                                                                            \
+      gemm8_kernel<AK, BK_, F, BT><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f);      \
+  } while (0)
 #define G8_OUT(AK, BK_)                                        \
   do {                                                         \
     if (out_f32) {                                             \

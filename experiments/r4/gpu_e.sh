@@ -8,5 +8,5 @@ rc=$?; tail -2 $OUT/tests.txt; case $rc in 0) ;; *) exit $rc;; esac
 timeout -k 10 200 python -u bench/gemm8_probe.py --ablate --layout-exp-only --rounds 5 > $OUT/ablate.txt 2>&1 || { echo "ablate rc=$?"; exit 1; }
 grep ablate $OUT/ablate.txt
 cp mxllm/tuning/gemm8_gfx950.json $OUT/gemm8_gfx950.json
-timeout -k 10 500 python -u bench/gemm8_probe.py --aug --forms nn,tt,tt32 --rounds 3 --write-table $OUT/gemm8_gfx950.json --json-out $OUT/probe.json > $OUT/probe.txt 2>&1 || { echo "probe rc=$?"; exit 1; }
+timeout -k 10 600 python -u bench/gemm8_probe.py --aug --ph4 --forms nn,tt,tt32,tn --rounds 3 --write-table $OUT/gemm8_gfx950.json --json-out $OUT/probe.json > $OUT/probe.txt 2>&1 || { echo "probe rc=$?"; exit 1; }
 tail -1 $OUT/probe.txt

@@ -41,7 +41,7 @@ def _table() -> dict:
         try:
             with open(_TABLE_PATH) as f:
                 for e in json.load(f).get("wins", []):
-                    _TABLE[(e["form"], e["M"], e["N"], e["K"], e["out"])] = True
+                    _TABLE[(e["form"], e["M"], e["N"], e["K"], e["out"])] = int(e.get("ph", 8))
         except (OSError, ValueError, KeyError):
             pass
     return _TABLE
@@ -58,13 +58,22 @@ def takes(form: str, M: int, N: int, K: int) -> bool:
     return K % 64 == 0 or form == "tt"
 
 
-def want(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> bool:
+def schedule(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> int:
+    """0 = not on gemm8; else its phase schedule (8 or 4) for this shape."""
     pol = _policy()
     if pol == "0" or not takes(form, M, N, K):
-        return False
-    if pol == "all" or deterministic():
-        return True
-    return (form, M, N, K, "f32" if out_dtype == torch.float32 else "bf16") in _table()
+        return 0
+    ph = _table().get((form, M, N, K, "f32" if out_dtype == torch.float32 else "bf16"), 0)
+    if ph:
+        return ph
+    return DEFAULT_PH if (pol == "all" or deterministic()) else 0
+
+
+DEFAULT_PH = int(os.environ.get("MXLLM_GEMM8_DEFAULT_PH", "8"))
+
+
+def want(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> bool:
+    return schedule(form, M, N, K, out_dtype) > 0
 
 
 # (A k-contiguous, B k-contiguous) per form
@@ -91,11 +100,11 @@ def mm(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = N
     if out is None:
         out = torch.empty(M, N, dtype=odt, device=a.device)
         beta = 0.0
-    if (use_native(a) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and odt in (torch.bfloat16,
-                                                                                              torch.float32)
-            and want(form, M, N, K, odt)):
+    ph = (schedule(form, M, N, K, odt) if use_native(a) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+          and odt in (torch.bfloat16, torch.float32) else 0)
+    if ph:
         a_kc, b_kc = _KC[form]
-        if native().gemm8(a, a_kc, b, b_kc, out, float(beta), alpha_t, 1.0):
+        if native().gemm8(a, a_kc, b, b_kc, out, float(beta), alpha_t, 1.0, ph):
             return out
     A = a if form in ("tn", "nn") else a.t()
     B = b.t() if form in ("tn", "nt") else b

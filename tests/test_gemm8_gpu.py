@@ -29,9 +29,11 @@ def _check(got, ref, tol):
     assert err < tol, err
 
 
+@pytest.mark.parametrize("ph", ["8", "4"])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 640), (768, 512, 192)])
-def test_gemm8_orders(gpu, a_kc, b_kc, M, N, K):
+def test_gemm8_orders(gpu, a_kc, b_kc, M, N, K, ph, monkeypatch):
+    monkeypatch.setenv("MXLLM_GEMM8_PH", ph)  # 8-phase (default) and 4-phase schedules
     a = _mat(M, K, gpu, pad=8, seed=1) if a_kc else _mat(K, M, gpu, pad=16, seed=1)
     b = _mat(N, K, gpu, pad=24, seed=2) if b_kc else _mat(K, N, gpu, pad=8, seed=2)
     A = a.float() if a_kc else a.float().t()
@@ -57,8 +59,10 @@ def test_gemm8_beta_alpha(gpu, f32):
     _check(out, ref, 1e-5 if f32 else 5e-3)
 
 
+@pytest.mark.parametrize("ph", ["8", "4"])
 @pytest.mark.parametrize("T", [1, 63, 100, 1000, 4097])
-def test_gemm8_weight_grad_odd_tokens(gpu, T):
+def test_gemm8_weight_grad_odd_tokens(gpu, T, ph, monkeypatch):
+    monkeypatch.setenv("MXLLM_GEMM8_PH", ph)
     M, N = 256, 512
     dy, x = _mat(T, M, gpu, pad=8, seed=6), _mat(T, N, gpu, pad=8, seed=7)
     out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.float32)  # beta 0 must ignore it
@@ -66,8 +70,10 @@ def test_gemm8_weight_grad_odd_tokens(gpu, T):
     _check(out, dy.float().t() @ x.float(), 1e-5)
 
 
-def test_gemm8_odd_ktiles_nn(gpu):
+@pytest.mark.parametrize("ph", ["8", "4"])
+def test_gemm8_odd_ktiles_nn(gpu, ph, monkeypatch):
     """the LoRA-augmented dX shape: K = N_out + 64 (an odd number of 64-deep K-tiles)."""
+    monkeypatch.setenv("MXLLM_GEMM8_PH", ph)
     T, N, K = 512, 1024, 1024 + 64
     dya = _mat(T, K, gpu, seed=8)
     w = _mat(K, N, gpu, pad=64, seed=9)
