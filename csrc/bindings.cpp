@@ -222,6 +222,13 @@ bool gemm8(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::T
   return true;
 }
 
+// the gemm8 diagnostic build's cycle stamps (MXLLM_GEMM8_STAMPS): int64 [1024, 2, 80] on the host
+at::Tensor gemm8_stamps() {
+  auto out = at::empty({1024, 2, 80}, at::TensorOptions().dtype(at::kLong));
+  MX_OK(mx_gemm8_stamps(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>())));
+  return out;
+}
+
 // A HIP stream confined to a subset of the device's CUs (hipExtStreamCreateWithCUMask):
 // ``mask`` = one int per 32 CUs (bit i of word w = CU 32 w + i).  Returns the stream handle
 // for torch.cuda.ExternalStream; the stream lives for the process (never destroyed).
@@ -986,6 +993,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("gemm8(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, float beta, Tensor? alpha_t=None, float alpha=1.0, int ph=8) -> bool");
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
+  m.def("gemm8_stamps() -> Tensor", &gemm8_stamps);
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");

@@ -101,9 +101,21 @@ __device__ __forceinline__ uint32_t g8_mn_lane(int lane, int cb) {
   return (uint32_t)((8 * g + q) * 256 + 16 * (((cb >> 3) ^ (2 * t)) + (p >> 1)) + 8 * (p & 1));
 }
 
+// In-kernel cycle stamps (diagnostic build V & 4; guide §7 "In-kernel stamps"): lane 0 of wave 0
+// (wave row 0) and of wave 4 (wave row 1) record s_memtime at kernel start, after the prologue,
+// at the top of every K-loop iteration (2 K-tiles) and after the loop / the epilogue, plus
+// s_memrealtime at start and end (clock = d memtime / d realtime x 100 MHz).  Written with
+// ordinary VECTOR global stores into a buffer nothing else reads; the normal build has none.
+constexpr int G8_NST = 80;
+__device__ unsigned long long g8_stamps[1024 * 2 * G8_NST];
+__device__ __forceinline__ void g8_stamp(int wg, int row, int k, unsigned long long v) {
+  if (wg < 1024 && k < G8_NST) g8_stamps[((size_t)wg * 2 + row) * G8_NST + k] = v;
+}
+
 // V != 0: timing-only ablation builds (bench/gemm8_probe.py --ablate; results are WRONG):
 //   V & 1: every phase issues its 16 MFMAs twice (MFMA time per barrier doubled)
 //   V & 2: no barriers in the K loop and no wave-row stagger (no LDS ordering at all)
+//   V & 4: stamps only (results correct)
 // PH = 4: the same images and registers on a 4-phase schedule (two quadrants = 32 MFMAs per phase,
 // half the barriers; every phase retires its LDS reads before its first barrier so each image is
 // restaged one phase after its last read; two half-tiles in flight across barriers, vmcnt(4))
@@ -129,6 +141,16 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int nk = (K + G8_BK - 1) / G8_BK;
+  constexpr bool ST = (V & 4) != 0;
+  const bool stw = ST && (tid == 0 || tid == 256);  // lane 0 of waves 0 and 4
+  const int strow = tid >= 256;
+  int sti = 0;
+  if constexpr (ST) {
+    if (stw) {
+      g8_stamp(blockIdx.x, strow, sti++, __builtin_amdgcn_s_memtime());
+      g8_stamp(blockIdx.x, strow, sti++, __builtin_amdgcn_s_memrealtime());
+    }
+  }
 
   // ---- operand descriptors (range-checked: mn-contiguous rows past K read as zeros)
   const uint16_t* abase = A_KC ? A + (int64_t)m0 * lda : A + m0;
@@ -265,6 +287,9 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   }
   __builtin_amdgcn_s_barrier();
   if (!(V & 2) && wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+  if constexpr (ST) {
+    if (stw) g8_stamp(blockIdx.x, strow, sti++, __builtin_amdgcn_s_memtime());
+  }
 
   // one phase: reads -> prefetch -> [wait] -> barrier -> lgkmcnt(0) -> MFMA -> barrier
 #define G8_SYNC_MMA(QA, QB, FB)                   \
@@ -286,6 +311,9 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   mma(QA, QB1, FB1);                                      \
   __builtin_amdgcn_s_barrier();
     for (int kt = 0;; kt += 2) {
+      if constexpr (ST) {
+        if (stw) g8_stamp(blockIdx.x, strow, sti++, __builtin_amdgcn_s_memtime());
+      }
       // phase 1: buffer 0 (tile kt) B0, B1, A0; tile kt + 1's A0, A1 -> buffer 1
       read_b(0, 0, fb0);
       read_b(0, 1, fb1);
@@ -334,6 +362,9 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 #undef G8_SYNC_MMA2
   } else
   for (int kt = 0;; kt += 2) {
+    if constexpr (ST) {
+      if (stw) g8_stamp(blockIdx.x, strow, sti++, __builtin_amdgcn_s_memtime());
+    }
     // phases 1-4: tile kt in buffer 0
     read_b(0, 0, fb0);
     read_a(0, 0);
@@ -377,6 +408,9 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   }
 #undef G8_SYNC_MMA
   if (!(V & 2) && wr == 0) __builtin_amdgcn_s_barrier();  // match the stagger barrier
+  if constexpr (ST) {
+    if (stw) g8_stamp(blockIdx.x, strow, G8_NST - 3, __builtin_amdgcn_s_memtime());
+  }
 
   // ---- epilogue: lane holds C[m][n .. n+3] per block
   const float alpha = alpha_f * (alpha_t ? alpha_t[0] : 1.f);
@@ -440,6 +474,12 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
         }
     }
   }
+  if constexpr (ST) {
+    if (stw) {
+      g8_stamp(blockIdx.x, strow, G8_NST - 2, __builtin_amdgcn_s_memtime());
+      g8_stamp(blockIdx.x, strow, G8_NST - 1, __builtin_amdgcn_s_memrealtime());
+    }
+  }
 }
 
 }  // namespace mx
@@ -483,6 +523,15 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
       if (acc) G8_L(AK, BK_, false, true); else G8_L(AK, BK_, false, false); \
     }                                                          \
   } while (0)
+  if (const char* st = getenv("MXLLM_GEMM8_STAMPS")) {  // diagnostic stamped build, NN bf16 beta 0
+    if (a_kc && !b_kc && !out_f32 && !acc && grid <= 1024 && *st) {
+      if (atoi(st) == 4)
+        gemm8_kernel<true, false, false, false, 4, 4><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f);
+      else
+        gemm8_kernel<true, false, false, false, 4, 8><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f);
+      return (int)hipGetLastError();
+    }
+  }
   if (const char* ab = getenv("MXLLM_GEMM8_ABLATE")) {  // timing-only variants, NN bf16 beta 0 (results wrong)
     const int v = atoi(ab);
     if (a_kc && !b_kc && !out_f32 && !acc && v >= 1 && v <= 3) {
@@ -506,4 +555,10 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
 #undef G8_OUT
 #undef G8_L
   return (int)hipGetLastError();
+}
+
+// copy the diagnostic stamps out (host buffer of 1024 * 2 * 80 uint64)
+extern "C" int mx_gemm8_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g8_stamps), sizeof(unsigned long long) * 1024 * 2 * G8_NST, 0,
+                                  hipMemcpyDeviceToHost);
 }
