@@ -406,6 +406,21 @@ def memory_guard(a, env) -> dict | None:
     return {"min_free_hbm_gb": round(free, 1), "need_gb": round(need, 1), "checkpointed_layers": n}
 
 
+def _gemm_desc(tuned: bool) -> str:
+    """Which GEMM implementations the step may use (mxllm/ops/gemm.py dispatch)."""
+    from mxllm.ops import gemm
+
+    lib = "hipBLASLt/rocBLAS" + (" (tuned solution table)" if tuned else "")
+    if gemm.deterministic():
+        return "gemm8 (8-phase MFMA HIP kernel) for every shape it takes, DETERMINISTIC mode; " + lib + " otherwise"
+    pol = gemm._policy()
+    if pol == "0":
+        return lib
+    if pol == "all":
+        return "gemm8 (8-phase MFMA HIP kernel) wherever it takes the shape; " + lib + " otherwise"
+    return f"{lib} + gemm8 (8-phase MFMA HIP kernel) on the {len(gemm._table())} measured-win shapes"
+
+
 def run(a, env) -> dict:
     """Build the trainer, run W warm-up + K timed steps, return the JSON dict."""
     from mxllm.models import Llama, get_config
@@ -544,7 +559,7 @@ def run(a, env) -> dict:
                 ", per-layer updates overlapped with the next forward" if getattr(trainer, "overlap_optimizer", False)
                 else ""),
             "grad_reduce_dtype": gd,
-            "gemm": "hipBLASLt/rocBLAS" + (" (tuned solution table)" if tuned else ""),
+            "gemm": _gemm_desc(tuned),
         },
         "tokens_per_sec_per_gpu": round(tps / env.world_size, 2),
         "model_tflops_per_gpu": round(tps * flops_tok / env.world_size / 1e12, 1),

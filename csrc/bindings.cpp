@@ -406,9 +406,11 @@ void embedding_bwd_sorted(const at::Tensor& dy, const at::Tensor& sid, const at:
                dy.numel() == sid.numel() * dy.size(-1) && out.device() == dy.device(),
            "embedding_bwd_sorted: out [V, H] f32/bf16 contiguous, dy [T, H] contiguous");
   DevGuard g(dy.device());
-  MX_OK(mx_embedding_bwd_sorted(bf(dy), sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), sid.numel(),
-                                (int)out.size(1), out.size(0), out.data_ptr(), out.scalar_type() == at::kFloat ? 1 : 0,
-                                cur_stream()));
+  const int64_t T = sid.numel(), nch = (T + 63) / 64;
+  auto ws = at::empty({std::max<int64_t>(1, 2 * nch * out.size(1))}, dy.options().dtype(at::kFloat));
+  MX_OK(mx_embedding_bwd_sorted(bf(dy), sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), T, (int)out.size(1),
+                                out.size(0), out.data_ptr(), out.scalar_type() == at::kFloat ? 1 : 0,
+                                ws.data_ptr<float>(), cur_stream()));
 }
 
 // ---------------------------------------------------------------- cross-entropy

@@ -45,7 +45,7 @@ int mx_join_master(const uint16_t* hi, const int16_t* lo, float* x, int64_t n, h
 int mx_embedding_fwd(const int64_t* ids, const uint16_t* w, uint16_t* out, int64_t T, int H, int64_t V,
                      hipStream_t stream);
 int mx_embedding_bwd_sorted(const uint16_t* dy, const int64_t* sid, const int64_t* perm, int64_t T, int H,
-                            int64_t V, void* out, int out_f32, hipStream_t stream);
+                            int64_t V, void* out, int out_f32, float* ws, hipStream_t stream);
 int mx_embedding_bwd(const int64_t* ids, const uint16_t* dy, float* dw, int64_t T, int H, int64_t V,
                      hipStream_t stream);
 // cross_entropy.hip

@@ -184,39 +184,99 @@ __global__ void __launch_bounds__(256) embedding_bwd_kernel(const int64_t* __res
 }
 
 // Sparse, deterministic embedding backward into the parameter's own gradient buffer:
-// sid = the batch's token ids sorted (stable), perm = their positions.  A workgroup per
-// segment START (first position of each distinct id) sums that id's dy rows in sorted
-// order in fp32 and adds the sum into row sid[i] of `out` (fp32, or bf16 with one
-// rounding) -- only the rows the batch touched are read or written, instead of
-// zero-filling and casting a full [V, H] fp32 accumulator.  Grid-stride over positions.
+// sid = the batch's token ids sorted (stable), perm = their positions.  Only the rows the
+// batch touched are read or written (no zero-filled full [V, H] accumulator).
+//
+// The sorted positions are cut into fixed chunks of EB_CH rows, one workgroup each (grid-stride),
+// so a dominant id (pad / EOS in packed batches: thousands of rows of one segment) is spread over
+// many workgroups instead of one walking it serially.  Inside a chunk each run of one
+// id is summed in sorted order in fp32; a run wholly inside its chunk is added to `out` directly
+// (fp32, or bf16 with one rounding); a run that continues into a neighbouring chunk writes an fp32
+// partial (slot 0: it continues from the previous chunk; slot 1: it starts here and continues),
+// and embedding_bwd_combine_kernel adds each such segment's partials in chunk order -- a fixed
+// order, so the result is still bit-reproducible.
+constexpr int EB_CH = 64;
+
+template <bool F32>
+__device__ __forceinline__ void eb_add_row(void* __restrict__ out, int64_t row, int H, int c, const float (&acc)[8]) {
+  if constexpr (F32) {
+    float* o = reinterpret_cast<float*>(out) + row * H + c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += acc[e];
+  } else {
+    uint16_t* o = reinterpret_cast<uint16_t*>(out) + row * H + c;
+    u16x8 cur = *reinterpret_cast<const u16x8*>(o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cur[e] = f2bf(bf2f(cur[e]) + acc[e]);
+    *reinterpret_cast<u16x8*>(o) = cur;
+  }
+}
+
 template <bool F32>
 __global__ void __launch_bounds__(256) embedding_bwd_sorted_kernel(const uint16_t* __restrict__ dy,
                                                                    const int64_t* __restrict__ sid,
                                                                    const int64_t* __restrict__ perm, int64_t T,
-                                                                   int H, int64_t V, void* __restrict__ out) {
-  for (int64_t i = blockIdx.x; i < T; i += gridDim.x) {
-    const int64_t row = sid[i];
-    if ((i > 0 && sid[i - 1] == row) || row < 0 || row >= V) continue;  // workgroup-uniform
-    int64_t end = i + 1;
-    while (end < T && sid[end] == row) ++end;
+                                                                   int H, int64_t V, void* __restrict__ out,
+                                                                   float* __restrict__ ws) {
+  const int64_t nch = (T + EB_CH - 1) / EB_CH;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const int64_t p0 = ch * EB_CH, p1 = min(T, p0 + EB_CH);
+    for (int64_t r0 = p0; r0 < p1;) {  // runs of one id (workgroup-uniform control flow)
+      const int64_t row = sid[r0];
+      int64_t r1 = r0 + 1;
+      while (r1 < p1 && sid[r1] == row) ++r1;
+      const bool from_prev = r0 == p0 && p0 > 0 && sid[p0 - 1] == row;
+      const bool to_next = r1 == p1 && p1 < T && sid[p1] == row;
+      if (row >= 0 && row < V) {
+        for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
+          float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          for (int64_t j = r0; j < r1; ++j) {
+            const u16x8 v = *reinterpret_cast<const u16x8*>(dy + perm[j] * H + c);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+          }
+          if (!from_prev && !to_next) {
+            eb_add_row<F32>(out, row, H, c, acc);
+          } else {
+            float* w = ws + (ch * 2 + (from_prev ? 0 : 1)) * (int64_t)H + c;
+            *reinterpret_cast<float4*>(w) = float4{acc[0], acc[1], acc[2], acc[3]};
+            *reinterpret_cast<float4*>(w + 4) = float4{acc[4], acc[5], acc[6], acc[7]};
+          }
+        }
+      }
+      r0 = r1;
+    }
+  }
+}
+
+// one workgroup per chunk: the chunk where a chunk-crossing segment STARTS sums its slot-1 partial
+// and the following chunks' slot-0 partials in chunk order, then adds the sum into `out` once
+template <bool F32>
+__global__ void __launch_bounds__(256) embedding_bwd_combine_kernel(const int64_t* __restrict__ sid, int64_t T,
+                                                                    int H, int64_t V, void* __restrict__ out,
+                                                                    const float* __restrict__ ws) {
+  const int64_t nch = (T + EB_CH - 1) / EB_CH;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const int64_t p0 = ch * EB_CH, p1 = min(T, p0 + EB_CH);
+    if (p1 >= T) continue;
+    const int64_t row = sid[p1 - 1];
+    if (sid[p1] != row || row < 0 || row >= V) continue;  // last run does not continue
+    int64_t r0 = p1 - 1;
+    while (r0 > p0 && sid[r0 - 1] == row) --r0;
+    if (r0 == p0 && p0 > 0 && sid[p0 - 1] == row) continue;  // the segment started in an earlier chunk
     for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int64_t j = i; j < end; ++j) {
-        const u16x8 v = *reinterpret_cast<const u16x8*>(dy + perm[j] * H + c);
+      float acc[8];
+      const float* w = ws + (ch * 2 + 1) * (int64_t)H + c;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+      for (int e = 0; e < 8; ++e) acc[e] = w[e];
+      for (int64_t k = ch + 1; k < nch; ++k) {
+        const float* w0 = ws + (k * 2) * (int64_t)H + c;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += w0[e];
+        const int64_t q1 = min(T, (k + 1) * EB_CH);
+        if (!(q1 < T && sid[q1] == row)) break;  // the segment ends inside chunk k
       }
-      if constexpr (F32) {
-        float* o = reinterpret_cast<float*>(out) + row * H + c;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += acc[e];
-      } else {
-        uint16_t* o = reinterpret_cast<uint16_t*>(out) + row * H + c;
-        u16x8 cur = *reinterpret_cast<const u16x8*>(o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cur[e] = f2bf(bf2f(cur[e]) + acc[e]);
-        *reinterpret_cast<u16x8*>(o) = cur;
-      }
+      eb_add_row<F32>(out, row, H, c, acc);
     }
   }
 }
@@ -225,15 +285,20 @@ __global__ void __launch_bounds__(256) embedding_bwd_sorted_kernel(const uint16_
 
 using namespace mx;
 
+// ws: 2 * ceil(T / 64) * H floats (partials of chunk-crossing segments; never read before written)
 extern "C" int mx_embedding_bwd_sorted(const uint16_t* dy, const int64_t* sid, const int64_t* perm, int64_t T, int H,
-                                       int64_t V, void* out, int out_f32, hipStream_t stream) {
+                                       int64_t V, void* out, int out_f32, float* ws, hipStream_t stream) {
   if (T <= 0) return 0;
   if (H % 8) return -1;
-  const unsigned grid = (unsigned)(T < 8192 ? T : 8192);
-  if (out_f32)
-    embedding_bwd_sorted_kernel<true><<<grid, 256, 0, stream>>>(dy, sid, perm, T, H, V, out);
-  else
-    embedding_bwd_sorted_kernel<false><<<grid, 256, 0, stream>>>(dy, sid, perm, T, H, V, out);
+  const int64_t nch = (T + EB_CH - 1) / EB_CH;
+  const unsigned grid = (unsigned)(nch < 8192 ? nch : 8192);
+  if (out_f32) {
+    embedding_bwd_sorted_kernel<true><<<grid, 256, 0, stream>>>(dy, sid, perm, T, H, V, out, ws);
+    embedding_bwd_combine_kernel<true><<<grid, 256, 0, stream>>>(sid, T, H, V, out, ws);
+  } else {
+    embedding_bwd_sorted_kernel<false><<<grid, 256, 0, stream>>>(dy, sid, perm, T, H, V, out, ws);
+    embedding_bwd_combine_kernel<false><<<grid, 256, 0, stream>>>(sid, T, H, V, out, ws);
+  }
   return (int)hipGetLastError();
 }
 
