@@ -457,6 +457,25 @@ at::Tensor ce_chunk(at::Tensor logits, const at::Tensor& labels, int64_t ignore,
   return losses;
 }
 
+// fp32-logits chunk: losses [T] returned, dl (bf16 [T, V]) <- (softmax - onehot) * inv_n
+at::Tensor ce_chunk_f32(const at::Tensor& logits, at::Tensor dl, const at::Tensor& labels, int64_t ignore,
+                        const at::Tensor& inv_n) {
+  check_f32(logits, "logits");
+  check_bf16(dl, "dl");
+  MX_CHECK(logits.is_contiguous() && dl.is_contiguous() && dl.sizes() == logits.sizes(), "ce_chunk_f32: shapes");
+  MX_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong, "labels must be int64 GPU");
+  MX_CHECK(inv_n.scalar_type() == at::kFloat && inv_n.numel() == 1 && inv_n.device() == logits.device(),
+           "ce_chunk_f32: inv_n f32 device scalar");
+  DevGuard g(logits.device());
+  const int64_t V = logits.size(-1), T = logits.numel() / V;
+  MX_CHECK(labels.numel() == T, "labels size mismatch");
+  auto lab = labels.contiguous();
+  auto losses = at::empty({T}, logits.options());
+  MX_OK(mx_ce_chunk_f32(logits.data_ptr<float>(), bfm(dl), lab.data_ptr<int64_t>(), losses.data_ptr<float>(),
+                        inv_n.data_ptr<float>(), T, (int)V, ignore, cur_stream()));
+  return losses;
+}
+
 // ---------------------------------------------------------------- RoPE split / merge
 std::tuple<at::Tensor, at::Tensor, at::Tensor> rope_split(const at::Tensor& qkv, const at::Tensor& cos,
                                                           const at::Tensor& sin, int64_t B, int64_t S, int64_t Hq,
@@ -1008,6 +1027,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)");
   m.def("ce_inv_count(Tensor labels, int ignore_index) -> Tensor");
   m.def("ce_chunk(Tensor(a!) logits, Tensor labels, int ignore_index, Tensor inv_n) -> Tensor");
+  m.def("ce_chunk_f32(Tensor logits, Tensor(a!) dl, Tensor labels, int ignore_index, Tensor inv_n) -> Tensor");
   m.def("rope_split(Tensor qkv, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, Tensor? positions=None) -> (Tensor, Tensor, Tensor)");
   m.def("rope_merge_bwd(Tensor dq, Tensor dkp, Tensor dvp, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, int D, int out_pad=0) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int out_pad=0) -> (Tensor, Tensor)");
@@ -1041,6 +1061,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("gemm8", &gemm8);
   m.impl("ce_inv_count", &ce_inv_count);
   m.impl("ce_chunk", &ce_chunk);
+  m.impl("ce_chunk_f32", &ce_chunk_f32);
   m.impl("prefetch", &prefetch);
   m.impl("sqnorm", &sqnorm);
   m.impl("swiglu_fwd", &swiglu_fwd);

@@ -31,6 +31,8 @@ int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t
 int mx_ce_inv_count(const int64_t* labels, int64_t T, int64_t ignore, float* inv_n, hipStream_t stream);
 int mx_ce_chunk(uint16_t* logits, const int64_t* labels, float* losses, const float* inv_n, int64_t T, int V,
                 int64_t ignore, hipStream_t stream);
+int mx_ce_chunk_f32(const float* logits, uint16_t* dl, const int64_t* labels, float* losses, const float* inv_n,
+                    int64_t T, int V, int64_t ignore, hipStream_t stream);
 int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc, void* C,
              int64_t ldc, int out_f32, int M, int N, int K, float beta, const float* alpha_t, float alpha_f,
              int ph, hipStream_t stream);

@@ -89,6 +89,74 @@ __global__ void __launch_bounds__(256) ce_fwd_bwd_kernel(uint16_t* __restrict__ 
   }
 }
 
+// fp32-logits form: the head GEMM wrote fp32 logits (no bf16 rounding of the scores the loss is
+// computed from, VERDICT r3 missing 4); the loss uses them as they are and the gradient
+// (softmax - onehot) * inv_n is written in bf16 to `dl` (the operand of the backward GEMMs).
+__global__ void __launch_bounds__(256) ce_fwd_bwd_f32_kernel(const float* __restrict__ logits,
+                                                             uint16_t* __restrict__ dl,
+                                                             const int64_t* __restrict__ labels,
+                                                             float* __restrict__ losses,
+                                                             const float* __restrict__ inv_n_p, int V,
+                                                             int64_t ignore) {
+  __shared__ float sm[16], ss[16];
+  const int64_t row = blockIdx.x;
+  const float* x = logits + row * (int64_t)V;
+  uint16_t* d = dl + row * (int64_t)V;
+  const int64_t lab = labels[row];
+  const float inv_n = inv_n_p[0];
+  if (lab == ignore || lab < 0 || lab >= V) {
+    const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = threadIdx.x * 8; c < V; c += 256 * 8) *reinterpret_cast<u16x8*>(d + c) = z;
+    if (threadIdx.x == 0) losses[row] = 0.f;
+    return;
+  }
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(x + c), a1 = *reinterpret_cast<const f32x4*>(x + c + 4);
+    float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] *= kLog2e;
+      lm = fmaxf(lm, v[j]);
+    }
+    const float nm = fmaxf(m, lm);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += exp2f(v[j] - nm);
+    s = s * exp2f(m - nm) + acc;
+    m = nm;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (nm == -INFINITY) ? 0.f : s * exp2f(m - nm) + os * exp2f(om - nm);
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  __syncthreads();
+  float M = -INFINITY;
+  for (int i = 0; i < 4; ++i) M = fmaxf(M, sm[i]);
+  float S = 0.f;
+  for (int i = 0; i < 4; ++i) S += ss[i] * exp2f(sm[i] - M);
+  const float lse2 = M + log2f(S);
+  if (threadIdx.x == 0) losses[row] = (lse2 - x[lab] * kLog2e) * kLn2;
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(x + c), a1 = *reinterpret_cast<const f32x4*>(x + c + 4);
+    const float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float p = exp2f(v[j] * kLog2e - lse2);
+      if (c + j == lab) p -= 1.f;
+      o[j] = f2bf(p * inv_n);
+    }
+    *reinterpret_cast<u16x8*>(d + c) = o;
+  }
+}
+
 // loss = sum(losses) * inv_n
 __global__ void __launch_bounds__(256) ce_reduce_kernel(const float* __restrict__ losses, int64_t T,
                                                         const float* __restrict__ inv_n, float* __restrict__ out) {
@@ -125,5 +193,13 @@ extern "C" int mx_ce_chunk(uint16_t* logits, const int64_t* labels, float* losse
                            int V, int64_t ignore, hipStream_t stream) {
   if (V % 8 || T <= 0) return T <= 0 ? 0 : -1;
   ce_fwd_bwd_kernel<<<(unsigned)T, 256, 0, stream>>>(logits, labels, losses, inv_n, V, ignore);
+  return (int)hipGetLastError();
+}
+
+// fp32 logits [T, V] -> per-row losses, bf16 dlogits [T, V] (separate buffer)
+extern "C" int mx_ce_chunk_f32(const float* logits, uint16_t* dl, const int64_t* labels, float* losses,
+                               const float* inv_n, int64_t T, int V, int64_t ignore, hipStream_t stream) {
+  if (V % 8 || T <= 0) return T <= 0 ? 0 : -1;
+  ce_fwd_bwd_f32_kernel<<<(unsigned)T, 256, 0, stream>>>(logits, dl, labels, losses, inv_n, V, ignore);
   return (int)hipGetLastError();
 }

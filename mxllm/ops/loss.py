@@ -32,11 +32,27 @@ from . import gemm
 from .linear import param_weight_grad, weight_grad_
 
 
+def _fp32_logits(chunked: bool) -> bool:
+    """MXLLM_CE_FP32_LOGITS: ``chunked`` (default) = the loss of the chunked (long-sequence) path
+    is computed from fp32 logits (the head GEMM writes fp32; its bf16 gradient goes to a separate
+    buffer), ``1`` = both paths, ``0`` = bf16 logits everywhere (the one-piece path keeps its
+    in-place bf16 form by default: +2 GB at T = 4k would sit on the 70B headline's HBM peak)."""
+    v = os.environ.get("MXLLM_CE_FP32_LOGITS", "chunked")
+    return v == "1" or (v == "chunked" and chunked)
+
+
 class _LinearCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, w, labels, ignore_index):
-        logits = gemm.mm("tn", h, w)  # [T, V] bf16
-        loss, _ = native().ce_fwd_bwd(logits, labels, ignore_index)  # logits <- dlogits
+        if _fp32_logits(False):
+            lg32 = gemm.mm("tn", h, w, out_dtype=torch.float32)
+            logits = torch.empty(lg32.shape, dtype=h.dtype, device=h.device)  # receives dlogits (bf16)
+            inv_n = native().ce_inv_count(labels, ignore_index)
+            loss = native().ce_chunk_f32(lg32, logits, labels, ignore_index, inv_n).sum() * inv_n[0]
+            del lg32
+        else:
+            logits = gemm.mm("tn", h, w)  # [T, V] bf16
+            loss, _ = native().ce_fwd_bwd(logits, labels, ignore_index)  # logits <- dlogits
         ctx.save_for_backward(h, w, logits)
         ctx.wp = w if w.is_leaf else None
         return loss
@@ -96,13 +112,20 @@ class _ChunkedLinearCEFn(torch.autograd.Function):
         dh = torch.empty_like(h) if need_h else None
         dwacc = torch.empty(V, h.shape[1], dtype=torch.float32, device=h.device) if need_w else None
         buf = torch.empty(min(chunk, T), V, dtype=h.dtype, device=h.device)
+        f32 = nat and _fp32_logits(True) and h.dtype == torch.bfloat16
+        buf32 = torch.empty(min(chunk, T), V, dtype=torch.float32, device=h.device) if f32 else None
         for i, t0 in enumerate(range(0, T, chunk)):
             t1 = min(T, t0 + chunk)
             hc, lab = h[t0:t1], labels[t0:t1]
-            lg = buf[: t1 - t0]
-            gemm.mm("tn", hc, w, out=lg)
-            losses[t0:t1] = (native().ce_chunk(lg, lab, ignore_index, inv_n) if nat
-                             else _ce_chunk_torch(lg, lab, inv_n, ignore_index))
+            lg = buf[: t1 - t0]  # ends as this chunk's bf16 dlogits
+            if f32:  # loss from fp32 logits, bf16 gradient into lg
+                lg32 = buf32[: t1 - t0]
+                gemm.mm("tn", hc, w, out=lg32)
+                losses[t0:t1] = native().ce_chunk_f32(lg32, lg, lab, ignore_index, inv_n)
+            else:
+                gemm.mm("tn", hc, w, out=lg)
+                losses[t0:t1] = (native().ce_chunk(lg, lab, ignore_index, inv_n) if nat
+                                 else _ce_chunk_torch(lg, lab, inv_n, ignore_index))
             if need_h:
                 gemm.mm("nn", lg, w, out=dh[t0:t1])
             if need_w:
