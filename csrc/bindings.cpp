@@ -165,33 +165,6 @@ at::Tensor transpose2d(const at::Tensor& in, const c10::optional<at::Tensor>& sc
   return out;
 }
 
-// out = beta * out + alpha * dy^T x over the token rows (csrc/kernels/dw_gemm.hip), both operands
-// token-major bf16 [T, *] row-strided views, out fp32 or bf16 [M, N] row-strided; alpha = the
-// optional f32 device scalar `scale`.  Returns false (nothing launched) for shapes the kernel does
-// not take.
-bool dw_gemm(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, double beta,
-             const c10::optional<at::Tensor>& scale) {
-  MX_CHECK(dy.is_cuda() && x.is_cuda() && out.is_cuda(), "dw_gemm: GPU tensors");
-  MX_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "dw_gemm: bf16 operands");
-  MX_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "dw_gemm: fp32 / bf16 output");
-  MX_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2 && dy.size(0) == x.size(0), "dw_gemm: [T, M], [T, N]");
-  MX_CHECK(out.size(0) == dy.size(1) && out.size(1) == x.size(1), "dw_gemm: out must be [M, N]");
-  if (dy.stride(1) != 1 || x.stride(1) != 1 || out.stride(1) != 1) return false;
-  const float* sc = nullptr;
-  if (scale.has_value()) {
-    MX_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->device() == dy.device(),
-             "dw_gemm scale: f32 scalar on the device");
-    sc = scale->data_ptr<float>();
-  }
-  DevGuard g(dy.device());
-  const int rc = mx_dw_gemm(bf(dy), dy.stride(0), bf(x), x.stride(0), out.data_ptr(), out.stride(0),
-                            out.scalar_type() == at::kFloat ? 1 : 0, (int)dy.size(1), (int)x.size(1),
-                            (int)dy.size(0), (float)beta, sc, 1.f, cur_stream());
-  if (rc == -1) return false;
-  MX_OK(rc);
-  return true;
-}
-
 // out[M, N] = beta * out + alpha * op(a) op(b) on the 8-phase MFMA GEMM (csrc/kernels/gemm8.hip).
 // a: [M, K] when a_kc (k-contiguous) else [K, M]; b: [N, K] when b_kc else [K, N]; all row-strided
 // bf16 views, out fp32 or bf16; alpha = alpha_f * (the optional f32 device scalar alpha_t).
@@ -1010,7 +983,6 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("segmented_mean(Tensor codes, Tensor offsets) -> Tensor");
   m.def("copy2d_batched(Tensor desc, int total_blocks) -> ()");
   m.def("transpose2d(Tensor x, Tensor? scale=None) -> Tensor");
-  m.def("dw_gemm(Tensor dy, Tensor x, Tensor(a!) out, float beta, Tensor? scale=None) -> bool");
   m.def("gemm8(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, float beta, Tensor? alpha_t=None, float alpha=1.0, int ph=8) -> bool");
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
@@ -1057,7 +1029,6 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("segmented_mean", &segmented_mean);
   m.impl("copy2d_batched", &copy2d_batched);
   m.impl("transpose2d", &transpose2d);
-  m.impl("dw_gemm", &dw_gemm);
   m.impl("gemm8", &gemm8);
   m.impl("ce_inv_count", &ce_inv_count);
   m.impl("ce_chunk", &ce_chunk);

@@ -239,12 +239,6 @@ def transpose2d(t: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Ten
 _DW_TN = os.environ.get("MXLLM_DW_TN", "1") != "0"
 
 
-def _dw_kernel_on() -> bool:
-    """Hand-written dW GEMM on token-major operands (no transposes).  Read per call so one
-    process can A/B it (bench/adamw_overlap_ab.py)."""
-    return os.environ.get("MXLLM_DW_KERNEL", "0") == "1"
-
-
 def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, beta: float = 1.0,
                  dy_scale: torch.Tensor | None = None) -> torch.Tensor:
     """dW = dy^T x (reduction over the token dimension), accumulated into
@@ -268,13 +262,6 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, be
             sc = None if dy_scale is None else dy_scale.reshape(1).float()
             return gemm.mm("tt", dy, x, out=out, beta=beta if out is not None else 0.0, alpha_t=sc,
                            out_dtype=odt)
-    if _dw_kernel_on() and use_native(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
-        # token-major operands straight into the MFMA kernel (csrc/kernels/dw_gemm.hip): the
-        # transposes happen in its LDS reads; False = shape not taken -> the path below
-        tgt = out if out is not None else torch.empty(dy.shape[1], x.shape[1], dtype=dy.dtype, device=dy.device)
-        sc = None if dy_scale is None else dy_scale.reshape(1).float()
-        if native().dw_gemm(dy, x, tgt, float(beta) if out is not None else 0.0, sc):
-            return tgt
     if _DW_TN and use_native(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
         xt = transpose2d(x)
         dyt = transpose2d(dy, None if dy_scale is None else dy_scale.reshape(1).float())

@@ -682,37 +682,6 @@ def test_embedding_backward_tied_is_deterministic(gpu):
     assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
 
 
-@pytest.mark.parametrize("T,M,N,ldpad,f32,beta,scaled", [
-    (64, 256, 256, 0, False, 0.0, False),
-    (192, 512, 768, 64, True, 1.0, True),
-    (4096, 1024, 512, 0, True, 0.0, False),
-    (320, 768, 256, 8, False, 1.0, True),
-])
-@pytest.mark.parametrize("form", ["dbuf", "ring", "w8"])
-def test_dw_gemm_token_major(gpu, T, M, N, ldpad, f32, beta, scaled, form, monkeypatch):
-    """csrc/kernels/dw_gemm.hip: out = beta out + s dy^T x on token-major operands (row-strided views,
-    fp32 / bf16 output) vs an fp32 PyTorch reference; both pipeline forms (MXLLM_DW_GEMM)."""
-    monkeypatch.setenv("MXLLM_DW_GEMM", form)
-    torch.manual_seed(0)
-    dyb = torch.randn(T, M + ldpad, device=gpu, dtype=torch.bfloat16)
-    xb = torch.randn(T, N + ldpad, device=gpu, dtype=torch.bfloat16)
-    dy, x = dyb[:, :M], xb[:, :N]
-    out = torch.randn(M, N, device=gpu, dtype=torch.float32 if f32 else torch.bfloat16)
-    out0 = out.clone()
-    s = torch.tensor([0.37], device=gpu) if scaled else None
-    assert _ops().dw_gemm(dy, x, out, beta, s)
-    refv = (s.item() if scaled else 1.0) * (dy.float().t() @ x.float()) + beta * out0.float()
-    assert rel_err(out, refv) < (2e-6 if f32 else 4e-3), rel_err(out, refv)
-
-
-def test_dw_gemm_declines_untiled_shapes(gpu):
-    dy = torch.randn(64, 320, device=gpu, dtype=torch.bfloat16)
-    x = torch.randn(64, 256, device=gpu, dtype=torch.bfloat16)
-    out = torch.zeros(320, 256, device=gpu, dtype=torch.bfloat16)
-    assert not _ops().dw_gemm(dy, x, out, 0.0, None)
-    assert not _ops().dw_gemm(dy[:48], x[:48], out, 0.0, None)  # T not a multiple of 64
-
-
 def test_chunked_lm_head_ce_matches_unchunked_gpu(gpu):
     """Long-sequence LM head + CE walked in token chunks (ce_inv_count + ce_chunk_f32 kernels: the
     loss from fp32 logits, dh / dW formed per chunk) vs the one-piece fused path (bf16 logits) and an
