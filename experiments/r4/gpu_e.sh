@@ -12,3 +12,5 @@ cat $OUT/stamps.txt
 cp mxllm/tuning/gemm8_gfx950.json $OUT/gemm8_gfx950.json
 timeout -k 10 600 python -u bench/gemm8_probe.py --aug --ph4 --forms nn,tt,tt32,tn --rounds 3 --write-table $OUT/gemm8_gfx950.json --json-out $OUT/probe.json > $OUT/probe.txt 2>&1 || { echo "probe rc=$?"; exit 1; }
 tail -1 $OUT/probe.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/suite.txt 2>&1
+rc=$?; tail -4 $OUT/suite.txt; echo "gpu suite rc=$rc"

@@ -25,9 +25,10 @@ def _run(gpu, steps: int):
     cfg = get_config("llama3.2-1b")
     torch.manual_seed(0)
     model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=1234)
-    tr = Trainer(model, DistEnv(device=gpu, backend="nccl"), OptimConfig(lr=2e-5, weight_decay=0.01, grad_clip=1.0))
+    tr = Trainer(model, DistEnv(device=gpu, backend="nccl"), OptimConfig(lr=1e-4, weight_decay=0.01, grad_clip=1.0))
     data = SyntheticTokens(cfg.vocab_size, 8, 512, gpu, seed=1)
-    losses = [tr.train_step([data.next()]) for _ in range(steps)]
+    batches = [data.next() for _ in range(4)]  # cycled: random tokens are only learnable by repetition
+    losses = [tr.train_step([batches[i % 4]]) for i in range(steps)]
     torch.cuda.synchronize()
     tr.params_ready()
     out = ([float(x) for x in losses], tr.master_fp32().clone())
