@@ -69,7 +69,7 @@ def schedule(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> int:
     return DEFAULT_PH if (pol == "all" or deterministic()) else 0
 
 
-DEFAULT_PH = int(os.environ.get("MXLLM_GEMM8_DEFAULT_PH", "8"))
+DEFAULT_PH = int(os.environ.get("MXLLM_GEMM8_DEFAULT_PH", "4"))
 
 
 def want(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> bool:
