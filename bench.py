@@ -412,13 +412,13 @@ def _gemm_desc(tuned: bool) -> str:
 
     lib = "hipBLASLt/rocBLAS" + (" (tuned solution table)" if tuned else "")
     if gemm.deterministic():
-        return "gemm8 (8-phase MFMA HIP kernel) for every shape it takes, DETERMINISTIC mode; " + lib + " otherwise"
+        return "gemm8 (hand-written MFMA HIP kernel) for every shape it takes, DETERMINISTIC mode; " + lib + " otherwise"
     pol = gemm._policy()
     if pol == "0":
         return lib
     if pol == "all":
-        return "gemm8 (8-phase MFMA HIP kernel) wherever it takes the shape; " + lib + " otherwise"
-    return f"{lib} + gemm8 (8-phase MFMA HIP kernel) on the {len(gemm._table())} measured-win shapes"
+        return "gemm8 (hand-written MFMA HIP kernel) wherever it takes the shape; " + lib + " otherwise"
+    return f"{lib} + gemm8 (hand-written MFMA HIP kernel) on the {len(gemm._table())} measured-win shapes"
 
 
 def run(a, env) -> dict:

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""8-phase MFMA GEMM (csrc/kernels/gemm8.hip) vs hipBLASLt on the Llama-3.1 training shapes.
+"""gemm8 MFMA GEMM (4- and 8-phase schedules) (csrc/kernels/gemm8.hip) vs hipBLASLt on the Llama-3.1 training shapes.
 
 For every shape the variants run interleaved in ONE process (guide §5.4 rule 24): R rounds, each
 round times every variant (median of `--calls` back-to-back calls after warm-up); reported is the
@@ -30,7 +30,8 @@ from mxllm.ops.linear import transpose2d  # noqa: E402
 
 SHAPES = {
     # name: (out, in) of the projection weight
-    "70b": {"qkv": (10240, 8192), "o": (8192, 8192), "gu": (57344, 8192), "down": (8192, 28672)},
+    "70b": {"qkv": (10240, 8192), "o": (8192, 8192), "gu": (57344, 8192), "down": (8192, 28672),
+            "head": (128256, 8192)},
     "8b": {"qkv": (6144, 4096), "o": (4096, 4096), "gu": (28672, 4096), "down": (4096, 14336),
            "head": (128256, 4096)},
 }
