@@ -82,19 +82,17 @@ def parse(argv=None):
                     help="also measure BASELINE config 4 (70B full fine-tune, ZeRO-3) after the headline; "
                          "auto = when the headline runs on 8 GPUs")
     ap.add_argument("--config4-micro-batch", type=int, default=4)
-    # selective checkpointing: the last 24 of 80 layers keep their activations.  Emulated world-8
-    # step (profiles/r2s3_emul8_ck*.json): all 80 checkpointed 3,559 ms / 191 GB peak; first 56
-    # 3,321 ms / 239 GB; first 48 3,247 ms / 255 GB.  56 leaves ~65 GB for RCCL buffers and the
-    # in-flight gather / reduce-scatter units of the real 8-rank job.
-    ap.add_argument("--config4-act-ckpt-layers", type=int, default=56)
+    # selective checkpointing of the first N of 80 layers (the rest keep their activations).  Emulated
+    # world-8 per-rank step, one box (profiles/r4g/c4_ck*.json): N = 56 3,298 ms / 223.5 GB reserved;
+    # 40: 3,141 ms / 255.2 GB; 24: 2,990 ms / 286.9 GB (~2 GB per checkpointed layer).  Default: the
+    # fewest checkpointed layers (>= 40) whose reserved peak + CONFIG4_MARGIN_GB fits the smallest free
+    # HBM over the ranks (config4_plan).
+    ap.add_argument("--config4-act-ckpt-layers", type=int, default=None)
     ap.add_argument("--config4-model", default="llama3.1-70b", help=argparse.SUPPRESS)  # tests: tiny models
     ap.add_argument("--config4-steps", type=int, default=3)
     ap.add_argument("--config4-warmup", type=int, default=2)
     ap.add_argument("--config4-timeout", type=float, default=360.0,
                     help="hard limit for the config-4 child job; the headline line is printed either way")
-    # per-rank HBM the config-4 child needs: the emulated world-8 peak with the first 56 of 80 layers
-    # checkpointed (239 GB reserved, profiles/r2s3_emul8_ck56.json) + RCCL buffers / in-flight units
-    ap.add_argument("--config4-need-gb", type=float, default=255.0)
     ap.add_argument("--config2", choices=["auto", "on", "off"], default="auto",
                     help="also measure BASELINE config 2 (Llama-3.1-8B FULL fine-tune, DDP) in-process after "
                          "the headline; auto = when the headline runs on 1 GPU")
@@ -228,11 +226,15 @@ def main(argv=None):
     out["child_phases"] = {"headline_ranks_exited_s": released, "min_free_hbm_gb_before": (
         round(free_gb, 1) if free_gb is not None else None)}
     for kind, key in children:
-        if kind == "config4" and free_gb is not None and free_gb < a.config4_need_gb:
-            out[key] = {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < "
-                                   f"{a.config4_need_gb:.0f} GB the config-4 child needs"}
-        elif kind == "config4":
-            out[key] = run_config4(a, env.world_size)
+        if kind == "config4":
+            ck, need = config4_plan(a, free_gb)
+            if ck is None:
+                out[key] = {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < {need:.0f} GB the "
+                                       f"config-4 child needs with every layer checkpointed"}
+            else:
+                out[key] = run_config4(a, env.world_size, ck)
+                out[key]["hbm_plan"] = {"min_free_hbm_gb": None if free_gb is None else round(free_gb, 1),
+                                        "need_gb": round(need, 1), "checkpointed_layers": ck}
         else:
             out[key] = run_config3(a, env.world_size)
     emit(out, a.json_out)
@@ -361,12 +363,35 @@ def run_config3(a, world: int) -> dict:
     return res
 
 
-def run_config4(a, world: int) -> dict:
-    """70B full-parameter ZeRO-3 fine-tune (activation checkpointing) on ``world``
-    GPUs as a child torchrun job; returns its parsed JSON (or the error)."""
+# config 4 per-rank HBM model (70B, micro-batch 4 x 2048, world-8 shards; profiles/r4g/c4_ck*.json):
+# reserved peak = 223.5 GB with the first 56 layers checkpointed, +1.98 GB per layer fewer;
+# margin: RCCL buffers of the two ZeRO-3 communicators + allocator slack of the real 8-rank job
+CONFIG4_RESERVED = (56, 223.5, 1.98)
+CONFIG4_MARGIN_GB = 14.0
+
+
+def config4_plan(a, free_gb: float | None) -> tuple[int | None, float]:
+    """(checkpointed layers, HBM needed) for the config-4 child: ``--config4-act-ckpt-layers``
+    when given, else the fewest of 40 / 48 / 56 / 64 / 80 that fit ``free_gb``; (None, need of
+    80) when even full checkpointing does not fit."""
+    n0, r0, per = CONFIG4_RESERVED
+    need = lambda ck: r0 + (n0 - ck) * per + CONFIG4_MARGIN_GB  # noqa: E731
+    if a.config4_act_ckpt_layers is not None:
+        ck = a.config4_act_ckpt_layers
+        return (ck if free_gb is None or free_gb >= need(ck) else None), need(ck)
+    for ck in (40, 48, 56, 64, 80):
+        if free_gb is None or free_gb >= need(ck):
+            return ck, need(ck)
+    return None, need(80)
+
+
+def run_config4(a, world: int, ckpt_layers: int = 40) -> dict:
+    """70B full-parameter ZeRO-3 fine-tune (activation checkpointing of the first
+    ``ckpt_layers`` layers) on ``world`` GPUs as a child torchrun job; returns its parsed
+    JSON (or the error)."""
     argv = ["--model", a.config4_model, "--finetune", "full", "--parallel", "zero3",
             "--act-ckpt", "--micro-batch", str(a.config4_micro_batch), "--seq-len", str(a.seq_len),
-            "--act-ckpt-layers", str(a.config4_act_ckpt_layers),
+            "--act-ckpt-layers", str(ckpt_layers),
             "--steps", str(a.config4_steps), "--warmup", str(a.config4_warmup)]
     res = _run_child(a, world, argv, a.config4_timeout)
     name = PRETTY.get(a.config4_model, a.config4_model)

@@ -1,6 +1,8 @@
 """Per-step kernel time breakdown from a rocprofv3 kernel trace: the window
 between the last two grad-norm launches (one per optimizer step) -> one step.
-usage: python scripts/step_breakdown.py <run_kernel_trace.csv> [top]"""
+usage: python scripts/step_breakdown.py <run_kernel_trace.csv> [top] [marker]
+marker: kernel-name substring launched once per step (default: the grad-norm kernel; ZeRO-3 runs
+its norm per unit, so use e.g. ``embedding_fwd`` there)."""
 import collections
 import csv
 import sys
@@ -12,6 +14,8 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # one grad-norm kernel per optimizer step (AdamW may be issued as several chunk launches)
     key = "sqnorm_partial" if any("sqnorm_partial" in r["Kernel_Name"] for r in rows) else "adamw_kernel"
+    if len(sys.argv) > 3:
+        key = sys.argv[3]
     marks = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
     a, b = marks[-2], marks[-1]
     win = rows[a + 1:b + 1]

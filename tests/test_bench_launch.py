@@ -119,3 +119,20 @@ def test_memory_guard_checkpoints_only_when_short(monkeypatch):
             assert g["checkpointed_layers"] >= 10 * 1 / 1.7 and a.act_ckpt and a.act_ckpt_layers == g["checkpointed_layers"]
     a = bench.parse([])
     assert bench.memory_guard(a, types.SimpleNamespace(device=torch.device("cuda", 0), world_size=1)) is None
+
+
+def test_config4_plan_fits_free_hbm():
+    """The config-4 child checkpoints the fewest layers whose modelled per-rank peak + margin fits
+    the smallest free HBM over the ranks; an explicit depth is honoured or skipped."""
+    import argparse
+
+    import bench
+
+    a = argparse.Namespace(config4_act_ckpt_layers=None)
+    assert bench.config4_plan(a, 308.0)[0] == 40
+    assert bench.config4_plan(a, 262.0)[0] == 48
+    assert bench.config4_plan(a, 200.0)[0] == 80
+    assert bench.config4_plan(a, 150.0)[0] is None
+    assert bench.config4_plan(a, None)[0] == 40  # CPU rehearsal: no HBM to check
+    a.config4_act_ckpt_layers = 24
+    assert bench.config4_plan(a, 308.0)[0] == 24 and bench.config4_plan(a, 250.0)[0] is None
