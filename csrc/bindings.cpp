@@ -282,6 +282,33 @@ at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu, int64_t out_pa
   return dgu;
 }
 
+// SwiGLU fused with the LoRA tail of its augmented-GEMM neighbour (csrc/kernels/lora.hip):
+// fwd: m [T, F] in a [T, F + pad] buffer, tail = alpha m v^T (v [>= 16 nrb, F] row view);
+// bwd: dgu [T, 2F] in a [T, 2F + pad] buffer, tail = alpha dgu v^T (v [>= 16 nrb, 2F]).
+at::Tensor swiglu_lora(const c10::optional<at::Tensor>& dm, const at::Tensor& gu, int64_t pad, const at::Tensor& v,
+                       int64_t nrb, double alpha) {
+  check_bf16(gu, "gu");
+  const int64_t ldv = check_rows_bf16(v, "v");
+  DevGuard g(gu.device());
+  const bool bwd = dm.has_value();
+  const int64_t F2 = gu.size(-1), F = F2 / 2, T = gu.numel() / F2;
+  MX_CHECK(gu.dim() == 2 && F % 128 == 0 && T % 16 == 0, "swiglu_lora: [T, 2F] with T % 16 == 0, F % 128 == 0");
+  MX_CHECK(nrb >= 1 && nrb <= 4 && pad >= 16 * nrb && pad % 8 == 0, "swiglu_lora: 16 nrb <= pad");
+  MX_CHECK(v.size(0) >= 16 * nrb && v.size(1) == (bwd ? F2 : F), "swiglu_lora: v shape");
+  if (bwd) {
+    check_bf16(*dm, "dm");
+    MX_CHECK(dm->numel() == T * F, "swiglu_lora: dm shape");
+  }
+  const int64_t W = bwd ? F2 : F;
+  at::Tensor out = at::empty({T, W + pad}, gu.options());
+  const int64_t nws = mx_swiglu_lora_ws((int)T, (int)F, (int)nrb);
+  auto ws = at::empty({nws > 0 ? nws : 1}, gu.options().dtype(at::kFloat));
+  if (T > 0)
+    MX_OK(mx_swiglu_lora(bwd ? 1 : 0, bf(gu), bwd ? bf(*dm) : nullptr, bfm(out), W + pad, bf(v), ldv, (int)nrb,
+                         (int)pad, (float)alpha, ws.data_ptr<float>(), (int)T, (int)F, cur_stream()));
+  return out.narrow(1, 0, W);
+}
+
 // ---------------------------------------------------------------- AdamW
 void adamw_step(const c10::optional<at::Tensor>& master, at::Tensor grad, at::Tensor m, at::Tensor v,
                 const c10::optional<at::Tensor>& lowp, const c10::optional<at::Tensor>& lo, double lr, double b1,
@@ -1018,6 +1045,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
   m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha) -> ()");
+  m.def("swiglu_lora(Tensor? dm, Tensor gu, int pad, Tensor v, int nrb, float alpha) -> Tensor");
   m.def("lora_grads(Tensor x, Tensor dy, Tensor g, Tensor st, Tensor(a!) ga, Tensor(b!) gb, int[] splits, int r, bool accumulate) -> ()");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3) -> (Tensor, Tensor, Tensor)");
@@ -1064,5 +1092,6 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("w8_dequant", &w8_dequant);
   m.impl("quant_rows_e4m3", &quant_rows_e4m3);
   m.impl("lora_xwt", &lora_xwt);
+  m.impl("swiglu_lora", &swiglu_lora);
   m.impl("lora_grads", &lora_grads);
 }

@@ -109,5 +109,8 @@ int64_t mx_lora_xwt_ws(int M, int K);
 int64_t mx_lora_xtg_ws(int ntiles, int T);
 int mx_lora_xwt(const uint16_t* X, int64_t ldx, const uint16_t* V, int64_t ldv, int Vrows, uint16_t* out, int64_t ldo,
                 float* ws, int M, int K, float alpha, hipStream_t stream);
+int64_t mx_swiglu_lora_ws(int T, int F, int nrb);
+int mx_swiglu_lora(int bwd, const uint16_t* gu, const uint16_t* dm, uint16_t* out, int64_t ldo, const uint16_t* V,
+                   int64_t ldv, int nrb, int pad, float alpha, float* ws, int T, int F, hipStream_t stream);
 int mx_lora_xtg(const int64_t* desc, int np, int T, float alpha, int accumulate, float* ws, hipStream_t stream);
 }

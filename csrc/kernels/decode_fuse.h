@@ -8,7 +8,8 @@
 
 namespace mx {
 
-__device__ __forceinline__ float dfuse_silu(float x) { return x / (1.f + __expf(-x)); }
+// the same expression as the SwiGLU kernels (elementwise.hip sigmoid_f): bit-identical outputs
+__device__ __forceinline__ float dfuse_silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 struct SkNorm {
   const uint16_t* delta;  // [M, K] sub-block output added to the residual (nullptr: plain RMSNorm)

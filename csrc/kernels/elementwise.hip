@@ -10,7 +10,9 @@
 
 namespace mx {
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+// sigmoid by the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division sequence;
+// csrc/kernels/lora.hip swiglu_lora_kernel uses the identical expressions (bitwise-equal outputs)
+__device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // m[t, c] = silu(gu[t, c]) * gu[t, F + c]
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ m,
@@ -25,7 +27,10 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restr
     u16x8 u = *reinterpret_cast<const u16x8*>(row + F + c);
     u16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(silu_f(bf2f(g[j])) * bf2f(u[j]));
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]);
+      o[j] = f2bf(gf * sigmoid_f(gf) * bf2f(u[j]));
+    }
     *reinterpret_cast<u16x8*>(m + t * ldm + c) = o;
   }
 }
@@ -48,7 +53,7 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
-      const float s = 1.f / (1.f + __expf(-gf));
+      const float s = sigmoid_f(gf);
       og[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
       ou[j] = f2bf(df * gf * s);
     }

@@ -584,9 +584,179 @@ __global__ void __launch_bounds__(256) lora_xtg_reduce_kernel(const XtgArgs a, c
   }
 }
 
+// ------------------------------------------------------------------ SwiGLU + LoRA tail
+// The SwiGLU pass that also produces the rank-r LoRA product of its own output for the
+// neighbouring augmented GEMM, so that product no longer re-streams the [T, F] / [T, 2F]
+// tensor through lora_xwt (70B: 235 MB per layer forward, 470 MB backward):
+//   FWD: m = silu(g) u            -> out[:, :F];   tail = s m . V^T   (V = A of the down projection, [*, F])
+//   BWD: dg, du (swiglu_bwd math) -> out[:, :2F];  tail = s [dg | du] . V^T   (V = B^T of gate-up, [*, 2F])
+// grid (T/16, CS), 256 threads.  A workgroup owns 16 token rows and a contiguous range of
+// 128-column tiles of F.  Per tile every thread moves 16 B per operand (row tid >> 4, chunk
+// tid & 15: 256-B row segments, the same coalescing as the plain SwiGLU kernels), writes the
+// bf16 result to global AND to a double-buffered LDS image, and after ONE barrier the 4 waves
+// read that image back as MFMA A-fragments (wave w: columns 32 w .. 32 w + 31 of the tile;
+// BWD: of the dg and the du image) against V fragments straight from L2 (16 rank rows x 64 B).
+// The next tile's operands are loaded before this tile's math, after this tile's V loads, so
+// the MFMA's counted wait never drains the prefetch.  Per-wave 16 x 16 NRB fp32 accumulators
+// -> LDS -> one partial per (split, row block) in ws; swiglu_lora_reduce_kernel sums the CS
+// partials in split order (bit-reproducible), scales by s and writes the whole pad (zeros past
+// 16 NRB columns).  The elementwise math is bitwise that of swiglu_fwd_kernel /
+// swiglu_bwd_kernel (csrc/kernels/elementwise.hip).
+constexpr int kSlRow = 136;  // LDS image row stride (elements): 272 B -> conflict-free b128 fragment reads
+
+__device__ __forceinline__ float sl_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
+template <bool BWD, int NRB>
+__global__ void __launch_bounds__(256) swiglu_lora_kernel(const uint16_t* __restrict__ gu,
+                                                          const uint16_t* __restrict__ dm, uint16_t* __restrict__ out,
+                                                          int64_t ldo, const uint16_t* __restrict__ V, int64_t ldv,
+                                                          float* __restrict__ ws, int F, int CS) {
+  constexpr int NP = BWD ? 2 : 1;  // LDS images per tile (BWD: dg, du)
+  constexpr int NC = 16 * NRB;
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][NP][16 * kSlRow];
+  __shared__ __attribute__((aligned(16))) float red[4][16][NC + 4];
+  const int rb = blockIdx.x, split = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, r = lane & 15, gq = lane >> 4;
+  const int row = tid >> 4, ch = tid & 15;
+  const int tiles = F >> 7;
+  const int t0 = (int)((int64_t)split * tiles / CS), t1 = (int)((int64_t)(split + 1) * tiles / CS);
+  const int64_t tok = (int64_t)rb * 16 + row;
+  const uint16_t* grow = gu + tok * (2 * (int64_t)F) + 8 * ch;
+  const uint16_t* drow = dm + tok * (int64_t)F + 8 * ch;  // BWD only
+  uint16_t* orow = out + tok * ldo + 8 * ch;
+  const uint16_t* vrow = V + (int64_t)r * ldv + 32 * w + 8 * gq;
+  const int wofs = row * kSlRow + 8 * ch, rofs = r * kSlRow + 32 * w + 8 * gq;
+
+  f32x4 acc[NRB];
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u16x8 g, u, d, vf[NP][NRB];
+  auto vload = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int b = 0; b < NRB; ++b)
+        vf[p][b] = *reinterpret_cast<const u16x8*>(vrow + (int64_t)(16 * b) * ldv + p * F + (t << 7));
+  };
+  if (t0 < t1) {
+    g = *reinterpret_cast<const u16x8*>(grow + (t0 << 7));
+    u = *reinterpret_cast<const u16x8*>(grow + F + (t0 << 7));
+    if (BWD) d = *reinterpret_cast<const u16x8*>(drow + (t0 << 7));
+    vload(t0);
+  }
+  for (int t = t0; t < t1; ++t) {
+    const int c = t << 7, buf = (t - t0) & 1;
+    u16x8 gn, un, dn;
+    const int cn = (t + 1 < t1 ? t + 1 : t) << 7;  // the last trip reloads its own tile (no branch)
+    gn = *reinterpret_cast<const u16x8*>(grow + cn);
+    un = *reinterpret_cast<const u16x8*>(grow + F + cn);
+    if (BWD) dn = *reinterpret_cast<const u16x8*>(drow + cn);
+    u16x8 o0, o1;
+    if (!BWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gf = bf2f(g[j]);
+        o0[j] = f2bf(gf * sl_sigmoid(gf) * bf2f(u[j]));
+      }
+      *reinterpret_cast<u16x8*>(orow + c) = o0;
+      *reinterpret_cast<u16x8*>(&img[buf][0][wofs]) = o0;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+        const float s = sl_sigmoid(gf);
+        o0[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
+        o1[j] = f2bf(df * gf * s);
+      }
+      *reinterpret_cast<u16x8*>(orow + c) = o0;
+      *reinterpret_cast<u16x8*>(orow + F + c) = o1;
+      *reinterpret_cast<u16x8*>(&img[buf][0][wofs]) = o0;
+      *reinterpret_cast<u16x8*>(&img[buf][NP - 1][wofs]) = o1;
+    }
+    __syncthreads();  // the image is complete; the other buffer's readers (trip t-1) are past it
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const u16x8 a = *reinterpret_cast<const u16x8*>(&img[buf][p][rofs]);
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) acc[b] = lmfma(a, vf[p][b], acc[b]);
+    }
+    vload(t + 1 < t1 ? t + 1 : t);  // next tile's V fragments (L2) under this tile's tail and the next math
+    g = gn, u = un;
+    if (BWD) d = dn;
+  }
+  // 4 waves -> one 16 x NC partial (fixed wave order)
+#pragma unroll
+  for (int b = 0; b < NRB; ++b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[w][4 * gq + e][16 * b + r] = acc[b][e];
+  __syncthreads();
+  float* wp = ws + ((int64_t)split * gridDim.x + rb) * (16 * NC);
+  for (int i = tid; i < 16 * NC; i += 256) {
+    const int rr = i / NC, cc = i % NC;
+    wp[i] = ((red[0][rr][cc] + red[1][rr][cc]) + red[2][rr][cc]) + red[3][rr][cc];
+  }
+}
+
+// ws[CS][T/16][16][NC] -> tail[:, 0:pad] = bf16(alpha * sum over splits), zeros past NC; grid T/16
+__global__ void __launch_bounds__(256) swiglu_lora_reduce_kernel(const float* __restrict__ ws, int CS, int NC, int pad,
+                                                                 uint16_t* __restrict__ tail, int64_t ldo, float alpha) {
+  const int rb = blockIdx.x, nrb = gridDim.x;
+  for (int i = threadIdx.x; i < 16 * pad; i += 256) {
+    const int rr = i / pad, cc = i % pad;
+    float v = 0.f;
+    if (cc < NC)
+      for (int sp = 0; sp < CS; ++sp) v += ws[(((int64_t)sp * nrb + rb) * 16 + rr) * NC + cc];
+    tail[((int64_t)rb * 16 + rr) * ldo + cc] = f2bf(alpha * v);
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
+
+static int lora_env(const char* name, int dflt);
+
+static int swiglu_lora_splits(int T, int F) {
+  const int tiles = F / 128, rbs = T / 16;
+  int cs = lora_env("MXLLM_SWIGLU_LORA_CS", 0);
+  if (cs <= 0) cs = (512 + rbs - 1) / rbs;  // ~512 workgroups (T 4096: 2 splits; measured best of 1-16, r4h)
+  cs = cs < 1 ? 1 : cs;
+  cs = cs > tiles ? tiles : cs;
+  return cs > 32 ? 32 : cs;
+}
+
+extern "C" int64_t mx_swiglu_lora_ws(int T, int F, int nrb) {
+  if (T <= 0 || F < 128) return 0;
+  return (int64_t)swiglu_lora_splits(T, F) * T * 16 * nrb;
+}
+
+// bwd = 0: out[T, F (+pad)] = swiglu(gu), tail out[:, F:F+pad] = alpha m V^T (V [>= 16 nrb, F]);
+// bwd = 1: out[T, 2F (+pad)] = swiglu_bwd(dm, gu), tail out[:, 2F:2F+pad] = alpha dgu V^T (V [.., 2F]).
+// T % 16 == 0, F % 128 == 0, 1 <= nrb <= 4, 16 nrb <= pad, 16-B aligned rows.
+extern "C" int mx_swiglu_lora(int bwd, const uint16_t* gu, const uint16_t* dm, uint16_t* out, int64_t ldo,
+                              const uint16_t* V, int64_t ldv, int nrb, int pad, float alpha, float* ws, int T, int F,
+                              hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (T % 16 || F % 128 || nrb < 1 || nrb > 4 || pad < 16 * nrb || pad % 8 || ldo % 8 || ldv % 8 ||
+      ldo < (bwd ? 2 * (int64_t)F : F) + pad || ((uintptr_t)gu | (uintptr_t)out | (uintptr_t)V) % 16 ||
+      (bwd && (!dm || (uintptr_t)dm % 16)))
+    return (int)hipErrorInvalidValue;
+  const int CS = swiglu_lora_splits(T, F);
+  const dim3 grid(T / 16, CS);
+#define MX_SL(B, N) swiglu_lora_kernel<B, N><<<grid, 256, 0, stream>>>(gu, dm, out, ldo, V, ldv, ws, F, CS)
+  if (bwd) {
+    switch (nrb) { case 1: MX_SL(true, 1); break; case 2: MX_SL(true, 2); break;
+                   case 3: MX_SL(true, 3); break; default: MX_SL(true, 4); break; }
+  } else {
+    switch (nrb) { case 1: MX_SL(false, 1); break; case 2: MX_SL(false, 2); break;
+                   case 3: MX_SL(false, 3); break; default: MX_SL(false, 4); break; }
+  }
+#undef MX_SL
+  swiglu_lora_reduce_kernel<<<T / 16, 256, 0, stream>>>(ws, CS, 16 * nrb, pad, out + (bwd ? 2 * (int64_t)F : F), ldo,
+                                                        alpha);
+  return (int)hipGetLastError();
+}
 
 // split count of the ordered split reduction: ~512 workgroups, >= 2 blocks per wave
 static int lora_env(const char* name, int dflt) {

@@ -135,12 +135,20 @@ class FusedLinear(nn.Module):
                 self.sync_adapter_()
                 self.refresh_images_()
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def tail_operands(self):
+        """((A rows [pad, in], R, s), (B^T rows [pad, N], R, s)): the k-contiguous operands of the
+        forward / backward rank-r tails, for producers that write them (fused SwiGLU)."""
+        R = self.lora_a.shape[0]
+        amat = self.wa if self.transposed else self.wbuf[sum(self.splits):, :self.in_features]
+        return (amat, R, self.scaling), (self.wbt, R, self.scaling)
+
+    def forward(self, x: torch.Tensor, x_tail: bool = False, dy_tail: bool = False) -> torch.Tensor:
         if self.lora_r > 0:
             if self.augmented():
                 return ops.lora_linear_aug(x, self.lora_a, self.lora_b, self.wbuf, self.splits, self.scaling,
                                            self.pad, self.wbt, getattr(self, "wxt", None),
-                                           getattr(self, "wa", None) if self.transposed else None)
+                                           getattr(self, "wa", None) if self.transposed else None,
+                                           x_tail=x_tail, dy_tail=dy_tail)
             return ops.lora_linear(x, self.weight, self.lora_a, self.lora_b, self.splits, self.scaling)
         return ops.linear(x, self.weight)
 
@@ -248,13 +256,29 @@ class Llama(nn.Module):
         a = layer.wo(o)
         x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps, out_pad=self._pad(layer.wgu),
                                 grad_pad=self._pad(layer.wo))
-        m = ops.swiglu(layer.wgu(x), out_pad=self._pad(layer.wd), grad_pad=self._pad(layer.wgu))
-        d = layer.wd(m)
+        tf, tb = self._swiglu_tails(layer, x)
+        m = ops.swiglu(layer.wgu(x, dy_tail=tb is not None), out_pad=self._pad(layer.wd),
+                       grad_pad=self._pad(layer.wgu), tail_fwd=tf, tail_bwd=tb)
+        d = layer.wd(m, x_tail=tf is not None)
         last = i + 1 == len(self.layers)
         nxt = self.final_norm if last else self.layers[i + 1].attn_norm
         x, h = ops.add_rms_norm(d, h, nxt, cfg.norm_eps, out_pad=0 if last else self._pad(self.layers[i + 1].wqkv),
                                 grad_pad=self._pad(layer.wd))
         return x, h
+
+    def _swiglu_tails(self, layer, x: torch.Tensor):
+        """LoRA tails the SwiGLU pass writes itself: the down projection's s m A^T (forward)
+        and the gate-up projection's s dgu B (backward) -- None where the fused kernel does
+        not take the shape (mxllm/ops/activation.py)."""
+        if x.dim() != 2:
+            return None, None
+        T, F2 = x.shape[0], 2 * self.cfg.ffn
+        tf = tb = None
+        if layer.wd.augmented() and ops.lora_tail_ok(x, T, F2, layer.wd.pad, layer.wd.lora_a.shape[0]):
+            tf = layer.wd.tail_operands()[0]
+        if layer.wgu.augmented() and ops.lora_tail_ok(x, T, F2, layer.wgu.pad, layer.wgu.lora_a.shape[0]):
+            tb = layer.wgu.tail_operands()[1]
+        return tf, tb
 
     def _wait_groups(self):
         """Parameter groups in first-use order: embedding (+ first norm), layer i

@@ -138,24 +138,27 @@ class _LoRAAugFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt, wxt=None, wa=None):
+    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt, wxt=None, wa=None, x_tail=False, dy_tail=False):
         tr = wa is not None  # transposed buffer [[W^T, A^T], [B^T, 0]] (FusedLinear ``transposed``)
         if tr:
             K, N = wbuf.shape[0] - pad, wbuf.shape[1] - pad
         else:
             N, K = wbuf.shape[0] - pad, wbuf.shape[1] - pad
         x2 = x.reshape(-1, K)
-        xa = _augment(x2, pad)
         nat = _lora_native(x2, N, K, splits, r, wbt)
-        amat = wa if tr else wbuf[N:, :K]  # A rows [pad, K] (zero rows past n*r), k-contiguous
-        if nat:
-            native().lora_xwt(x2, amat, xa[:, K:], scaling)  # s t, zero in the pad columns
-        else:
-            xa[:, K:].addmm_(x2, amat.t(), beta=0.0, alpha=scaling)
+        xa = _padded_rows(x2, pad) if x_tail else None
+        if xa is None:  # ``x_tail``: the producer (SwiGLU) already wrote s x A^T into the pad columns
+            xa = _augment(x2, pad)
+            amat = wa if tr else wbuf[N:, :K]  # A rows [pad, K] (zero rows past n*r), k-contiguous
+            if nat:
+                native().lora_xwt(x2, amat, xa[:, K:], scaling)  # s t, zero in the pad columns
+            else:
+                xa[:, K:].addmm_(x2, amat.t(), beta=0.0, alpha=scaling)
         y = gemm.mm("nn", xa, wbuf[:, :N]) if tr else gemm.mm("tn", xa, wbuf[:N, :])
         ctx.save_for_backward(xa, wbuf)
         ctx.lora_a, ctx.lora_b, ctx.wbt, ctx.wxt = a, b, wbt, wxt
         ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat, tr)
+        ctx.dy_tail = dy_tail
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -164,12 +167,14 @@ class _LoRAAugFn(torch.autograd.Function):
         N, K, s, splits, r, pad, xshape, nat, tr = ctx.dims
         R = r * len(splits)
         dy2 = dy.reshape(-1, N)
-        dya = _augment(dy2, pad)
-        if nat:
-            native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s)  # g = s dy B, zero in the pad columns
-        else:
-            bmat = wbuf[K:, :N].t() if tr else wbuf[:N, K:]  # B [N, pad]
-            dya[:, N:].addmm_(dy2, bmat, beta=0.0, alpha=s)
+        dya = _padded_rows(dy2, pad) if ctx.dy_tail else None
+        if dya is None:  # ``dy_tail``: the SwiGLU backward already wrote s dy B into the pad columns
+            dya = _augment(dy2, pad)
+            if nat:
+                native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s)  # g = s dy B, zero in the pad columns
+            else:
+                bmat = wbuf[K:, :N].t() if tr else wbuf[:N, K:]  # B [N, pad]
+                dya[:, N:].addmm_(dy2, bmat, beta=0.0, alpha=s)
         g = dya[:, N:N + R]
         x2, st = xa[:, :K], xa[:, K:K + R]
         da = db = None
@@ -211,17 +216,21 @@ class _LoRAAugFn(torch.autograd.Function):
             dx = gemm.mm("tn", dya, ctx.wxt)
         else:  # the n-contiguous weight itself ("NN": gemm8 where it wins, csrc/kernels/gemm8.hip)
             dx = gemm.mm("nn", dya, wbuf[:, :K])
-        return dx.view(xshape), da, db, None, None, None, None, None, None, None, None
+        return dx.view(xshape), da, db, None, None, None, None, None, None, None, None, None, None
 
 
 def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: torch.Tensor, splits: Sequence[int],
                     scaling: float, pad: int, wbt: torch.Tensor | None = None,
-                    wxt: torch.Tensor | None = None, wa: torch.Tensor | None = None) -> torch.Tensor:
+                    wxt: torch.Tensor | None = None, wa: torch.Tensor | None = None,
+                    x_tail: bool = False, dy_tail: bool = False) -> torch.Tensor:
     """LoRA projection through the augmented weight buffer (see _LoRAAugFn);
     ``wxt``: optional [K, N+pad] transposed image of wbuf[:, :K] for dX;
-    ``wa``: given for a TRANSPOSED buffer [[W^T, A^T], [B^T, 0]] (A rows, k-contiguous)."""
+    ``wa``: given for a TRANSPOSED buffer [[W^T, A^T], [B^T, 0]] (A rows, k-contiguous);
+    ``x_tail`` / ``dy_tail``: the producer of x (forward) / of the output gradient (backward)
+    writes the rank-r tail itself (mxllm/ops/activation.py fused SwiGLU); used whenever the
+    tensor arrives in its padded buffer, recomputed otherwise."""
     r = a.shape[0] // len(splits)
-    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt, wa)
+    return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt, wa, bool(x_tail), bool(dy_tail))
 
 
 def transpose2d(t: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:

@@ -66,6 +66,33 @@ def test_swiglu(gpu, T, F):
     assert rel_err(dgu, guf.grad) < 1e-2
 
 
+@pytest.mark.parametrize("bwd", [False, True])
+@pytest.mark.parametrize("T,F,R", [(16, 128, 16), (48, 384, 32), (1024, 1536, 48), (256, 256, 64), (4096, 28672, 16)])
+def test_swiglu_lora_tail(gpu, T, F, R, bwd):
+    """SwiGLU fused with the neighbour's LoRA tail (csrc/kernels/lora.hip swiglu_lora_kernel):
+    the SwiGLU output is bitwise the plain kernel's, the tail is s out V[:R]^T against fp32,
+    zeros past R (V rows past R deliberately non-zero), bit-reproducible."""
+    from mxllm.ops.linear import _padded_rows
+
+    torch.manual_seed(4)
+    pad, s = 64, 2.0
+    gu = torch.randn(T, 2 * F, device=gpu, dtype=torch.bfloat16)
+    W = 2 * F if bwd else F
+    V = torch.randn(pad, W + 24, device=gpu, dtype=torch.bfloat16)[:, :W]  # padded row stride
+    dm = torch.randn(T, F, device=gpu, dtype=torch.bfloat16) if bwd else None
+    out = _ops().swiglu_lora(dm, gu, pad, V, R // 16, s)
+    plain = _ops().swiglu_bwd(dm, gu) if bwd else _ops().swiglu_fwd(gu)
+    assert torch.equal(out, plain)
+    full = _padded_rows(out, pad)
+    assert full is not None
+    tail = full[:, W:]
+    ref_tail = s * (out.float() @ V[:R].float().t())
+    assert rel_err(tail[:, :R], ref_tail) < 1e-2
+    assert not tail[:, R:].any()
+    again = _padded_rows(_ops().swiglu_lora(dm, gu, pad, V, R // 16, s), pad)
+    assert torch.equal(again[:, W:], tail)
+
+
 @pytest.mark.parametrize("T,V", [(5, 1000), (256, 128256)])
 def test_cross_entropy(gpu, T, V):
     torch.manual_seed(3)

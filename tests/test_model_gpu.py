@@ -402,6 +402,52 @@ def test_engine_fp8_graphed_decode_b16_close_to_bf16(gpu, small_m, monkeypatch):
     assert cos.min().item() > 0.99, cos
 
 
+def test_lora_fused_swiglu_tails_match_unfused(gpu, monkeypatch):
+    """The SwiGLU pass writing the down projection's forward tail and the gate-up projection's
+    backward tail (no lora_xwt over m / dgu) gives the loss and every adapter gradient of the
+    unfused path, and removes exactly those two lora_xwt calls per layer."""
+    import importlib
+
+    from mxllm.models import Llama, get_config
+
+    A = importlib.import_module("mxllm.ops.activation")
+    Lin = importlib.import_module("mxllm.ops.linear")  # (the mxllm.ops attributes are the functions)
+
+    cfg = get_config("tiny-d128").replace(n_layers=2)
+
+    class Spy:
+        def __init__(self, real):
+            self.real, self.xwt = real, 0
+
+        def __getattr__(self, k):
+            if k == "lora_xwt":
+                self.xwt += 1
+            return getattr(self.real, k)
+
+    def run(flag):
+        monkeypatch.setattr(A, "_FUSE_TAIL", flag)
+        spy = Spy(Lin.native())
+        monkeypatch.setattr(Lin, "native", lambda: spy)
+        m = Llama(cfg, device=gpu, lora_r=16, seed=3)
+        with torch.no_grad():
+            g = torch.Generator(device=gpu).manual_seed(0)
+            for n, p in m.named_parameters():
+                p.copy_(torch.randn(p.shape, device=gpu, generator=g).to(p.dtype) * 0.02)
+        m.sync_adapters_()
+        m.refresh_images_()
+        ids = torch.randint(0, cfg.vocab_size, (2, 128), device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
+        loss = m(ids, ids)
+        loss.backward()
+        return float(loss), {n: p.grad.float() for n, p in m.named_parameters() if p.requires_grad}, spy.xwt
+
+    l0, g0, n0 = run(False)
+    l1, g1, n1 = run(True)
+    assert n0 - n1 == 2 * cfg.n_layers, (n0, n1)
+    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0)), (l0, l1)
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 2e-2, k
+
+
 def test_lora_transposed_buffers_match_gpu(gpu, monkeypatch):
     """LoRA projections with TRANSPOSED augmented buffers (forward NN, dX TN GEMM,
     A kept as a k-contiguous copy for the HIP rank-r kernel) give the same loss and

@@ -128,6 +128,75 @@ def test_lora_augmented_gemm_matches_two_gemm_form():
     assert float(lin.lora_b.grad[:40, 4:].abs().max()) == 0.0
 
 
+def test_lora_producer_written_tails_are_used():
+    """``x_tail`` / ``dy_tail`` (the fused SwiGLU writes the LoRA tails): a padded x / dy whose
+    pad columns already hold s x A^T / s dy B gives the same output and gradients as the
+    recomputed tails; a wrong tail changes them (so it really is read, not recomputed); an
+    unpadded tensor falls back to recomputing."""
+    from mxllm.models.llama import FusedLinear
+
+    torch.manual_seed(1)
+    lin = FusedLinear(48, [40, 24], dtype=torch.float32, device="cpu", lora_r=4, lora_alpha=8.0, train_base=False)
+    lin.reset_parameters(0.05, None)
+    with torch.no_grad():
+        for blk in lin.lora_b_blocks():
+            blk.normal_(0, 0.1)
+    lin.sync_adapter_()
+    (amat, R, s), (bt, _, _) = lin.tail_operands()
+    pad, K, N = lin.pad, 48, 64
+    x0 = torch.randn(10, K)
+    dy0 = torch.randn(10, N)
+
+    class Produce(torch.autograd.Function):
+        """identity whose output / gradient live in padded buffers with producer-written tails"""
+        @staticmethod
+        def forward(ctx, x, bad):
+            ctx.bad = bad
+            buf = torch.empty(x.shape[0], K + pad)
+            buf[:, :K] = x
+            buf[:, K:] = s * x @ amat.t() + (1.0 if bad == "x" else 0.0)
+            return buf[:, :K]
+
+        @staticmethod
+        def backward(ctx, g):
+            return g, None
+
+    class GradPad(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, y, bad):
+            ctx.bad = bad
+            return y.view_as(y)
+
+        @staticmethod
+        def backward(ctx, g):
+            buf = torch.empty(g.shape[0], N + pad)
+            buf[:, :N] = g
+            buf[:, N:] = s * g @ bt.t() + (1.0 if ctx.bad == "dy" else 0.0)
+            return buf[:, :N], None
+
+    def run(bad=None, fused=True):
+        lin.lora_a.grad = lin.lora_b.grad = None
+        x = x0.clone().requires_grad_(True)
+        xin = Produce.apply(x, bad) if fused else x
+        y = lin(xin, x_tail=fused, dy_tail=fused)
+        y = GradPad.apply(y, bad) if fused else y
+        y.backward(dy0)
+        return y.detach(), x.grad, lin.lora_a.grad.clone(), lin.lora_b.grad.clone()
+
+    want = run(fused=False)
+    for g, w in zip(run(), want):
+        torch.testing.assert_close(g, w, rtol=1e-5, atol=1e-5)
+    assert not torch.allclose(run("x")[0], want[0])
+    assert not torch.allclose(run("dy")[2], want[2])
+    # flags set but the tensors arrive unpadded: tails recomputed, same result
+    x = x0.clone().requires_grad_(True)
+    lin.lora_a.grad = lin.lora_b.grad = None
+    y = lin(x, x_tail=True, dy_tail=True)
+    y.backward(dy0)
+    torch.testing.assert_close(y.detach(), want[0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(lin.lora_a.grad, want[2], rtol=1e-5, atol=1e-5)
+
+
 def test_fp8_weight_quantization_roundtrip():
     """Serving-time e4m3 weight quantisation (mxllm/serve/quant.py): per-channel
     scales, no zero / subnormal codes (the HIP decoder relies on it), the
