@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """LoRA rank-r kernels (csrc/kernels/lora.hip) at the Llama-3.1-70B headline shapes: achieved HBM
-bandwidth of ``lora_xwt`` (s x A^T / s dy B tails) and ``lora_grads`` (dA and every dB_i in one
-launch) per projection, for several workgroup targets (MXLLM_LORA_WGS, read per launch).
+bandwidth of ``lora_xwt`` (s x A^T / s dy B tails: the row-tiled kernel on the adapter rows vs the
+64-row LDS-DMA kernel on all padded rows) and ``lora_grads`` (dA and every dB_i in one launch) per
+projection, the latter for several workgroup targets (MXLLM_LORA_WGS, read per launch).
 
 Usage: python bench/lora_probe.py [--tokens 4096] [--wgs 256,512,1024] [--rounds 5]
 """
@@ -39,7 +40,7 @@ def time_us(fn, calls):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=4096)
-    ap.add_argument("--wgs", default="256,512,1024")
+    ap.add_argument("--wgs", default="128,256")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--json-out", default=None)
@@ -58,24 +59,41 @@ def main():
         ga = torch.empty(R, K, device=dev, dtype=torch.bfloat16)
         gb = torch.zeros(N, R, device=dev, dtype=torch.bfloat16)
         x, dy = xa[:, :K], dya[:, :N]
-        cases = {
-            "xwt_x": (lambda: ops.lora_xwt(x, A, xa[:, K:], s), T * K * 2),
-            "xwt_dy": (lambda: ops.lora_xwt(dy, Bt, dya[:, N:], s), T * N * 2),
-            "grads": (lambda: ops.lora_grads(x, dy, dya[:, N:], xa[:, K:], ga, gb, splits, r, True), T * (K + N) * 2),
-        }
-        for cname, (fn, nbytes) in cases.items():
-            res = {w: [] for w in wgs}
+        def xwt(mode, X, V, tail):
+            def f():
+                if mode == "lds":
+                    os.environ["MXLLM_LORA_XWT"] = "lds"
+                    ops.lora_xwt(X, V, tail, s)
+                else:
+                    os.environ["MXLLM_LORA_XWT"] = "tile"
+                    ops.lora_xwt(X, V, tail, s, R)
+            return f
+
+        for cname, X, V, tail, nbytes in (("xwt_x", x, A, xa[:, K:], T * K * 2), ("xwt_dy", dy, Bt, dya[:, N:], T * N * 2)):
+            res = {"lds": [], "tile": []}
             for _ in range(a.rounds):
-                for w in wgs:
-                    os.environ["MXLLM_LORA_WGS"] = str(w)
-                    res[w].append(time_us(fn, a.calls))
-            os.environ.pop("MXLLM_LORA_WGS", None)
-            rec = {"case": f"70b {name} {cname} T{T}", "gb": round(nbytes / 1e9, 3)}
-            for w, v in res.items():
+                for m in res:
+                    res[m].append(time_us(xwt(m, X, V, tail), a.calls))
+            os.environ.pop("MXLLM_LORA_XWT", None)
+            rec = {"case": f"70b {name} {cname} T{T} R{R}", "gb": round(nbytes / 1e9, 3)}
+            for m, v in res.items():
                 us = statistics.median(v)
-                rec[f"wgs{w}"] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
+                rec[m] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
             print(json.dumps(rec), flush=True)
             out.append(rec)
+        fn, nbytes = (lambda: ops.lora_grads(x, dy, dya[:, N:], xa[:, K:], ga, gb, splits, r, True)), T * (K + N) * 2
+        res = {w: [] for w in wgs}
+        for _ in range(a.rounds):
+            for w in wgs:
+                os.environ["MXLLM_LORA_WGS"] = str(w)
+                res[w].append(time_us(fn, a.calls))
+        os.environ.pop("MXLLM_LORA_WGS", None)
+        rec = {"case": f"70b {name} grads T{T}", "gb": round(nbytes / 1e9, 3)}
+        for w, v in res.items():
+            us = statistics.median(v)
+            rec[f"wgs{w}"] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
         del xa, dya, A, Bt, ga, gb
         torch.cuda.empty_cache()
     if a.json_out:

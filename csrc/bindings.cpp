@@ -949,16 +949,19 @@ at::Tensor w8_dequant(const at::Tensor& q, const at::Tensor& scale) {
 // ---------------------------------------------------------------- LoRA rank-r GEMMs
 // out[:, 0:Vrows] = alpha * x . v^T (x [M, K], v [Vrows, K] row views, Vrows % 64 == 0):
 // the forward s x A^T / backward s dy B products written into the augmented-GEMM tails.
-void lora_xwt(const at::Tensor& x, const at::Tensor& v, at::Tensor& out, double alpha) {
+// rows > 0: only v's first `rows` rows are non-zero (the adapter; the rest is padding).
+void lora_xwt(const at::Tensor& x, const at::Tensor& v, at::Tensor& out, double alpha, int64_t rows) {
   const int64_t ldx = check_rows_bf16(x, "x"), ldv = check_rows_bf16(v, "v"), ldo = check_rows_bf16(out, "out");
   const int64_t M = x.size(0), K = x.size(1), Vr = v.size(0);
   MX_CHECK(v.size(1) == K && out.size(0) == M && out.size(1) >= Vr, "lora_xwt shapes");
-  MX_CHECK(M % 64 == 0 && K % 64 == 0 && Vr % 64 == 0 && ldo % 4 == 0, "lora_xwt: M, K, rows(v) must be multiples of 64");
+  MX_CHECK(rows >= 0 && rows <= Vr, "lora_xwt: rows <= rows(v)");
+  MX_CHECK(M % 16 == 0 && K % 64 == 0 && Vr % 64 == 0 && ldo % 4 == 0,
+           "lora_xwt: M % 16, K % 64, rows(v) % 64");
   DevGuard g(x.device());
-  const int64_t nws = mx_lora_xwt_ws((int)M, (int)K);
+  const int64_t nws = mx_lora_xwt_ws((int)M, (int)K, (int)rows);
   auto ws = at::empty({nws > 0 ? nws : 1}, x.options().dtype(at::kFloat));
   MX_OK(mx_lora_xwt(bf(x), ldx, bf(v), ldv, (int)Vr, bfm(out), ldo, ws.data_ptr<float>(), (int)M, (int)K, (float)alpha,
-                    cur_stream()));
+                    (int)rows, cur_stream()));
 }
 
 // LoRA adapter gradients in ONE launch: ga [R, K] (+)= g^T x and the diagonal blocks
@@ -1044,7 +1047,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("skinny_norm_linear(Tensor h, Tensor? delta, Tensor gamma, float eps, Tensor w, bool swiglu) -> (Tensor, Tensor)");
   m.def("w8_dequant(Tensor q, Tensor scale) -> Tensor");
   m.def("quant_rows_e4m3(Tensor x) -> (Tensor, Tensor)");
-  m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha) -> ()");
+  m.def("lora_xwt(Tensor x, Tensor v, Tensor(a!) out, float alpha, int rows=0) -> ()");
   m.def("swiglu_lora(Tensor? dm, Tensor gu, int pad, Tensor v, int nrb, float alpha) -> Tensor");
   m.def("lora_grads(Tensor x, Tensor dy, Tensor g, Tensor st, Tensor(a!) ga, Tensor(b!) gb, int[] splits, int r, bool accumulate) -> ()");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");

@@ -105,10 +105,10 @@ int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, const float*
                   int M, int N, int K, hipStream_t stream);
 int mx_w8_dequant(const uint8_t* q, const float* scale, uint16_t* w, int64_t N, int K, hipStream_t stream);
 int mx_quant_rows_e4m3(const uint16_t* x, int64_t ldx, uint8_t* q, float* s, int64_t M, int K, hipStream_t stream);
-int64_t mx_lora_xwt_ws(int M, int K);
+int64_t mx_lora_xwt_ws(int M, int K, int rows);
 int64_t mx_lora_xtg_ws(int ntiles, int T);
 int mx_lora_xwt(const uint16_t* X, int64_t ldx, const uint16_t* V, int64_t ldv, int Vrows, uint16_t* out, int64_t ldo,
-                float* ws, int M, int K, float alpha, hipStream_t stream);
+                float* ws, int M, int K, float alpha, int rows, hipStream_t stream);
 int64_t mx_swiglu_lora_ws(int T, int F, int nrb);
 int mx_swiglu_lora(int bwd, const uint16_t* gu, const uint16_t* dm, uint16_t* out, int64_t ldo, const uint16_t* V,
                    int64_t ldv, int nrb, int pad, float alpha, float* ws, int T, int F, hipStream_t stream);

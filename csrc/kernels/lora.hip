@@ -711,6 +711,83 @@ __global__ void __launch_bounds__(256) swiglu_lora_reduce_kernel(const float* __
   }
 }
 
+// lora_xwt, row-tiled ("tile") form: out[:, 0:pad] = alpha X V[:16 NRB]^T with the structure of
+// swiglu_lora_kernel minus the elementwise math: a workgroup owns 16 RBW token rows and a range
+// of 128-column tiles; per tile each thread loads RBW 16-B pieces of X (256-B row segments),
+// stores them to a double-buffered LDS image, one barrier, and each wave multiplies its 32-column
+// slice of all RBW row blocks against NRB V fragments from L2 (loaded one tile ahead, SHARED by the
+// RBW row blocks).  Only the 16 NRB rows of V that hold the adapter are read (the LDS-DMA kernels
+// above multiply all 64 padded rows and re-read V once per 64 rows).  Partials ws[CS][T/16][16][NC]
+// -> swiglu_lora_reduce_kernel (fixed split order).  grid (T / (16 RBW), CS), 256 threads.
+template <int NRB, int RBW>
+__global__ void __launch_bounds__(256) lora_xwt_tile_kernel(const uint16_t* __restrict__ X, int64_t ldx,
+                                                            const uint16_t* __restrict__ V, int64_t ldv,
+                                                            float* __restrict__ ws, int K, int CS) {
+  constexpr int NC = 16 * NRB;
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][RBW][16 * kSlRow];
+  __shared__ __attribute__((aligned(16))) float red[4][16][NC + 4];
+  const int rg = blockIdx.x, split = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, r = lane & 15, gq = lane >> 4;
+  const int row = tid >> 4, ch = tid & 15;
+  const int tiles = K >> 7;
+  const int t0 = (int)((int64_t)split * tiles / CS), t1 = (int)((int64_t)(split + 1) * tiles / CS);
+  const uint16_t* xrow = X + ((int64_t)rg * 16 * RBW + row) * ldx + 8 * ch;
+  const int64_t xstep = 16 * ldx;  // next 16-row block
+  const uint16_t* vrow = V + (int64_t)r * ldv + 32 * w + 8 * gq;
+  const int wofs = row * kSlRow + 8 * ch, rofs = r * kSlRow + 32 * w + 8 * gq;
+
+  f32x4 acc[RBW][NRB];
+#pragma unroll
+  for (int i = 0; i < RBW; ++i)
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u16x8 x[RBW], vf[NRB];
+  auto xload = [&](int t, u16x8(&dst)[RBW]) {
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) dst[i] = *reinterpret_cast<const u16x8*>(xrow + i * xstep + (t << 7));
+  };
+  auto vload = [&](int t) {
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) vf[b] = *reinterpret_cast<const u16x8*>(vrow + (int64_t)(16 * b) * ldv + (t << 7));
+  };
+  if (t0 < t1) {
+    xload(t0, x);
+    vload(t0);
+  }
+  for (int t = t0; t < t1; ++t) {
+    const int buf = (t - t0) & 1;
+    u16x8 xn[RBW];
+    xload(t + 1 < t1 ? t + 1 : t, xn);  // the last trip reloads its own tile (no branch)
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) *reinterpret_cast<u16x8*>(&img[buf][i][wofs]) = x[i];
+    __syncthreads();  // image complete; the other buffer's readers (trip t-1) are past it
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      const u16x8 a = *reinterpret_cast<const u16x8*>(&img[buf][i][rofs]);
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) acc[i][b] = lmfma(a, vf[b], acc[i][b]);
+    }
+    vload(t + 1 < t1 ? t + 1 : t);
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) x[i] = xn[i];
+  }
+  // per row block: 4 waves -> one 16 x NC partial (fixed wave order)
+#pragma unroll
+  for (int i = 0; i < RBW; ++i) {
+    __syncthreads();  // red reused per row block
+#pragma unroll
+    for (int b = 0; b < NRB; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[w][4 * gq + e][16 * b + r] = acc[i][b][e];
+    __syncthreads();
+    float* wp = ws + ((int64_t)split * (gridDim.x * RBW) + rg * RBW + i) * (16 * NC);
+    for (int k = tid; k < 16 * NC; k += 256) {
+      const int rr = k / NC, cc = k % NC;
+      wp[k] = ((red[0][rr][cc] + red[1][rr][cc]) + red[2][rr][cc]) + red[3][rr][cc];
+    }
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -764,6 +841,7 @@ static int lora_env(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 static int lora_splits(int tiles, int blocks, int smax) {
+  if (tiles <= 0) return 1;
   const int target = lora_env("MXLLM_LORA_WGS", 256);  // tuning knob: workgroups to aim for
   int S = (target + tiles - 1) / tiles;
   S = S < 1 ? 1 : (S > smax ? smax : S);
@@ -771,28 +849,74 @@ static int lora_splits(int tiles, int blocks, int smax) {
   return S;
 }
 
-// fp32 workspace floats needed by mx_lora_xwt (M, K) / mx_lora_xtg (total 64-col tiles, T)
-extern "C" int64_t mx_lora_xwt_ws(int M, int K) {
-  const int S = lora_splits(M / 64, K / 64, 16);
-  return S > 1 ? (int64_t)S * (M / 64) * 4096 : 0;
+// lora_xwt kernel choice (MXLLM_LORA_XWT, read per call: an in-process A/B can flip it):
+// "lds" (default) = the 64-row LDS-DMA kernel, "reg" = the register-fragment kernel (both on all
+// 64 padded rows of V), "tile" = lora_xwt_tile_kernel (adapter rows only; needs M % 16, K % 128,
+// <= 64 adapter rows, 16-B aligned rows).  The tile kernel measured 3-7 us SLOWER on the 64-84 MB
+// calls of the 70B step (profiles/r4i: those calls are bound by their fixed cost, not by bytes).
+static int xwt_mode() {
+  const char* kv = getenv("MXLLM_LORA_XWT");
+  if (kv && !strcmp(kv, "reg")) return 2;
+  if (kv && !strcmp(kv, "tile")) return 0;
+  return 1;
+}
+static bool xwt_tile_ok(const void* X, int64_t ldx, const void* V, int64_t ldv, int M, int K, int rows) {
+  return xwt_mode() == 0 && M % 16 == 0 && K % 128 == 0 && rows > 0 && rows <= 64 && ldx % 8 == 0 &&
+         ldv % 8 == 0 && (uintptr_t)X % 16 == 0 && (uintptr_t)V % 16 == 0;
+}
+static int xwt_rbw(int M) { return M % 64 == 0 ? 4 : (M % 32 == 0 ? 2 : 1); }
+static int xwt_tile_splits(int M, int K) {
+  const int groups = M / (16 * xwt_rbw(M)), tiles = K / 128;
+  int cs = lora_env("MXLLM_LORA_XWT_CS", 0);
+  if (cs <= 0) cs = (512 + groups - 1) / groups;  // ~512 workgroups
+  cs = cs < 1 ? 1 : cs;
+  return cs > tiles ? tiles : cs;
+}
+
+// fp32 workspace floats needed by mx_lora_xwt (M, K, adapter rows; 0 = all) / mx_lora_xtg (total 64-col tiles, T)
+extern "C" int64_t mx_lora_xwt_ws(int M, int K, int rows) {
+  const int S = M >= 64 && K >= 64 ? lora_splits(M / 64, K / 64, 16) : 1;
+  const int64_t dma = S > 1 ? (int64_t)S * (M / 64) * 4096 : 0;
+  if (rows > 0 && rows <= 64 && M % 16 == 0 && K % 128 == 0 && xwt_mode() == 0) {
+    const int64_t tile = (int64_t)xwt_tile_splits(M, K) * M * 16 * ((rows + 15) / 16);
+    return tile > dma ? tile : dma;
+  }
+  return dma;
 }
 extern "C" int64_t mx_lora_xtg_ws(int ntiles, int T) {
   const int S = lora_splits(ntiles, T / 64, 8);
   return S > 1 ? (int64_t)S * ntiles * 4096 : 0;
 }
 
-// out[:, 0:Vrows] = alpha X V^T, one launch per 64 output columns.
+// out[:, 0:Vrows] = alpha X V^T.  rows > 0: only V's first `rows` rows are non-zero (the adapter;
+// the rest is padding) -> the row-tiled kernel computes those and writes zeros past them.
 extern "C" int mx_lora_xwt(const uint16_t* X, int64_t ldx, const uint16_t* V, int64_t ldv, int Vrows, uint16_t* out,
-                           int64_t ldo, float* ws, int M, int K, float alpha, hipStream_t stream) {
+                           int64_t ldo, float* ws, int M, int K, float alpha, int rows, hipStream_t stream) {
   if (M <= 0) return 0;
+  if (xwt_tile_ok(X, ldx, V, ldv, M, K, rows) && rows <= Vrows && ldo % 4 == 0) {
+    const int nrb = (rows + 15) / 16, rbw = xwt_rbw(M), CS = xwt_tile_splits(M, K);
+    const dim3 grid(M / (16 * rbw), CS);
+#define MX_XT(N, R) lora_xwt_tile_kernel<N, R><<<grid, 256, 0, stream>>>(X, ldx, V, ldv, ws, K, CS)
+#define MX_XT_N(R)                                  \
+  switch (nrb) {                                    \
+    case 1: MX_XT(1, R); break;                     \
+    case 2: MX_XT(2, R); break;                     \
+    case 3: MX_XT(3, R); break;                     \
+    default: MX_XT(4, R); break;                    \
+  }
+    if (rbw == 4) { MX_XT_N(4) } else if (rbw == 2) { MX_XT_N(2) } else { MX_XT_N(1) }
+#undef MX_XT_N
+#undef MX_XT
+    swiglu_lora_reduce_kernel<<<M / 16, 256, 0, stream>>>(ws, CS, 16 * nrb, Vrows, out, ldo, alpha);
+    return (int)hipGetLastError();
+  }
   if (M % 64 || K % 64 || Vrows % 64 || M / 64 > kMaxTiles) return (int)hipErrorInvalidValue;
   const int mtiles = M / 64, S = lora_splits(mtiles, K / 64, 16);
   const int fused = lora_env("MXLLM_LORA_FUSED_RED", 0);
   // LDS-staged kernel (16-B aligned rows required by its 16-B DMA pieces); the
   // register-fragment kernel stays for A/B (MXLLM_LORA_XWT=reg)
-  const char* kv = getenv("MXLLM_LORA_XWT");  // read per call: an in-process A/B can flip it
-  const bool reg = kv && !strcmp(kv, "reg");
-  const bool lds = !reg && ((uintptr_t)X % 16 == 0) && ((uintptr_t)V % 16 == 0) && ldx % 8 == 0 && ldv % 8 == 0;
+  const bool lds = xwt_mode() != 2 && ((uintptr_t)X % 16 == 0) && ((uintptr_t)V % 16 == 0) && ldx % 8 == 0 &&
+                   ldv % 8 == 0;
   for (int c0 = 0; c0 < Vrows; c0 += 64) {
     if (lds)
       lora_xwt_lds_kernel<<<dim3(mtiles, S), 256, 0, stream>>>(X, ldx, V + (int64_t)c0 * ldv, ldv, out + c0, ldo, ws,

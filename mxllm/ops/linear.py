@@ -151,7 +151,7 @@ class _LoRAAugFn(torch.autograd.Function):
             xa = _augment(x2, pad)
             amat = wa if tr else wbuf[N:, :K]  # A rows [pad, K] (zero rows past n*r), k-contiguous
             if nat:
-                native().lora_xwt(x2, amat, xa[:, K:], scaling)  # s t, zero in the pad columns
+                native().lora_xwt(x2, amat, xa[:, K:], scaling, a.shape[0])  # s t, zero in the pad columns
             else:
                 xa[:, K:].addmm_(x2, amat.t(), beta=0.0, alpha=scaling)
         y = gemm.mm("nn", xa, wbuf[:, :N]) if tr else gemm.mm("tn", xa, wbuf[:N, :])
@@ -171,7 +171,7 @@ class _LoRAAugFn(torch.autograd.Function):
         if dya is None:  # ``dy_tail``: the SwiGLU backward already wrote s dy B into the pad columns
             dya = _augment(dy2, pad)
             if nat:
-                native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s)  # g = s dy B, zero in the pad columns
+                native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s, len(splits) * r)  # g = s dy B, zero in the pad columns
             else:
                 bmat = wbuf[K:, :N].t() if tr else wbuf[:N, K:]  # B [N, pad]
                 dya[:, N:].addmm_(dy2, bmat, beta=0.0, alpha=s)

@@ -429,6 +429,30 @@ def test_quant_rows_e4m3(gpu):
     assert rel_err(q.view(torch.float8_e4m3fn).float() * s, xf) < 0.04
 
 
+@pytest.mark.parametrize("rows", [16, 32, 48, 64])
+@pytest.mark.parametrize("T,K", [(16, 128), (48, 384), (96, 1024), (4096, 8192), (4096, 28672), (4096, 10240)])
+def test_lora_xwt_tile(gpu, T, K, rows, monkeypatch):
+    """Row-tiled lora_xwt (MXLLM_LORA_XWT=tile): only the first `rows` rows of V are the adapter ->
+    out[:, :rows] = alpha x V[:rows]^T, zeros in the rest of the 64-column pad (V's padding rows
+    are deliberately non-zero here), columns past the pad untouched, bit-reproducible; row counts
+    that select 1, 2 and 4 row blocks per workgroup."""
+    monkeypatch.setenv("MXLLM_LORA_XWT", "tile")
+    torch.manual_seed(5)
+    pad = 64
+    buf = torch.randn(T, K + pad + 8, device=gpu, dtype=torch.bfloat16)
+    x = buf[:, :K]
+    v = torch.randn(pad, K + 16, device=gpu, dtype=torch.bfloat16)[:, :K]
+    sentinel = buf[:, K + pad:].clone()
+    _ops().lora_xwt(x, v, buf[:, K:K + pad], 2.0, rows)
+    want = 2.0 * x.float() @ v[:rows].float().t()
+    assert rel_err(buf[:, K:K + rows], want) < 1e-2
+    assert not buf[:, K + rows:K + pad].any()
+    assert torch.equal(buf[:, K + pad:], sentinel)
+    first = buf[:, K:K + pad].clone()
+    _ops().lora_xwt(x, v, buf[:, K:K + pad], 2.0, rows)
+    assert torch.equal(buf[:, K:K + pad], first)
+
+
 @pytest.mark.parametrize("kern", ["lds", "reg"])
 @pytest.mark.parametrize("T,K,vrows", [(256, 512, 64), (256, 4096, 64), (4096, 1024, 128), (64, 192, 64),
                                        (4096, 8192, 64)])
