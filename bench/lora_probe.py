@@ -40,7 +40,7 @@ def time_us(fn, calls):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=4096)
-    ap.add_argument("--wgs", default="128,256")
+    ap.add_argument("--wgs", default="256")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--json-out", default=None)
@@ -61,8 +61,10 @@ def main():
         x, dy = xa[:, :K], dya[:, :N]
         def xwt(mode, X, V, tail):
             def f():
-                if mode == "lds":
+                if mode in ("lds", "lds_fused", "lds_red64"):
                     os.environ["MXLLM_LORA_XWT"] = "lds"
+                    os.environ["MXLLM_LORA_FUSED_RED"] = "1" if mode == "lds_fused" else "0"
+                    os.environ["MXLLM_LORA_XWT_RED_ROWS"] = "64" if mode == "lds_red64" else "16"
                     ops.lora_xwt(X, V, tail, s)
                 else:
                     os.environ["MXLLM_LORA_XWT"] = "tile"
@@ -70,11 +72,13 @@ def main():
             return f
 
         for cname, X, V, tail, nbytes in (("xwt_x", x, A, xa[:, K:], T * K * 2), ("xwt_dy", dy, Bt, dya[:, N:], T * N * 2)):
-            res = {"lds": [], "tile": []}
+            res = {"lds": [], "lds_red64": []}
             for _ in range(a.rounds):
                 for m in res:
                     res[m].append(time_us(xwt(m, X, V, tail), a.calls))
             os.environ.pop("MXLLM_LORA_XWT", None)
+            os.environ.pop("MXLLM_LORA_FUSED_RED", None)
+            os.environ.pop("MXLLM_LORA_XWT_RED_ROWS", None)
             rec = {"case": f"70b {name} {cname} T{T} R{R}", "gb": round(nbytes / 1e9, 3)}
             for m, v in res.items():
                 us = statistics.median(v)
@@ -82,16 +86,18 @@ def main():
             print(json.dumps(rec), flush=True)
             out.append(rec)
         fn, nbytes = (lambda: ops.lora_grads(x, dy, dya[:, N:], xa[:, K:], ga, gb, splits, r, True)), T * (K + N) * 2
-        res = {w: [] for w in wgs}
+        res = {w: [] for w in wgs + ["fused"]}
         for _ in range(a.rounds):
-            for w in wgs:
-                os.environ["MXLLM_LORA_WGS"] = str(w)
+            for w in res:
+                os.environ["MXLLM_LORA_WGS"] = str(w if w != "fused" else 256)
+                os.environ["MXLLM_LORA_FUSED_RED"] = "1" if w == "fused" else "0"
                 res[w].append(time_us(fn, a.calls))
         os.environ.pop("MXLLM_LORA_WGS", None)
+        os.environ.pop("MXLLM_LORA_FUSED_RED", None)
         rec = {"case": f"70b {name} grads T{T}", "gb": round(nbytes / 1e9, 3)}
         for w, v in res.items():
             us = statistics.median(v)
-            rec[f"wgs{w}"] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
+            rec[f"wgs{w}" if w != "fused" else "wgs256_fused_red"] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
         print(json.dumps(rec), flush=True)
         out.append(rec)
         del xa, dya, A, Bt, ga, gb

@@ -346,18 +346,21 @@ __global__ void __launch_bounds__(256, 1) lora_xwt_lds_kernel(const uint16_t* __
   }
 }
 
-// split partials ws[S][M/64][64][64] -> out (fixed split order); grid M/64
+// split partials ws[S][M/64][64][64] -> out (fixed split order); grid (64 / ROWS) M/64, ROWS rows
+// per workgroup (16 by default: at M 4096 the one-tile-per-workgroup grid of 64 workgroups left
+// this pass latency-bound, ~6 us per call; MXLLM_LORA_XWT_RED_ROWS=64 restores it for A/B)
 __global__ void __launch_bounds__(256) lora_xwt_reduce_kernel(const float* __restrict__ ws, int S, int mtiles,
-                                                              uint16_t* __restrict__ out, int64_t ldo, float alpha) {
-  const int mt = blockIdx.x, tid = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[tid + 256 * q];
+                                                              uint16_t* __restrict__ out, int64_t ldo, float alpha,
+                                                              int qpw) {
+  const int per = 4 / qpw;  // workgroups per 64-row tile
+  const int mt = blockIdx.x / per, tid = threadIdx.x;
+  for (int q = (blockIdx.x % per) * qpw; q < (blockIdx.x % per + 1) * qpw; ++q) {
+    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
+    float4 s = reinterpret_cast<const float4*>(ws + (int64_t)mt * 4096)[e4];
     for (int sp = 1; sp < S; ++sp) {
-      const float4 t = reinterpret_cast<const float4*>(ws + ((int64_t)sp * mtiles + mt) * 4096)[tid + 256 * q];
+      const float4 t = reinterpret_cast<const float4*>(ws + ((int64_t)sp * mtiles + mt) * 4096)[e4];
       s.x += t.x, s.y += t.y, s.z += t.z, s.w += t.w;
     }
-    const int e4 = tid + 256 * q, row = e4 >> 4, col = (e4 & 15) * 4;
     uint2 o;
     o.x = pack_bf16x2(alpha * s.x, alpha * s.y);
     o.y = pack_bf16x2(alpha * s.z, alpha * s.w);
@@ -924,7 +927,10 @@ extern "C" int mx_lora_xwt(const uint16_t* X, int64_t ldx, const uint16_t* V, in
     else
       lora_xwt_kernel<<<dim3(mtiles, S), 256, 0, stream>>>(X, ldx, V + (int64_t)c0 * ldv, ldv, out + c0, ldo, ws, M,
                                                            K, S, alpha, fused);
-    if (S > 1 && !fused) lora_xwt_reduce_kernel<<<mtiles, 256, 0, stream>>>(ws, S, mtiles, out + c0, ldo, alpha);
+    if (S > 1 && !fused) {
+      const int qpw = lora_env("MXLLM_LORA_XWT_RED_ROWS", 16) >= 64 ? 4 : 1;
+      lora_xwt_reduce_kernel<<<(4 / qpw) * mtiles, 256, 0, stream>>>(ws, S, mtiles, out + c0, ldo, alpha, qpw);
+    }
   }
   return (int)hipGetLastError();
 }
