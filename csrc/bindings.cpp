@@ -543,10 +543,16 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
 
 // dq_mode: 1 = f32 atomics, 2 = deterministic per-key-block partials + ordered reduce,
 // 3 = split (dS^T to HBM + separate dQ kernel; default, deterministic)
+// outs (optional, split mode only): preallocated f32 dq [B, Hq, S, D] and dK / dV partials
+// [B, P, Sk, D] to write into (e.g. head-range views of larger tensors: the chunked long-context
+// backward, mxllm/ops/attention.py) instead of fresh tensors.
 std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q,
                                                              const at::Tensor& k, const at::Tensor& v,
                                                              const at::Tensor& o, const at::Tensor& lse, int causal,
-                                                             double scale, int64_t dq_mode) {
+                                                             double scale, int64_t dq_mode,
+                                                             const c10::optional<at::Tensor>& dq_out = c10::nullopt,
+                                                             const c10::optional<at::Tensor>& dk_out = c10::nullopt,
+                                                             const c10::optional<at::Tensor>& dv_out = c10::nullopt) {
   check_bf16(dout, "dout");
   check_f32(lse, "lse");
   const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
@@ -571,13 +577,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
   const int64_t P = (causal >= 0 && dq_mode == 3)
                         ? mx_attn_bwd_partial_heads((int)B, (int)Hq, (int)Hkv, (int)S, (int)Sk, (int)D, (int)dq_mode)
                         : Hq;
-  auto dkp = at::empty({B, P, Sk, D}, q.options().dtype(at::kFloat));
-  auto dvp = at::empty({B, P, Sk, D}, q.options().dtype(at::kFloat));
+  const bool outs = dq_out.has_value() || dk_out.has_value() || dv_out.has_value();
+  if (outs) {
+    MX_CHECK(dq_out.has_value() && dk_out.has_value() && dv_out.has_value() && dq_mode == 3 && causal >= 0,
+             "attn_bwd: preallocated outputs need all three and the split mode");
+    check_f32(*dq_out, "dq_out");
+    check_f32(*dk_out, "dk_out");
+    check_f32(*dv_out, "dv_out");
+    MX_CHECK(dq_out->numel() == B * Hq * S * D && dk_out->numel() == B * P * Sk * D &&
+                 dv_out->numel() == B * P * Sk * D, "attn_bwd: output sizes");
+  }
+  auto dkp = outs ? *dk_out : at::empty({B, P, Sk, D}, q.options().dtype(at::kFloat));
+  auto dvp = outs ? *dv_out : at::empty({B, P, Sk, D}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   if (causal >= 0 && dq_mode != 1) {
     at::Tensor work = dq_mode == 2 ? at::empty({nkb, B, Hq, S_pad, D}, q.options().dtype(at::kFloat))
                                    : at::empty({B * Hq, nkb * 128, S_pad}, q.options());
-    auto dq = at::empty({B, Hq, S, D}, q.options().dtype(at::kFloat));
+    auto dq = outs ? *dq_out : at::empty({B, Hq, S, D}, q.options().dtype(at::kFloat));
     MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                       dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
                       (int)S, (int)Sk, (int)D, causal, (float)scale, (int)dq_mode, work.data_ptr(), ldo,
@@ -595,8 +611,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
 std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q,
                                                         const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
                                                         const at::Tensor& lse, bool causal, double scale,
-                                                        int64_t dq_mode) {
-  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, dq_mode);
+                                                        int64_t dq_mode, const c10::optional<at::Tensor>& dq_out,
+                                                        const c10::optional<at::Tensor>& dk_out,
+                                                        const c10::optional<at::Tensor>& dv_out) {
+  return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, dq_mode, dq_out, dk_out, dv_out);
 }
 
 // timing-only ablation variants (mode: -1 = causal without dQ atomics)
@@ -1051,7 +1069,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("swiglu_lora(Tensor? dm, Tensor gu, int pad, Tensor v, int nrb, float alpha) -> Tensor");
   m.def("lora_grads(Tensor x, Tensor dy, Tensor g, Tensor st, Tensor(a!) ga, Tensor(b!) gb, int[] splits, int r, bool accumulate) -> ()");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3) -> (Tensor, Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3, Tensor? dq_out=None, Tensor? dk_out=None, Tensor? dv_out=None) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {

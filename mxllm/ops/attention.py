@@ -44,9 +44,55 @@ class _AttnBlockFn(torch.autograd.Function):
         q, k, v, o, lse, cos, sin = ctx.saved_tensors
         B, S, Hq, Hkv, D, causal, grad_pad = ctx.dims
         ops = native()
-        dq, dkp, dvp = ops.attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D), dq_mode())
+        dq, dkp, dvp = attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D), dq_mode())
         dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D, grad_pad)
         return dqkv, None, None, None, None, None, None, None, None, None, None
+
+
+_DS_BUDGET = float(os.environ.get("MXLLM_ATTN_DS_BUDGET_GB", "4")) * 2**30
+
+
+def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float, mode: int):
+    """``native().attn_bwd`` with bounded memory.  The split dQ mode (3) passes dS^T through an
+    HBM image of B * Hq * Sk * S bf16 -- O(S^2): 1.1 GB at the 70B training shape, 64 GiB for one
+    8B sequence of 32k tokens.  Above ``MXLLM_ATTN_DS_BUDGET_GB`` (4 GiB) the call runs per
+    (sequence, chunk of whole KV groups), each chunk's image within the budget, writing its dQ and
+    dK / dV partials into head ranges of the full outputs (a KV head's partials stay consecutive for
+    rope_merge_bwd).
+    ``do`` [B*S, Hq*D] or [B, S, Hq*D], ``o`` [B, S, Hq*D] (row-strided allowed)."""
+    ops = native()
+    B, Hq, S, D = q.shape
+    Hkv, Sk = k.shape[1], k.shape[2]
+    per_head = (Sk + 127) // 128 * 128 * ((S + 63) // 64 * 64) * 2
+    if mode != 3 or B * Hq * per_head <= _DS_BUDGET:
+        return ops.attn_bwd(do, q, k, v, o, lse, causal, scale, mode)
+    G = Hq // Hkv
+    hpc = G  # heads per chunk: whole KV groups, a divisor of Hq (equal chunks -> equal partial layout)
+    for c in range(G, Hq + 1, G):
+        if Hq % c == 0 and c * per_head <= _DS_BUDGET:
+            hpc = c
+    do4 = do.reshape(B, S, Hq, D)
+    o3 = o.view(B, S, o.shape[-1]) if o.dim() != 3 else o
+    n = Hq // hpc
+    dq = dk = dv = None
+    for b in range(B):
+        for i in range(n):
+            h0, h1 = i * hpc, (i + 1) * hpc
+            args = (do4[b:b + 1, :, h0:h1].contiguous(), q[b:b + 1, h0:h1], k[b:b + 1, h0 // G:h1 // G],
+                    v[b:b + 1, h0 // G:h1 // G], o3[b:b + 1, :, h0 * D:h1 * D], lse[b:b + 1, h0:h1], causal, scale, 3)
+            if dq is None:  # first chunk: its partial-head count sizes the full dK / dV partials
+                dq_c, dk_c, dv_c = ops.attn_bwd(*args)
+                P = dk_c.shape[1]
+                dq = torch.empty(B, Hq, S, D, dtype=dq_c.dtype, device=dq_c.device)
+                dk = torch.empty(B, n * P, Sk, D, dtype=dk_c.dtype, device=dk_c.device)
+                dv = torch.empty_like(dk)
+                dq[0:1, h0:h1].copy_(dq_c)
+                dk[0:1, 0:P].copy_(dk_c)
+                dv[0:1, 0:P].copy_(dv_c)
+                del dq_c, dk_c, dv_c
+            else:  # every other chunk writes its head range in place
+                ops.attn_bwd(*args, dq[b:b + 1, h0:h1], dk[b:b + 1, i * P:(i + 1) * P], dv[b:b + 1, i * P:(i + 1) * P])
+    return dq, dk, dv
 
 
 def dq_mode() -> int:

@@ -93,6 +93,33 @@ def test_swiglu_lora_tail(gpu, T, F, R, bwd):
     assert torch.equal(again[:, W:], tail)
 
 
+def test_attention_bwd_bounded_ds_image(gpu, monkeypatch):
+    """Long-context memory bound: with the split-mode dS^T image over budget, the backward runs per
+    (sequence, KV-group chunk) and gives the one-call dQ, and per-KV-head dK / dV (partials summed),
+    to fp32 rounding."""
+    from mxllm.ops import attention as A
+
+    torch.manual_seed(11)
+    B, Hq, Hkv, S, D = 2, 8, 2, 512, 128
+    q = torch.randn(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    sc = 1 / math.sqrt(D)
+    o, lse = _ops().attn_fwd(q, k, v, True, sc)
+    do = torch.randn(B * S, Hq * D, device=gpu, dtype=torch.bfloat16)
+    ref_dq, ref_dk, ref_dv = _ops().attn_bwd(do, q, k, v, o, lse, True, sc, 3)
+    monkeypatch.setattr(A, "_DS_BUDGET", 1.5 * 2**20)  # < one KV group's image: 4 chunks of 4 heads
+    dq, dk, dv = A.attn_bwd(do, q, k, v, o, lse, True, sc, 3)
+    assert dq.shape == ref_dq.shape
+    assert rel_err(dq, ref_dq) < 1e-5
+
+    def per_kv(t):
+        return t.view(B, Hkv, -1, S, D).sum(2)
+
+    assert rel_err(per_kv(dk), per_kv(ref_dk)) < 1e-5
+    assert rel_err(per_kv(dv), per_kv(ref_dv)) < 1e-5
+
+
 @pytest.mark.parametrize("T,V", [(5, 1000), (256, 128256)])
 def test_cross_entropy(gpu, T, V):
     torch.manual_seed(3)
