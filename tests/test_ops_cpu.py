@@ -197,6 +197,54 @@ def test_lora_producer_written_tails_are_used():
     torch.testing.assert_close(lin.lora_a.grad, want[2], rtol=1e-5, atol=1e-5)
 
 
+def test_attention_bwd_chunking_assembles_head_ranges(monkeypatch):
+    """The long-context bound on the attention backward (mxllm/ops/attention.py attn_bwd): with a
+    budget below one call's dS^T image the backward runs per (sequence, KV-group chunk) and writes
+    each chunk's dQ and per-q-head dK / dV partials into its head range.  A CPU stand-in for the
+    native op (fp32 autograd, per-q-head partials, the out= arguments honoured) checks the slicing
+    and the assembly against one unchunked call."""
+    from mxllm.ops import attention as A
+    from mxllm.ops import reference as R
+
+    class Fake:
+        calls = 0
+
+        def attn_bwd(self, do, q, k, v, o, lse, causal, scale, mode, dq_out=None, dk_out=None, dv_out=None):
+            Fake.calls += 1
+            B, Hq, S, D = q.shape
+            Hkv = k.shape[1]
+            G = Hq // Hkv
+            qf = q.detach().float().clone().requires_grad_(True)
+            kr = k.detach().float().repeat_interleave(G, dim=1).requires_grad_(True)  # per-q-head copies -> partials
+            vr = v.detach().float().repeat_interleave(G, dim=1).requires_grad_(True)
+            out = R.attention(qf.transpose(1, 2), kr.transpose(1, 2), vr.transpose(1, 2), causal, scale)
+            out.backward(do.reshape(B, S, Hq, D).float())
+            res = (qf.grad, kr.grad, vr.grad)
+            if dq_out is None:
+                return res
+            for dst, src in zip((dq_out, dk_out, dv_out), res):
+                dst.copy_(src)
+            return dq_out, dk_out, dv_out
+
+    torch.manual_seed(0)
+    B, Hq, Hkv, S, D = 2, 8, 2, 64, 16
+    q = torch.randn(B, Hq, S, D)
+    k = torch.randn(B, Hkv, S, D)
+    v = torch.randn(B, Hkv, S, D)
+    o = torch.randn(B, S, Hq * D)
+    lse = torch.zeros(B, Hq, S)
+    do = torch.randn(B * S, Hq * D)
+    monkeypatch.setattr(A, "native", lambda: Fake())
+    want = Fake().attn_bwd(do, q, k, v, o, lse, True, 0.25, 3)
+    per_head = 128 * 64 * 2
+    monkeypatch.setattr(A, "_DS_BUDGET", 4 * per_head)  # one KV group (4 heads) per chunk
+    Fake.calls = 0
+    got = A.attn_bwd(do, q, k, v, o, lse, True, 0.25, 3)
+    assert Fake.calls == B * (Hq // 4)
+    for g, w in zip(got, want):
+        torch.testing.assert_close(g, w, rtol=1e-5, atol=1e-6)
+
+
 def test_fp8_weight_quantization_roundtrip():
     """Serving-time e4m3 weight quantisation (mxllm/serve/quant.py): per-channel
     scales, no zero / subnormal codes (the HIP decoder relies on it), the
