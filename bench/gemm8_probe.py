@@ -25,7 +25,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from mxllm.ops import native  # noqa: E402
+from mxllm.ops import gemm, native  # noqa: E402
 from mxllm.ops.linear import transpose2d  # noqa: E402
 
 SHAPES = {
@@ -134,14 +134,26 @@ def main():
     def record(res, form, M, N, K, out):
         results.append(res)
         measured.add((form, M, N, K, out))
-        ph, g = 8, res["gemm8"]["ms"]
+        ph, g, tail = 8, res["gemm8"]["ms"], 0
         if "gemm8_ph4" in res and res["gemm8_ph4"]["ms"] < g:
             ph, g = 4, res["gemm8_ph4"]["ms"]
+        if "gemm8_tail" in res and res["gemm8_tail"]["ms"] < g:
+            ph, g, tail = 4, res["gemm8_tail"]["ms"], gemm.tail_split(M, N, K)
         d = res[DEFAULT[form]]["ms"]
         if g < d * (1 - a.margin):
-            wins.append({"form": form, "M": M, "N": N, "K": K, "out": out, "ph": ph,
-                         "gemm8_tflops": round(2.0 * M * N * K / (g * 1e-3) / 1e12, 1),
-                         "default_tflops": res[DEFAULT[form]]["tflops"], "case": res["case"]})
+            e = {"form": form, "M": M, "N": N, "K": K, "out": out, "ph": ph,
+                 "gemm8_tflops": round(2.0 * M * N * K / (g * 1e-3) / 1e12, 1),
+                 "default_tflops": res[DEFAULT[form]]["tflops"], "case": res["case"]}
+            if tail:
+                e["tail"] = tail
+            wins.append(e)
+
+    def tail_variant(var, x, w, o, M, N, K):
+        """the tail-balanced launch (mx_gemm8_tail) where the tile grid leaves a short last wave"""
+        n1 = gemm.tail_split(M, N, K)
+        if n1:
+            var["gemm8_tail"] = lambda: ops.gemm8_tail(x, True, w, True, o, n1, 4)
+        return var
 
     if a.ablate:
         # timing-only ablations of the NN kernel (results wrong): doubled MFMA per phase, no barriers
@@ -203,8 +215,8 @@ def main():
                        "hipblaslt_nn": lambda: torch.mm(xa, wb, out=o)}
             else:
                 wb = rnd(N, K, dev=dev)
-                var = {"gemm8": lambda: ops.gemm8(xa, True, wb, True, o, 0.0, None, 1.0),
-                       "hipblaslt_tn": lambda: torch.mm(xa, wb.t(), out=o)}
+                var = tail_variant({"gemm8": lambda: ops.gemm8(xa, True, wb, True, o, 0.0, None, 1.0),
+                                    "hipblaslt_tn": lambda: torch.mm(xa, wb.t(), out=o)}, xa, wb, o, M, N, K)
             if a.ph4:
                 var["gemm8_ph4"] = _ph4(var["gemm8"])
             record(run_case(f"70b-lora {name} {form} M{M} N{N} K{K}", 2.0 * M * N * K, var, a.rounds, a.calls),
@@ -243,10 +255,10 @@ def main():
                 }, a.rounds, a.calls), "tt", O, I, T, "f32")
             if "tn" in forms and O % 256 == 0:
                 o = torch.empty(T, O, device=dev, dtype=torch.bfloat16)
-                record(run_case(f"{mdl} {pname} fwd tn T{T}", fl, {
+                record(run_case(f"{mdl} {pname} fwd tn T{T}", fl, tail_variant({
                     "gemm8": lambda: ops.gemm8(x, True, w, True, o, 0.0, None, 1.0),
                     "hipblaslt_tn": lambda: torch.mm(x, w.t(), out=o),
-                }, a.rounds, a.calls), "tn", T, O, I, "bf16")
+                }, x, w, o, T, O, I), a.rounds, a.calls), "tn", T, O, I, "bf16")
             del w, dy, x
             torch.cuda.empty_cache()
     if a.json_out:

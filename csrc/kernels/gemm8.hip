@@ -123,7 +123,18 @@ template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA, int V = 0, int PH = 8>
 __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
              void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
-             float alpha_f) {
+             float alpha_f, int k0 = 0, int64_t cpart = 0) {
+  // K split in two (gridDim.y == 2, k0 = K of part 0): part 1 covers K rows / columns k0 .. K-1 of
+  // both operands and writes its own output image C + cpart (mx_gemm8_tail: the last, partial wave
+  // of tiles of a GEMM runs as twice as many half-K workgroups; the images are summed after)
+  if (gridDim.y > 1) {
+    const int kp = blockIdx.y;
+    const int64_t koff = kp ? k0 : 0;
+    A += A_KC ? koff : koff * lda;
+    B += B_KC ? koff : koff * ldb;
+    if (kp) C = reinterpret_cast<char*>(C) + cpart * (OUT_F32 ? 4 : 2);
+    K = kp ? K - k0 : k0;
+  }
   // ONE __shared__ array (a second LDS object makes hipcc drain vmcnt before LDS reads: guide §5 item 4a)
   __shared__ __attribute__((aligned(1024))) char smem[2 * G8_TILE];
   const int nM = M >> 8, nN = N >> 8;
@@ -554,6 +565,66 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
     G8_OUT(false, false);
 #undef G8_OUT
 #undef G8_L
+  return (int)hipGetLastError();
+}
+
+// C[m, c0 + n] = bf16(P0[m, n] + P1[m, n]) for the two K-part images of mx_gemm8_tail
+__global__ void __launch_bounds__(256) g8_sum2_kernel(const float* __restrict__ P, int64_t part, int N2,
+                                                      uint16_t* __restrict__ C, int64_t ldc, int64_t n_elems) {
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < n_elems; i += (int64_t)gridDim.x * 256 * 8) {
+    const int64_t m = i / N2;
+    const int n = (int)(i - m * N2);
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(P + i), a1 = *reinterpret_cast<const f32x4*>(P + i + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(P + part + i), b1 = *reinterpret_cast<const f32x4*>(P + part + i + 4);
+    uint4 o;
+    o.x = pack_bf16x2(a0[0] + b0[0], a0[1] + b0[1]);
+    o.y = pack_bf16x2(a0[2] + b0[2], a0[3] + b0[3]);
+    o.z = pack_bf16x2(a1[0] + b1[0], a1[1] + b1[1]);
+    o.w = pack_bf16x2(a1[2] + b1[2], a1[3] + b1[3]);
+    *reinterpret_cast<uint4*>(C + m * ldc + n) = o;
+  }
+}
+
+// Tail-balanced bf16 GEMM, beta 0, alpha 1: C[M, N] = op(A) op(B) where the tile count leaves a last
+// wave of <= 128 tiles on the 256 CUs (e.g. the 70B qkv forward: 16 x 40 = 640 tiles).  Columns
+// [0, N1) run as one plain launch (whole waves); columns [N1, N) as ONE launch of twice as many
+// workgroups, each over half of K (gridDim.y = 2), into two fp32 images in `ws` (2 * M * (N - N1)
+// floats); g8_sum2_kernel adds them in a fixed order into C (deterministic).  The last wave then
+// takes half a wave's time.  N1 % 256 == 0, (N - N1) % 256 == 0; K split at a 64 multiple.
+extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc,
+                             uint16_t* C, int64_t ldc, int M, int N, int K, int N1, float* ws, int ph,
+                             hipStream_t stream) {
+  const int N2 = N - N1;
+  if (N1 <= 0 || N2 <= 0 || (N1 & 255) || (N2 & 255) || K < 2 * G8_BK) return -1;
+  // plain part
+  int rc = mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, M, N1, K, 0.f, nullptr, 1.f, ph, stream);
+  if (rc) return rc;
+  const uint16_t* B2 = b_kc ? B + (int64_t)N1 * ldb : B + N1;
+  const int k0 = (K / G8_BK / 2) * G8_BK;  // part 0: floor(K-tiles / 2) tiles
+  if ((a_kc ? lda < K : lda < M) || (b_kc ? ldb < K : ldb < N) || ldb % 8 || lda % 8) return -1;
+  if (((uintptr_t)A | (uintptr_t)B2 | (uintptr_t)ws) & 15) return -1;
+  const int64_t part = (int64_t)M * N2;
+  const dim3 grid((M >> 8) * (N2 >> 8), 2);
+  const char* phs = getenv("MXLLM_GEMM8_PH");
+  const bool ph4 = phs && *phs ? atoi(phs) == 4 : ph == 4;
+#define G8_T(AK, BK_)                                                                                              \
+  do {                                                                                                             \
+    if (ph4)                                                                                                       \
+      gemm8_kernel<AK, BK_, true, false, 0, 4><<<grid, 512, 0, stream>>>(A, lda, B2, ldb, ws, N2, M, N2, K, nullptr, \
+                                                                         1.f, k0, part);                           \
+    else                                                                                                           \
+      gemm8_kernel<AK, BK_, true, false><<<grid, 512, 0, stream>>>(A, lda, B2, ldb, ws, N2, M, N2, K, nullptr, 1.f,  \
+                                                                   k0, part);                                      \
+  } while (0)
+  if (a_kc && b_kc) G8_T(true, true);
+  else if (a_kc) G8_T(true, false);
+  else if (b_kc) G8_T(false, true);
+  else G8_T(false, false);
+#undef G8_T
+  const int64_t n = part;
+  int64_t blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  g8_sum2_kernel<<<(int)blocks, 256, 0, stream>>>(ws, part, N2, C + N1, ldc, n);
   return (int)hipGetLastError();
 }
 

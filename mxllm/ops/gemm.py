@@ -10,6 +10,8 @@ Every training GEMM of a Llama step is one of four operand orders over row-major
   nt    [K][M]     [N][K]     A^T @ B^T         (unused; for completeness)
 
 ``gemm8`` is selected per (form, M, N, K, output dtype) only where it was measured faster
+(entries with ``tail``: the tail-balanced launch, ``mx_gemm8_tail`` -- a last wave of at most half
+the CUs runs as twice as many half-K workgroups, e.g. the 16 x 40-tile 70B qkv forward)
 (``mxllm/tuning/gemm8_gfx950.json``, written from ``bench/gemm8_probe.py`` runs), or for every
 shape it takes in deterministic mode (``MXLLM_DETERMINISTIC=1``: one workgroup per output tile,
 a fixed K order, no split-K or atomics — the step is bitwise reproducible; vendor stream-K
@@ -34,6 +36,9 @@ def deterministic() -> bool:
     return os.environ.get("MXLLM_DETERMINISTIC", "0") == "1"
 
 
+_TAIL: dict = {}
+
+
 def _table() -> dict:
     global _TABLE
     if _TABLE is None:
@@ -41,10 +46,29 @@ def _table() -> dict:
         try:
             with open(_TABLE_PATH) as f:
                 for e in json.load(f).get("wins", []):
-                    _TABLE[(e["form"], e["M"], e["N"], e["K"], e["out"])] = int(e.get("ph", 8))
+                    key = (e["form"], e["M"], e["N"], e["K"], e["out"])
+                    _TABLE[key] = int(e.get("ph", 8))
+                    if e.get("tail"):
+                        _TAIL[key] = int(e["tail"])
         except (OSError, ValueError, KeyError):
             pass
     return _TABLE
+
+
+CUS = 256  # MI355X compute units: one gemm8 workgroup (256 x 256 tile) per CU at a time
+
+
+def tail_split(M: int, N: int, K: int) -> int:
+    """Column split N1 of the tail-balanced launch (mx_gemm8_tail), 0 if it does not apply: the
+    tile grid leaves a last wave of at most half the CUs, and whole waves fit in columns [0, N1)."""
+    if M % 256 or N % 256 or K < 128:
+        return 0
+    nM, nN = M // 256, N // 256
+    r = (nM * nN) % CUS
+    if r == 0 or r > CUS // 2 or (nM * nN - r) % nM:
+        return 0
+    n1 = (nM * nN - r) // nM
+    return n1 * 256 if 0 < n1 < nN else 0
 
 
 def _policy() -> str:
@@ -104,6 +128,10 @@ def mm(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = N
           and odt in (torch.bfloat16, torch.float32) else 0)
     if ph:
         a_kc, b_kc = _KC[form]
+        n1 = _TAIL.get((form, M, N, K, "f32" if odt == torch.float32 else "bf16"), 0)
+        if (n1 and beta == 0.0 and alpha_t is None and odt == torch.bfloat16
+                and native().gemm8_tail(a, a_kc, b, b_kc, out, n1, ph)):
+            return out
         if native().gemm8(a, a_kc, b, b_kc, out, float(beta), alpha_t, 1.0, ph):
             return out
     A = a if form in ("tn", "nn") else a.t()

@@ -100,3 +100,47 @@ def test_gemm8_identity_asymmetric(gpu):
     out = torch.empty(n, n, device=gpu, dtype=torch.float32)
     assert _ops().gemm8(a, True, b, False, out, 0.0, None, 1.0)
     assert torch.equal(out, b.float())
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,n1,K", [(256, 512, 256, 640), (512, 1280, 768, 8256), (4096, 10240, 8192, 8256)])
+def test_gemm8_tail_split(gpu, a_kc, b_kc, M, N, n1, K):
+    """Tail-balanced launch (mx_gemm8_tail): columns [0, n1) plain, the rest as two half-K launches
+    summed through fp32 images (odd K-tile counts split 64 / 65 ...): equals the fp32 reference and
+    is bit-reproducible."""
+    a = _mat(M, K, gpu, pad=8, seed=11) if a_kc else _mat(K, M, gpu, pad=8, seed=11)
+    b = _mat(N, K, gpu, pad=8, seed=12) if b_kc else _mat(K, N, gpu, pad=8, seed=12)
+    A = a.float() if a_kc else a.float().t()
+    B = b.float().t() if b_kc else b.float()
+    ref = A @ B
+    out = torch.empty(M, N + 16, device=gpu, dtype=torch.bfloat16)[:, :N]
+    assert _ops().gemm8_tail(a, a_kc, b, b_kc, out, n1, 4)
+    _check(out, ref, 5e-3)
+    _check(out[:, n1:], ref[:, n1:], 5e-3)
+    again = torch.empty_like(out)
+    assert _ops().gemm8_tail(a, a_kc, b, b_kc, again, n1, 4)
+    assert torch.equal(again, out)
+
+
+def test_gemm_dispatch_uses_tail_entry(gpu, monkeypatch):
+    """A win-table entry with ``tail`` routes the forward GEMM through the tail-balanced launch."""
+    from mxllm.ops import gemm
+
+    M, N, K = 4096, 10240, 1024
+    key = ("tn", M, N, K, "bf16")
+    monkeypatch.setitem(gemm._table(), key, 4)
+    monkeypatch.setitem(gemm._TAIL, key, gemm.tail_split(M, N, K))
+    calls = []
+    real = _ops()
+
+    class Spy:
+        def __getattr__(self, k):
+            if k == "gemm8_tail":
+                calls.append(k)
+            return getattr(real, k)
+
+    monkeypatch.setattr(gemm, "native", lambda: Spy())
+    x, w = _mat(M, K, gpu, seed=13), _mat(N, K, gpu, seed=14)
+    y = gemm.mm("tn", x, w)
+    assert calls == ["gemm8_tail"]
+    _check(y, x.float() @ w.float().t(), 5e-3)
