@@ -148,11 +148,11 @@ def main():
                 e["tail"] = tail
             wins.append(e)
 
-    def tail_variant(var, x, w, o, M, N, K):
+    def tail_variant(var, x, w, o, M, N, K, a_kc=True, b_kc=True):
         """the tail-balanced launch (mx_gemm8_tail) where the tile grid leaves a short last wave"""
-        n1 = gemm.tail_split(M, N, K)
-        if n1:
-            var["gemm8_tail"] = lambda: ops.gemm8_tail(x, True, w, True, o, n1, 4)
+        t = gemm.tail_split(M, N, K)
+        if t:
+            var["gemm8_tail"] = lambda: ops.gemm8_tail(x, a_kc, w, b_kc, o, abs(t), t < 0, 4)
         return var
 
     if a.ablate:
@@ -239,11 +239,11 @@ def main():
                 }, a.rounds, a.calls), "nn", T, I, O, "bf16")
             if "tt" in forms and O % 256 == 0 and I % 256 == 0:
                 o = torch.empty(O, I, device=dev, dtype=torch.bfloat16)
-                record(run_case(f"{mdl} {pname} dW tt bf16 T{T}", fl, {
+                record(run_case(f"{mdl} {pname} dW tt bf16 T{T}", fl, tail_variant({
                     "gemm8": lambda: ops.gemm8(dy, False, x, False, o, 0.0, None, 1.0),
                     "transpose_tn": lambda: torch.mm(transpose2d(dy), transpose2d(x).t(), out=o),
                     "hipblaslt_nt": lambda: torch.mm(dy.t(), x, out=o),
-                }, a.rounds, a.calls), "tt", O, I, T, "bf16")
+                }, dy, x, o, O, I, T, False, False), a.rounds, a.calls), "tt", O, I, T, "bf16")
             if "tt32" in forms and O % 256 == 0 and I % 256 == 0:
                 o32 = torch.zeros(O, I, device=dev, dtype=torch.float32)
                 record(run_case(f"{mdl} {pname} dW tt fp32+=  T{T}", fl, {

@@ -195,11 +195,11 @@ bool gemm8(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::T
   return true;
 }
 
-// out[M, N] (bf16) = op(a) op(b) with the tail-balanced launch (mx_gemm8_tail): columns [0, n1) as
-// whole waves of tiles, columns [n1, N) as half-K workgroups summed through an fp32 workspace.
-// Returns false (nothing launched) for shapes it does not take.
-bool gemm8_tail(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::Tensor& out, int64_t n1,
-                int64_t ph) {
+// out[M, N] (bf16) = op(a) op(b) with the tail-balanced launch (mx_gemm8_tail): the output split at
+// `at` columns (rows when `rows`) -- whole waves of tiles before it, half-K workgroups summed through
+// an fp32 workspace after it.  Returns false (nothing launched) for shapes it does not take.
+bool gemm8_tail(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::Tensor& out, int64_t at,
+                bool rows, int64_t ph) {
   MX_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm8_tail: GPU tensors");
   MX_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
            "gemm8_tail: bf16 operands and output");
@@ -207,13 +207,14 @@ bool gemm8_tail(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, 
   const int64_t M = a_kc ? a.size(0) : a.size(1), K = a_kc ? a.size(1) : a.size(0);
   const int64_t N = b_kc ? b.size(0) : b.size(1), Kb = b_kc ? b.size(1) : b.size(0);
   MX_CHECK(K == Kb && out.size(0) == M && out.size(1) == N, "gemm8_tail: shape mismatch");
-  if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1 || n1 <= 0 || n1 >= N) return false;
+  const int64_t lim = rows ? M : N;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1 || at <= 0 || at >= lim) return false;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return false;
   DevGuard g(a.device());
-  auto ws = at::empty({2 * M * (N - n1)}, a.options().dtype(at::kFloat));
+  auto ws = at::empty({2 * (lim - at) * (rows ? N : M)}, a.options().dtype(at::kFloat));
   const int rc = mx_gemm8_tail(bf(a), a.stride(0), a_kc ? 1 : 0, bf(b), b.stride(0), b_kc ? 1 : 0, bfm(out),
-                               out.stride(0), (int)M, (int)N, (int)K, (int)n1, ws.data_ptr<float>(), (int)ph,
-                               cur_stream());
+                               out.stride(0), (int)M, (int)N, (int)K, rows ? 1 : 0, (int)at, ws.data_ptr<float>(),
+                               (int)ph, cur_stream());
   if (rc == -1) return false;
   MX_OK(rc);
   return true;
@@ -1059,7 +1060,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
   m.def("gemm8_stamps() -> Tensor", &gemm8_stamps);
-  m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int n1, int ph=4) -> bool");
+  m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4) -> bool");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");

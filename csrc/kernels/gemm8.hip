@@ -586,45 +586,48 @@ __global__ void __launch_bounds__(256) g8_sum2_kernel(const float* __restrict__ 
 }
 
 // Tail-balanced bf16 GEMM, beta 0, alpha 1: C[M, N] = op(A) op(B) where the tile count leaves a last
-// wave of <= 128 tiles on the 256 CUs (e.g. the 70B qkv forward: 16 x 40 = 640 tiles).  Columns
-// [0, N1) run as one plain launch (whole waves); columns [N1, N) as ONE launch of twice as many
-// workgroups, each over half of K (gridDim.y = 2), into two fp32 images in `ws` (2 * M * (N - N1)
-// floats); g8_sum2_kernel adds them in a fixed order into C (deterministic).  The last wave then
-// takes half a wave's time.  N1 % 256 == 0, (N - N1) % 256 == 0; K split at a 64 multiple.
+// wave of <= 128 tiles on the 256 CUs (e.g. the 70B qkv forward: 16 x 40 = 640 tiles).  The output is
+// split at `at` (columns, or rows when `rows`): [0, at) runs as one plain launch of whole waves; the
+// rest as ONE launch of twice as many workgroups, each over half of K (gridDim.y = 2), into two fp32
+// images in `ws` (2 * its element count); g8_sum2_kernel adds them in a fixed order into C
+// (deterministic).  The last wave then takes half a wave's time.  `at` and the rest multiples of 256.
 extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc,
-                             uint16_t* C, int64_t ldc, int M, int N, int K, int N1, float* ws, int ph,
+                             uint16_t* C, int64_t ldc, int M, int N, int K, int rows, int at, float* ws, int ph,
                              hipStream_t stream) {
-  const int N2 = N - N1;
-  if (N1 <= 0 || N2 <= 0 || (N1 & 255) || (N2 & 255) || K < 2 * G8_BK) return -1;
+  const int lim = rows ? M : N, rest = lim - at;
+  if (at <= 0 || rest <= 0 || (at & 255) || (rest & 255) || K < 2 * G8_BK) return -1;
+  if ((a_kc ? lda < K : lda < M) || (b_kc ? ldb < K : ldb < N) || ldb % 8 || lda % 8 || ldc % 8) return -1;
   // plain part
-  int rc = mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, M, N1, K, 0.f, nullptr, 1.f, ph, stream);
+  int rc = rows ? mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, at, N, K, 0.f, nullptr, 1.f, ph, stream)
+                : mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, M, at, K, 0.f, nullptr, 1.f, ph, stream);
   if (rc) return rc;
-  const uint16_t* B2 = b_kc ? B + (int64_t)N1 * ldb : B + N1;
+  const uint16_t* A2 = rows ? (a_kc ? A + (int64_t)at * lda : A + at) : A;
+  const uint16_t* B2 = rows ? B : (b_kc ? B + (int64_t)at * ldb : B + at);
+  uint16_t* C2 = rows ? C + (int64_t)at * ldc : C + at;
+  const int M2 = rows ? rest : M, N2 = rows ? N : rest;
   const int k0 = (K / G8_BK / 2) * G8_BK;  // part 0: floor(K-tiles / 2) tiles
-  if ((a_kc ? lda < K : lda < M) || (b_kc ? ldb < K : ldb < N) || ldb % 8 || lda % 8) return -1;
-  if (((uintptr_t)A | (uintptr_t)B2 | (uintptr_t)ws) & 15) return -1;
-  const int64_t part = (int64_t)M * N2;
-  const dim3 grid((M >> 8) * (N2 >> 8), 2);
+  if (((uintptr_t)A2 | (uintptr_t)B2 | (uintptr_t)ws) & 15) return -1;
+  const int64_t part = (int64_t)M2 * N2;
+  const dim3 grid((M2 >> 8) * (N2 >> 8), 2);
   const char* phs = getenv("MXLLM_GEMM8_PH");
   const bool ph4 = phs && *phs ? atoi(phs) == 4 : ph == 4;
-#define G8_T(AK, BK_)                                                                                              \
-  do {                                                                                                             \
-    if (ph4)                                                                                                       \
-      gemm8_kernel<AK, BK_, true, false, 0, 4><<<grid, 512, 0, stream>>>(A, lda, B2, ldb, ws, N2, M, N2, K, nullptr, \
-                                                                         1.f, k0, part);                           \
-    else                                                                                                           \
-      gemm8_kernel<AK, BK_, true, false><<<grid, 512, 0, stream>>>(A, lda, B2, ldb, ws, N2, M, N2, K, nullptr, 1.f,  \
-                                                                   k0, part);                                      \
+#define G8_T(AK, BK_)                                                                                               \
+  do {                                                                                                              \
+    if (ph4)                                                                                                        \
+      gemm8_kernel<AK, BK_, true, false, 0, 4><<<grid, 512, 0, stream>>>(A2, lda, B2, ldb, ws, N2, M2, N2, K, nullptr, \
+                                                                         1.f, k0, part);                            \
+    else                                                                                                            \
+      gemm8_kernel<AK, BK_, true, false><<<grid, 512, 0, stream>>>(A2, lda, B2, ldb, ws, N2, M2, N2, K, nullptr, 1.f, \
+                                                                   k0, part);                                       \
   } while (0)
   if (a_kc && b_kc) G8_T(true, true);
   else if (a_kc) G8_T(true, false);
   else if (b_kc) G8_T(false, true);
   else G8_T(false, false);
 #undef G8_T
-  const int64_t n = part;
-  int64_t blocks = (n / 8 + 255) / 256;
+  int64_t blocks = (part / 8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  g8_sum2_kernel<<<(int)blocks, 256, 0, stream>>>(ws, part, N2, C + N1, ldc, n);
+  g8_sum2_kernel<<<(int)blocks, 256, 0, stream>>>(ws, part, N2, C2, ldc, part);
   return (int)hipGetLastError();
 }
 

@@ -59,27 +59,21 @@ CUS = 256  # MI355X compute units: one gemm8 workgroup (256 x 256 tile) per CU a
 
 
 def tail_split(M: int, N: int, K: int) -> int:
-    """Column split N1 of the tail-balanced launch (mx_gemm8_tail), 0 if it does not apply: the
-    tile grid leaves a last wave of at most half the CUs, and whole waves fit in columns [0, N1)."""
+    """Split of the tail-balanced launch (mx_gemm8_tail), 0 if it does not apply: the tile grid leaves
+    a last wave of at most half the CUs.  > 0: split at that COLUMN (whole waves of tiles in columns
+    [0, N1)); < 0: split at ROW -value (when no column split gives whole waves)."""
     if M % 256 or N % 256 or K < 128:
         return 0
     nM, nN = M // 256, N // 256
     r = (nM * nN) % CUS
-    if r == 0 or r > CUS // 2 or (nM * nN - r) % nM:
+    if r == 0 or r > CUS // 2:
         return 0
-    n1 = (nM * nN - r) // nM
-    return n1 * 256 if 0 < n1 < nN else 0
-
-
-def _policy() -> str:
-    return os.environ.get("MXLLM_GEMM8", "table")
-
-
-def takes(form: str, M: int, N: int, K: int) -> bool:
-    """Shape constraints of the kernel (mirrors mx_gemm8)."""
-    if M % 256 or N % 256 or K <= 0:
-        return False
-    return K % 64 == 0 or form == "tt"
+    full = nM * nN - r
+    if full % nM == 0 and 0 < full // nM < nN:
+        return full // nM * 256
+    if full % nN == 0 and 0 < full // nN < nM:
+        return -(full // nN * 256)
+    return 0
 
 
 def schedule(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> int:
@@ -128,9 +122,9 @@ def mm(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = N
           and odt in (torch.bfloat16, torch.float32) else 0)
     if ph:
         a_kc, b_kc = _KC[form]
-        n1 = _TAIL.get((form, M, N, K, "f32" if odt == torch.float32 else "bf16"), 0)
-        if (n1 and beta == 0.0 and alpha_t is None and odt == torch.bfloat16
-                and native().gemm8_tail(a, a_kc, b, b_kc, out, n1, ph)):
+        t = _TAIL.get((form, M, N, K, "f32" if odt == torch.float32 else "bf16"), 0)
+        if (t and beta == 0.0 and alpha_t is None and odt == torch.bfloat16
+                and native().gemm8_tail(a, a_kc, b, b_kc, out, abs(t), t < 0, ph)):
             return out
         if native().gemm8(a, a_kc, b, b_kc, out, float(beta), alpha_t, 1.0, ph):
             return out

@@ -114,12 +114,19 @@ def test_gemm8_tail_split(gpu, a_kc, b_kc, M, N, n1, K):
     B = b.float().t() if b_kc else b.float()
     ref = A @ B
     out = torch.empty(M, N + 16, device=gpu, dtype=torch.bfloat16)[:, :N]
-    assert _ops().gemm8_tail(a, a_kc, b, b_kc, out, n1, 4)
+    assert _ops().gemm8_tail(a, a_kc, b, b_kc, out, n1, False, 4)
     _check(out, ref, 5e-3)
     _check(out[:, n1:], ref[:, n1:], 5e-3)
     again = torch.empty_like(out)
-    assert _ops().gemm8_tail(a, a_kc, b, b_kc, again, n1, 4)
+    assert _ops().gemm8_tail(a, a_kc, b, b_kc, again, n1, False, 4)
     assert torch.equal(again, out)
+    # the same split along rows (M1 = n1 rows when M allows it)
+    if M > 256:
+        m1 = 256
+        rows_out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        assert _ops().gemm8_tail(a, a_kc, b, b_kc, rows_out, m1, True, 4)
+        _check(rows_out, ref, 5e-3)
+        _check(rows_out[m1:], ref[m1:], 5e-3)
 
 
 def test_gemm_dispatch_uses_tail_entry(gpu, monkeypatch):
@@ -129,6 +136,7 @@ def test_gemm_dispatch_uses_tail_entry(gpu, monkeypatch):
     M, N, K = 4096, 10240, 1024
     key = ("tn", M, N, K, "bf16")
     monkeypatch.setitem(gemm._table(), key, 4)
+    assert gemm.tail_split(M, N, K) == 8192
     monkeypatch.setitem(gemm._TAIL, key, gemm.tail_split(M, N, K))
     calls = []
     real = _ops()
