@@ -76,6 +76,17 @@ def tail_split(M: int, N: int, K: int) -> int:
     return 0
 
 
+def _policy() -> str:
+    return os.environ.get("MXLLM_GEMM8", "table")
+
+
+def takes(form: str, M: int, N: int, K: int) -> bool:
+    """Shape constraints of the kernel (mirrors mx_gemm8)."""
+    if M % 256 or N % 256 or K <= 0:
+        return False
+    return K % 64 == 0 or form == "tt"
+
+
 def schedule(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> int:
     """0 = not on gemm8; else its phase schedule (8 or 4) for this shape."""
     pol = _policy()
