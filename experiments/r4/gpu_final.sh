@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 final evidence pass: GPU suite, smoke(), default bench line x2, kernel-trace breakdowns
-OUT=gpurun_out/r4_final; mkdir -p $OUT
+OUT=gpurun_out/${FINAL_OUT:-r4_final}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/tests.txt 2>&1
 rc=$?; tail -3 $OUT/tests.txt; [ $rc -eq 0 ] || { echo "gpu suite rc=$rc"; exit 1; }
@@ -10,6 +10,9 @@ for i in 1 2; do
   timeout -k 10 400 python bench.py > $OUT/bench_$i.json 2> $OUT/bench_$i.err || { echo "bench rc=$?"; exit 1; }
   echo "bench $i: $(python -c "import json;j=json.load(open('$OUT/bench_$i.json'));print(j['value'],j['ms_per_step'],j['config2_8b_full']['value'],j['config2_8b_full']['ms_per_step'],j['config2_8b_full_mb4']['value'],j['calibration'])")"
 done
+C4="--model llama3.1-70b --finetune full --parallel zero3 --act-ckpt --act-ckpt-layers 40 --micro-batch 4 --emulate-world 8 --steps 3 --warmup 2 --no-calibrate"
+timeout -k 10 400 python -u bench.py $C4 --json-out $OUT/c4_ck40.json > $OUT/c4_ck40.log 2>&1 || { echo "c4 rc=$?"; exit 1; }
+echo "c4 ck40: $(python -c "import json;j=json.load(open('$OUT/c4_ck40.json'));print(j['ms_per_step'],j['value'],j['peak_hbm_reserved_gb'])")"
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_head -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --config2 off --no-calibrate > $ROOT/$OUT/prof_head.log 2>&1 || { echo "prof head rc=$?"; exit 1; }
