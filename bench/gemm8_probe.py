@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-table", action="store_true", help="hipBLASLt defaults instead of the tuned table")
     ap.add_argument("--shapes", default="", help="comma list of projection names to run (default all)")
+    ap.add_argument("--aug-only", action="store_true", help="only the --aug shapes")
     ap.add_argument("--aug", action="store_true",
                     help="also the 70B LoRA headline's augmented shapes (K + 64 pad, padded weight buffers) and head")
     ap.add_argument("--write-table", default=None,
@@ -125,7 +126,8 @@ def main():
     if a.ph4:
         os.environ["_G8_PH4_ALL"] = "1"
     forms = a.forms.split(",")
-    models = ["70b", "8b"] if a.model == "both" else [a.model]
+    models = [] if a.aug_only else (["70b", "8b"] if a.model == "both" else [a.model])
+    a.aug = a.aug or a.aug_only
     only = set(filter(None, a.shapes.split(",")))
     results = []
     wins = []
@@ -200,6 +202,7 @@ def main():
         for name, form, M, N, K, ldb in (("o dX", "nn", T, 8192, 8192 + P, 8192 + P),
                                          ("gu dX", "nn", T, 8192, 57344 + P, 8192 + P),
                                          ("down fwd (transposed buffer)", "nn", T, 8192, 28672 + P, 8192 + P),
+                                         ("down fwd", "tn", T, 8192, 28672 + P, 28672 + P),
                                          ("head dX", "nn", T, 8192, 128256, 8192),
                                          ("qkv fwd", "tn", T, 10240, 8192 + P, 8192 + P),
                                          ("o fwd", "tn", T, 8192, 8192 + P, 8192 + P),
