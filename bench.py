@@ -227,14 +227,7 @@ def main(argv=None):
         round(free_gb, 1) if free_gb is not None else None)}
     for kind, key in children:
         if kind == "config4":
-            ck, need = config4_plan(a, free_gb)
-            if ck is None:
-                out[key] = {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < {need:.0f} GB the "
-                                       f"config-4 child needs with every layer checkpointed"}
-            else:
-                out[key] = run_config4(a, env.world_size, ck)
-                out[key]["hbm_plan"] = {"min_free_hbm_gb": None if free_gb is None else round(free_gb, 1),
-                                        "need_gb": round(need, 1), "checkpointed_layers": ck}
+            out[key] = run_config4_planned(a, env.world_size, free_gb)
         else:
             out[key] = run_config3(a, env.world_size)
     emit(out, a.json_out)
@@ -383,6 +376,27 @@ def config4_plan(a, free_gb: float | None) -> tuple[int | None, float]:
         if free_gb is None or free_gb >= need(ck):
             return ck, need(ck)
     return None, need(80)
+
+
+def run_config4_planned(a, world: int, free_gb: float | None) -> dict:
+    """Config-4 child with the checkpoint depth from ``config4_plan``; a failed child (e.g. RCCL
+    buffers beyond the HBM model) is rerun once with every layer checkpointed -- insurance for the
+    one real 8-rank measurement.  The plan (and a failed first attempt) is recorded as ``hbm_plan``."""
+    ck, need = config4_plan(a, free_gb)
+    if ck is None:
+        return {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < {need:.0f} GB the "
+                           f"config-4 child needs with every layer checkpointed"}
+    res = run_config4(a, world, ck)
+    first = None
+    if "error" in res and a.config4_act_ckpt_layers is None and ck < 80:
+        first = {"checkpointed_layers": ck, "error": res["error"]}
+        ck = 80
+        res = run_config4(a, world, ck)
+    res["hbm_plan"] = {"min_free_hbm_gb": None if free_gb is None else round(free_gb, 1),
+                       "need_gb": round(need, 1), "checkpointed_layers": ck}
+    if first is not None:
+        res["hbm_plan"]["first_attempt"] = first
+    return res
 
 
 def run_config4(a, world: int, ckpt_layers: int = 40) -> dict:

@@ -136,3 +136,27 @@ def test_config4_plan_fits_free_hbm():
     assert bench.config4_plan(a, None)[0] == 40  # CPU rehearsal: no HBM to check
     a.config4_act_ckpt_layers = 24
     assert bench.config4_plan(a, 308.0)[0] == 24 and bench.config4_plan(a, 250.0)[0] is None
+
+
+def test_config4_failed_child_is_retried_fully_checkpointed(monkeypatch):
+    """A failed config-4 child (the one real 8-rank measurement) is rerun once with every layer
+    checkpointed, and the first attempt is recorded; an explicit depth is not second-guessed."""
+    import argparse
+
+    import bench
+
+    calls = []
+
+    def fake(a, world, ck):
+        calls.append(ck)
+        return {"error": "child job exit code 1"} if len(calls) == 1 else {"ms_per_step": 1.0}
+
+    monkeypatch.setattr(bench, "run_config4", fake)
+    a = argparse.Namespace(config4_act_ckpt_layers=None)
+    r = bench.run_config4_planned(a, 8, 308.0)
+    assert calls == [40, 80] and r["ms_per_step"] == 1.0
+    assert r["hbm_plan"]["checkpointed_layers"] == 80 and r["hbm_plan"]["first_attempt"]["checkpointed_layers"] == 40
+    calls.clear()
+    a.config4_act_ckpt_layers = 56
+    r = bench.run_config4_planned(a, 8, 308.0)
+    assert calls == [56] and "error" in r
