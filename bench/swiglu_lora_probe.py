@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--cs", default="0")
+    ap.add_argument("--rbw", default="1", help="16-row blocks per workgroup (MXLLM_SWIGLU_LORA_RBW)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -61,9 +62,10 @@ def main():
 
                 def plain():
                     ops.swiglu_fwd(gu, pad)
-                fused = {f"fused_cs{c}": (lambda c=c: (os.environ.__setitem__("MXLLM_SWIGLU_LORA_CS", str(c)),
-                                                       ops.swiglu_lora(None, gu, pad, a_d, r_d // 16, s)))
-                         for c in map(int, a.cs.split(","))}
+                fused = {f"fused_r{rb}_cs{c}": (lambda c=c, rb=rb: (os.environ.__setitem__("MXLLM_SWIGLU_LORA_CS", str(c)),
+                                                                   os.environ.__setitem__("MXLLM_SWIGLU_LORA_RBW", rb),
+                                                                   ops.swiglu_lora(None, gu, pad, a_d, r_d // 16, s)))
+                         for c in map(int, a.cs.split(",")) for rb in a.rbw.split(",")}
                 nbytes = 3 * T * F * 2
             else:
                 def unfused():
@@ -73,9 +75,10 @@ def main():
 
                 def plain():
                     ops.swiglu_bwd(dm, gu, pad)
-                fused = {f"fused_cs{c}": (lambda c=c: (os.environ.__setitem__("MXLLM_SWIGLU_LORA_CS", str(c)),
-                                                       ops.swiglu_lora(dm, gu, pad, bt_gu, r_gu // 16, s)))
-                         for c in map(int, a.cs.split(","))}
+                fused = {f"fused_r{rb}_cs{c}": (lambda c=c, rb=rb: (os.environ.__setitem__("MXLLM_SWIGLU_LORA_CS", str(c)),
+                                                                   os.environ.__setitem__("MXLLM_SWIGLU_LORA_RBW", rb),
+                                                                   ops.swiglu_lora(dm, gu, pad, bt_gu, r_gu // 16, s)))
+                         for c in map(int, a.cs.split(",")) for rb in a.rbw.split(",")}
                 nbytes = 5 * T * F * 2
             variants = {"unfused": unfused, "swiglu_only": plain, **fused}
             res = {k: [] for k in variants}
@@ -87,6 +90,7 @@ def main():
                 us = statistics.median(v)
                 rec[k] = {"us": round(us, 1), "swiglu_tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
             os.environ.pop("MXLLM_SWIGLU_LORA_CS", None)
+            os.environ.pop("MXLLM_SWIGLU_LORA_RBW", None)
             print(json.dumps(rec), flush=True)
             out.append(rec)
         del gu, dm, a_d, bt_gu

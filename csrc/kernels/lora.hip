@@ -609,32 +609,37 @@ constexpr int kSlRow = 136;  // LDS image row stride (elements): 272 B -> confli
 
 __device__ __forceinline__ float sl_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
-template <bool BWD, int NRB>
+template <bool BWD, int NRB, int RBW>
 __global__ void __launch_bounds__(256) swiglu_lora_kernel(const uint16_t* __restrict__ gu,
                                                           const uint16_t* __restrict__ dm, uint16_t* __restrict__ out,
                                                           int64_t ldo, const uint16_t* __restrict__ V, int64_t ldv,
                                                           float* __restrict__ ws, int F, int CS) {
+  // RBW 16-row blocks per workgroup share every V fragment (V is read from L2 / the MALL once per
+  // 16 RBW tokens instead of once per 16)
   constexpr int NP = BWD ? 2 : 1;  // LDS images per tile (BWD: dg, du)
   constexpr int NC = 16 * NRB;
-  __shared__ __attribute__((aligned(16))) uint16_t img[2][NP][16 * kSlRow];
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][NP][RBW][16 * kSlRow];
   __shared__ __attribute__((aligned(16))) float red[4][16][NC + 4];
-  const int rb = blockIdx.x, split = blockIdx.y, tid = threadIdx.x;
+  const int rg = blockIdx.x, split = blockIdx.y, tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, r = lane & 15, gq = lane >> 4;
   const int row = tid >> 4, ch = tid & 15;
   const int tiles = F >> 7;
   const int t0 = (int)((int64_t)split * tiles / CS), t1 = (int)((int64_t)(split + 1) * tiles / CS);
-  const int64_t tok = (int64_t)rb * 16 + row;
+  const int64_t tok = (int64_t)rg * 16 * RBW + row;
   const uint16_t* grow = gu + tok * (2 * (int64_t)F) + 8 * ch;
   const uint16_t* drow = dm + tok * (int64_t)F + 8 * ch;  // BWD only
   uint16_t* orow = out + tok * ldo + 8 * ch;
+  const int64_t gstep = 16 * (2 * (int64_t)F), dstep = 16 * (int64_t)F, ostep = 16 * ldo;  // next row block
   const uint16_t* vrow = V + (int64_t)r * ldv + 32 * w + 8 * gq;
   const int wofs = row * kSlRow + 8 * ch, rofs = r * kSlRow + 32 * w + 8 * gq;
 
-  f32x4 acc[NRB];
+  f32x4 acc[RBW][NRB];
 #pragma unroll
-  for (int b = 0; b < NRB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < RBW; ++i)
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u16x8 g, u, d, vf[NP][NRB];
+  u16x8 g[RBW], u[RBW], d[RBW], vf[NP][NRB];
   auto vload = [&](int t) {
 #pragma unroll
     for (int p = 0; p < NP; ++p)
@@ -642,62 +647,78 @@ __global__ void __launch_bounds__(256) swiglu_lora_kernel(const uint16_t* __rest
       for (int b = 0; b < NRB; ++b)
         vf[p][b] = *reinterpret_cast<const u16x8*>(vrow + (int64_t)(16 * b) * ldv + p * F + (t << 7));
   };
+  auto load = [&](int t, u16x8(&g_)[RBW], u16x8(&u_)[RBW], u16x8(&d_)[RBW]) {
+    const int c = t << 7;
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      g_[i] = *reinterpret_cast<const u16x8*>(grow + i * gstep + c);
+      u_[i] = *reinterpret_cast<const u16x8*>(grow + i * gstep + F + c);
+      if (BWD) d_[i] = *reinterpret_cast<const u16x8*>(drow + i * dstep + c);
+    }
+  };
   if (t0 < t1) {
-    g = *reinterpret_cast<const u16x8*>(grow + (t0 << 7));
-    u = *reinterpret_cast<const u16x8*>(grow + F + (t0 << 7));
-    if (BWD) d = *reinterpret_cast<const u16x8*>(drow + (t0 << 7));
+    load(t0, g, u, d);
     vload(t0);
   }
   for (int t = t0; t < t1; ++t) {
     const int c = t << 7, buf = (t - t0) & 1;
-    u16x8 gn, un, dn;
-    const int cn = (t + 1 < t1 ? t + 1 : t) << 7;  // the last trip reloads its own tile (no branch)
-    gn = *reinterpret_cast<const u16x8*>(grow + cn);
-    un = *reinterpret_cast<const u16x8*>(grow + F + cn);
-    if (BWD) dn = *reinterpret_cast<const u16x8*>(drow + cn);
-    u16x8 o0, o1;
-    if (!BWD) {
+    u16x8 gn[RBW], un[RBW], dn[RBW];
+    load(t + 1 < t1 ? t + 1 : t, gn, un, dn);  // the last trip reloads its own tile (no branch)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gf = bf2f(g[j]);
-        o0[j] = f2bf(gf * sl_sigmoid(gf) * bf2f(u[j]));
-      }
-      *reinterpret_cast<u16x8*>(orow + c) = o0;
-      *reinterpret_cast<u16x8*>(&img[buf][0][wofs]) = o0;
-    } else {
+    for (int i = 0; i < RBW; ++i) {
+      u16x8 o0, o1;
+      if (!BWD) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
-        const float s = sl_sigmoid(gf);
-        o0[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
-        o1[j] = f2bf(df * gf * s);
+        for (int j = 0; j < 8; ++j) {
+          const float gf = bf2f(g[i][j]);
+          o0[j] = f2bf(gf * sl_sigmoid(gf) * bf2f(u[i][j]));
+        }
+        *reinterpret_cast<u16x8*>(orow + i * ostep + c) = o0;
+        *reinterpret_cast<u16x8*>(&img[buf][0][i][wofs]) = o0;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gf = bf2f(g[i][j]), uf = bf2f(u[i][j]), df = bf2f(d[i][j]);
+          const float s = sl_sigmoid(gf);
+          o0[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
+          o1[j] = f2bf(df * gf * s);
+        }
+        *reinterpret_cast<u16x8*>(orow + i * ostep + c) = o0;
+        *reinterpret_cast<u16x8*>(orow + i * ostep + F + c) = o1;
+        *reinterpret_cast<u16x8*>(&img[buf][0][i][wofs]) = o0;
+        *reinterpret_cast<u16x8*>(&img[buf][NP - 1][i][wofs]) = o1;
       }
-      *reinterpret_cast<u16x8*>(orow + c) = o0;
-      *reinterpret_cast<u16x8*>(orow + F + c) = o1;
-      *reinterpret_cast<u16x8*>(&img[buf][0][wofs]) = o0;
-      *reinterpret_cast<u16x8*>(&img[buf][NP - 1][wofs]) = o1;
     }
     __syncthreads();  // the image is complete; the other buffer's readers (trip t-1) are past it
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const u16x8 a = *reinterpret_cast<const u16x8*>(&img[buf][p][rofs]);
+    for (int i = 0; i < RBW; ++i)
 #pragma unroll
-      for (int b = 0; b < NRB; ++b) acc[b] = lmfma(a, vf[p][b], acc[b]);
+      for (int p = 0; p < NP; ++p) {
+        const u16x8 a = *reinterpret_cast<const u16x8*>(&img[buf][p][i][rofs]);
+#pragma unroll
+        for (int b = 0; b < NRB; ++b) acc[i][b] = lmfma(a, vf[p][b], acc[i][b]);
+      }
+    vload(t + 1 < t1 ? t + 1 : t);  // next tile's V fragments under this tile's tail and the next math
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      g[i] = gn[i], u[i] = un[i];
+      if (BWD) d[i] = dn[i];
     }
-    vload(t + 1 < t1 ? t + 1 : t);  // next tile's V fragments (L2) under this tile's tail and the next math
-    g = gn, u = un;
-    if (BWD) d = dn;
   }
-  // 4 waves -> one 16 x NC partial (fixed wave order)
+  // per row block: 4 waves -> one 16 x NC partial (fixed wave order)
 #pragma unroll
-  for (int b = 0; b < NRB; ++b)
+  for (int i = 0; i < RBW; ++i) {
+    __syncthreads();  // red reused per row block
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[w][4 * gq + e][16 * b + r] = acc[b][e];
-  __syncthreads();
-  float* wp = ws + ((int64_t)split * gridDim.x + rb) * (16 * NC);
-  for (int i = tid; i < 16 * NC; i += 256) {
-    const int rr = i / NC, cc = i % NC;
-    wp[i] = ((red[0][rr][cc] + red[1][rr][cc]) + red[2][rr][cc]) + red[3][rr][cc];
+    for (int b = 0; b < NRB; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[w][4 * gq + e][16 * b + r] = acc[i][b][e];
+    __syncthreads();
+    float* wp = ws + ((int64_t)split * (gridDim.x * RBW) + rg * RBW + i) * (16 * NC);
+    for (int k = tid; k < 16 * NC; k += 256) {
+      const int rr = k / NC, cc = k % NC;
+      wp[k] = ((red[0][rr][cc] + red[1][rr][cc]) + red[2][rr][cc]) + red[3][rr][cc];
+    }
   }
 }
 
@@ -797,8 +818,17 @@ using namespace mx;
 
 static int lora_env(const char* name, int dflt);
 
+// row blocks of 16 tokens per workgroup sharing the V fragments (MXLLM_SWIGLU_LORA_RBW: 1, 2 or 4;
+// clamped to divide T / 16).  2 by default: 70B backward 273 -> 249 us, headline -2.6 ms (r4p)
+static int swiglu_lora_rbw(int T) {
+  int rbw = lora_env("MXLLM_SWIGLU_LORA_RBW", 2);
+  rbw = rbw >= 4 ? 4 : (rbw >= 2 ? 2 : 1);
+  while (rbw > 1 && (T / 16) % rbw) rbw >>= 1;
+  return rbw;
+}
+
 static int swiglu_lora_splits(int T, int F) {
-  const int tiles = F / 128, rbs = T / 16;
+  const int tiles = F / 128, rbs = T / (16 * swiglu_lora_rbw(T));
   int cs = lora_env("MXLLM_SWIGLU_LORA_CS", 0);
   if (cs <= 0) cs = (512 + rbs - 1) / rbs;  // ~512 workgroups (T 4096: 2 splits; measured best of 1-16, r4h)
   cs = cs < 1 ? 1 : cs;
@@ -822,9 +852,15 @@ extern "C" int mx_swiglu_lora(int bwd, const uint16_t* gu, const uint16_t* dm, u
       ldo < (bwd ? 2 * (int64_t)F : F) + pad || ((uintptr_t)gu | (uintptr_t)out | (uintptr_t)V) % 16 ||
       (bwd && (!dm || (uintptr_t)dm % 16)))
     return (int)hipErrorInvalidValue;
-  const int CS = swiglu_lora_splits(T, F);
-  const dim3 grid(T / 16, CS);
-#define MX_SL(B, N) swiglu_lora_kernel<B, N><<<grid, 256, 0, stream>>>(gu, dm, out, ldo, V, ldv, ws, F, CS)
+  const int CS = swiglu_lora_splits(T, F), RBW = swiglu_lora_rbw(T);
+  const dim3 grid(T / (16 * RBW), CS);
+#define MX_SL_R(B, N, R) swiglu_lora_kernel<B, N, R><<<grid, 256, 0, stream>>>(gu, dm, out, ldo, V, ldv, ws, F, CS)
+#define MX_SL(B, N)                                 \
+  do {                                              \
+    if (RBW == 4) MX_SL_R(B, N, 4);                 \
+    else if (RBW == 2) MX_SL_R(B, N, 2);            \
+    else MX_SL_R(B, N, 1);                          \
+  } while (0)
   if (bwd) {
     switch (nrb) { case 1: MX_SL(true, 1); break; case 2: MX_SL(true, 2); break;
                    case 3: MX_SL(true, 3); break; default: MX_SL(true, 4); break; }
@@ -833,6 +869,7 @@ extern "C" int mx_swiglu_lora(int bwd, const uint16_t* gu, const uint16_t* dm, u
                    case 3: MX_SL(false, 3); break; default: MX_SL(false, 4); break; }
   }
 #undef MX_SL
+#undef MX_SL_R
   swiglu_lora_reduce_kernel<<<T / 16, 256, 0, stream>>>(ws, CS, 16 * nrb, pad, out + (bwd ? 2 * (int64_t)F : F), ldo,
                                                         alpha);
   return (int)hipGetLastError();

@@ -66,14 +66,16 @@ def test_swiglu(gpu, T, F):
     assert rel_err(dgu, guf.grad) < 1e-2
 
 
+@pytest.mark.parametrize("rbw", ["1", "2", "4"])
 @pytest.mark.parametrize("bwd", [False, True])
 @pytest.mark.parametrize("T,F,R", [(16, 128, 16), (48, 384, 32), (1024, 1536, 48), (256, 256, 64), (4096, 28672, 16)])
-def test_swiglu_lora_tail(gpu, T, F, R, bwd):
+def test_swiglu_lora_tail(gpu, T, F, R, bwd, rbw, monkeypatch):
     """SwiGLU fused with the neighbour's LoRA tail (csrc/kernels/lora.hip swiglu_lora_kernel):
     the SwiGLU output is bitwise the plain kernel's, the tail is s out V[:R]^T against fp32,
     zeros past R (V rows past R deliberately non-zero), bit-reproducible."""
     from mxllm.ops.linear import _padded_rows
 
+    monkeypatch.setenv("MXLLM_SWIGLU_LORA_RBW", rbw)  # 16-row blocks per workgroup (clamped to T)
     torch.manual_seed(4)
     pad, s = 64, 2.0
     gu = torch.randn(T, 2 * F, device=gpu, dtype=torch.bfloat16)
