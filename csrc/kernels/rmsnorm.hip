@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const size_t base = (size_t)row * H;
     const float rs = rstd[row];
     float xv[ITERS][8], gv[ITERS][8];
+    u16x8 rv[ITERS];  // the residual gradient, loaded with x / dy so its latency hides under the row sum
     float dot = 0.f;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -112,6 +113,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
       if (c < H) {
         u16x8 a = *reinterpret_cast<const u16x8*>(x + base + c);
         u16x8 d = *reinterpret_cast<const u16x8*>(dy + base + c);
+        if constexpr (DRES) rv[it] = *reinterpret_cast<const u16x8*>(dres + (size_t)row * ldr + c);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xv[it][j] = bf2f(a[j]);
@@ -133,9 +135,8 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
       if (c < H) {
         u16x8 o;
         if constexpr (DRES) {
-          u16x8 r = *reinterpret_cast<const u16x8*>(dres + (size_t)row * ldr + c);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(rs * gv[it][j] - xv[it][j] * k + bf2f(r[j]));
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(rs * gv[it][j] - xv[it][j] * k + bf2f(rv[it][j]));
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = f2bf(rs * gv[it][j] - xv[it][j] * k);
