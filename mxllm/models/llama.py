@@ -162,6 +162,9 @@ DX_IMAGE = tuple(x for x in os.environ.get("MXLLM_DX_IMAGE", "qkv,d").split(",")
 # LoRA projections whose augmented buffer is stored transposed (FusedLinear ``transposed``):
 # forward GEMM in the NN form, input gradient in the TN form, same memory
 LORA_T = tuple(x for x in os.environ.get("MXLLM_LORA_T", "").split(",") if x)
+# full fine-tuning, selective checkpointing: recompute m = swiglu(gu) in the backward of the
+# un-checkpointed layers instead of saving it (Llama._recompute_m)
+RECOMPUTE_SWIGLU = os.environ.get("MXLLM_RECOMPUTE_SWIGLU", "auto")
 
 
 class LlamaLayer(nn.Module):
@@ -256,15 +259,29 @@ class Llama(nn.Module):
         a = layer.wo(o)
         x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps, out_pad=self._pad(layer.wgu),
                                 grad_pad=self._pad(layer.wo))
-        tf, tb = self._swiglu_tails(layer, x)
-        m = ops.swiglu(layer.wgu(x, dy_tail=tb is not None), out_pad=self._pad(layer.wd),
-                       grad_pad=self._pad(layer.wgu), tail_fwd=tf, tail_bwd=tb)
-        d = layer.wd(m, x_tail=tf is not None)
+        if self._recompute_m(layer, i):
+            d = ops.swiglu_linear(layer.wgu(x), layer.wd.weight)  # m = swiglu(gu) recomputed in the backward
+        else:
+            tf, tb = self._swiglu_tails(layer, x)
+            m = ops.swiglu(layer.wgu(x, dy_tail=tb is not None), out_pad=self._pad(layer.wd),
+                           grad_pad=self._pad(layer.wgu), tail_fwd=tf, tail_bwd=tb)
+            d = layer.wd(m, x_tail=tf is not None)
         last = i + 1 == len(self.layers)
         nxt = self.final_norm if last else self.layers[i + 1].attn_norm
         x, h = ops.add_rms_norm(d, h, nxt, cfg.norm_eps, out_pad=0 if last else self._pad(self.layers[i + 1].wqkv),
                                 grad_pad=self._pad(layer.wd))
         return x, h
+
+    def _recompute_m(self, layer, i: int) -> bool:
+        """Recompute the MLP activation m = swiglu(gu) in the backward instead of saving it, in
+        the un-checkpointed layers of a selectively checkpointed run (memory-bound by design:
+        the saved HBM buys more un-checkpointed layers; ``MXLLM_RECOMPUTE_SWIGLU`` 0 / 1 / auto)."""
+        if RECOMPUTE_SWIGLU == "0" or layer.wd.lora_r > 0 or not self.training or not torch.is_grad_enabled():
+            return False
+        if RECOMPUTE_SWIGLU == "1":
+            return True
+        ck = self.activation_checkpointing
+        return not isinstance(ck, bool) and bool(ck) and not ckpt_layer(ck, i)
 
     def _swiglu_tails(self, layer, x: torch.Tensor):
         """LoRA tails the SwiGLU pass writes itself: the down projection's s m A^T (forward)

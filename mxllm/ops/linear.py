@@ -339,6 +339,59 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw
 
 
+def _swiglu_nograd(gu: torch.Tensor) -> torch.Tensor:
+    if use_native(gu):
+        return native().swiglu_fwd(gu.contiguous(), 0)
+    from . import reference as ref
+
+    return ref.swiglu(gu)
+
+
+class _SwiGLULinearFn(torch.autograd.Function):
+    """y = swiglu(gu) W^T that keeps only ``gu`` for the backward and recomputes m = swiglu(gu)
+    there (one elementwise pass) instead of saving it: m is the [T, F] activation of every MLP
+    (70B, 8,192 tokens: 470 MB per layer), so memory-bound runs (selective activation
+    checkpointing, config 4) keep more layers un-checkpointed for the same HBM.  The weight
+    gradient goes the _LinearFn way (direct accumulation into the owner's buffer)."""
+
+    @staticmethod
+    def forward(ctx, gu, w):
+        g2 = gu.reshape(-1, gu.shape[-1])
+        m = _swiglu_nograd(g2)
+        ctx.save_for_backward(g2, w)
+        ctx.wp = w if w.is_leaf else None
+        ctx.gshape = gu.shape
+        return gemm.mm("tn", m, w).view(*gu.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        g2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0])
+        dw = None
+        if ctx.needs_input_grad[1]:
+            m = _swiglu_nograd(g2)
+            dw = param_weight_grad(ctx.wp, dy2, m)
+            del m
+        dgu = None
+        if ctx.needs_input_grad[0]:
+            dm = gemm.mm("nn", dy2, w)
+            if use_native(g2):
+                dgu = native().swiglu_bwd(dm.contiguous(), g2.contiguous(), 0)
+            else:
+                with torch.enable_grad():
+                    gr = g2.detach().requires_grad_(True)
+                    from . import reference as ref
+
+                    (dgu,) = torch.autograd.grad(ref.swiglu(gr), gr, dm)
+            dgu = dgu.view(ctx.gshape)
+        return dgu, dw
+
+
+def swiglu_linear(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Training: ``linear(swiglu(gu), w)`` with m recomputed in the backward (_SwiGLULinearFn)."""
+    return _SwiGLULinearFn.apply(gu, w)
+
+
 # decode-sized GEMMs (bf16, no autograd) on the weight-streaming HIP kernel
 # (csrc/kernels/skinny_gemm.hip) where it beat hipBLASLt inside the decode step
 # (bench/serve_bench.py A/B, profiles/r2x_skinny_gemm.md): one token row for every projection

@@ -622,3 +622,26 @@ def test_engine_embeddings_gpu_match_cpu(gpu):
         eng.stop()
     assert got.shape == want.shape
     assert (torch.nn.functional.cosine_similarity(got, want, dim=1) > 0.995).all()
+
+
+def test_swiglu_recompute_bitwise_gpu(gpu, monkeypatch):
+    """Selective checkpointing on the HIP path: recomputing m = swiglu(gu) in the backward of the
+    un-checkpointed layers gives bitwise the loss and gradients of saving m (same kernels)."""
+    import mxllm.models.llama as L
+    from mxllm.models import get_config
+
+    cfg = get_config("tiny-d128").replace(n_layers=3)
+    ids = torch.randint(0, cfg.vocab_size, (2, 128), device=gpu, generator=torch.Generator(device=gpu).manual_seed(0))
+
+    def run(policy):
+        monkeypatch.setattr(L, "RECOMPUTE_SWIGLU", policy)
+        m = L.Llama(cfg, device=gpu, seed=4, activation_checkpointing=1)
+        loss = m(ids, ids)
+        loss.backward()
+        return float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()}
+
+    l0, g0 = run("0")
+    l1, g1 = run("auto")
+    assert l0 == l1
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
