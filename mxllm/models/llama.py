@@ -200,6 +200,7 @@ class Llama(nn.Module):
         self.lora = lora_r > 0
         train_base = not self.lora
         self.activation_checkpointing = activation_checkpointing
+        self.mlp_recompute_ckpt = None  # checkpoint spec of a trainer that runs _layer itself (ZeRO-3)
         self.seq_parallel = None  # UlyssesAttention when the sequence is sharded (set_sequence_parallel)
         # optional ``fn(params)`` called before the parameters are first used in a forward (ZeRO-1: wait for
         # their all-gather; mxllm/parallel/zero1.py) — None = parameters are always resident
@@ -280,7 +281,7 @@ class Llama(nn.Module):
             return False
         if RECOMPUTE_SWIGLU == "1":
             return True
-        ck = self.activation_checkpointing
+        ck = self.mlp_recompute_ckpt if self.mlp_recompute_ckpt is not None else self.activation_checkpointing
         return not isinstance(ck, bool) and bool(ck) and not ckpt_layer(ck, i)
 
     def _swiglu_tails(self, layer, x: torch.Tensor):

@@ -431,6 +431,7 @@ class Zero3Trainer:
         model = Llama(cfg, device="meta", init=False)
         _realize_on(model, dev)
         self.model = model
+        model.mlp_recompute_ckpt = activation_checkpointing  # _layer's recompute-m policy follows our checkpointing
         units = unit_layout(model)
         self.units = [Unit(k, ps, self.world, self.rank, comm, res) for k, (_, ps, res) in enumerate(units)]
         self.unit_names = [u[0] for u in units]

@@ -31,6 +31,11 @@ def _run(rank, world, port, q, mode, steps):
     from mxllm.train.trainer import OptimConfig, Trainer
 
     env = runtime.init(rank=rank, world_size=world)
+    import mxllm.ops as mops
+
+    recomputed = []  # selective checkpointing: the un-checkpointed layer recomputes m = swiglu(gu)
+    _swl = mops.swiglu_linear
+    mops.swiglu_linear = lambda *a: (recomputed.append(1), _swl(*a))[1]
     # "..._bf16": bf16 gradient reduction in both trainers (default: fp32 in both)
     gdt = torch.bfloat16 if mode.endswith("_bf16") else torch.float32
     mode = mode.removesuffix("_bf16")
@@ -59,6 +64,10 @@ def _run(rank, world, port, q, mode, steps):
     mbs = [(mine[:1], mine[:1]), (mine[1:], mine[1:])] if acc2 else [(mine, mine)]
     for s in range(steps):
         losses.append(float(tr.train_step(mbs)))
+    if mode == "zero3_ckpt2":
+        assert len(recomputed) == steps * len(mbs), recomputed
+    elif mode in ("zero3", "zero3_ckpt"):
+        assert not recomputed
     if mode.startswith("zero3") and world > 1:
         # the default runs gathers and reduce-scatters on two communicators (split RCCL streams)
         assert tr.comm.rs_pg is not None and tr.comm.rs_pg is not tr.comm.ag_pg
