@@ -307,6 +307,22 @@ at::Tensor swiglu_bwd(const at::Tensor& dm, const at::Tensor& gu, int64_t out_pa
   return dgu;
 }
 
+// swiglu_bwd that also re-emits m = swiglu(gu) (bitwise the forward's) from the same read of gu:
+// the backward of a linear whose input activation was recomputed instead of saved
+std::vector<at::Tensor> swiglu_bwd_m(const at::Tensor& dm, const at::Tensor& gu) {
+  check_bf16(dm, "dm");
+  check_bf16(gu, "gu");
+  DevGuard g(gu.device());
+  const int64_t F2 = gu.size(-1);
+  const int64_t T = gu.numel() / F2;
+  MX_CHECK(dm.numel() == T * (F2 / 2), "dm shape mismatch");
+  MX_CHECK(dm.is_contiguous() && gu.is_contiguous(), "swiglu_bwd_m: dense dm / gu");
+  at::Tensor dgu = at::empty_like(gu);
+  at::Tensor m = at::empty({T, F2 / 2}, gu.options());
+  if (T > 0) MX_OK(mx_swiglu_bwd(bf(dm), bf(gu), bfm(dgu), T, (int)(F2 / 2), F2, cur_stream(), bfm(m)));
+  return {dgu, m};
+}
+
 // SwiGLU fused with the LoRA tail of its augmented-GEMM neighbour (csrc/kernels/lora.hip):
 // fwd: m [T, F] in a [T, F + pad] buffer, tail = alpha m v^T (v [>= 16 nrb, F] row view);
 // bwd: dgu [T, 2F] in a [T, 2F + pad] buffer, tail = alpha dgu v^T (v [>= 16 nrb, 2F]).
@@ -1064,6 +1080,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
+  m.def("swiglu_bwd_m(Tensor dm, Tensor gu) -> Tensor[]");
   m.def("adamw_step(Tensor(a!)? master, Tensor(e!) grad, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? lowp, Tensor(f!)? lo, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, Tensor? scale_t, float scale_f, bool zero_grad=False) -> ()");
   m.def("split_master(Tensor x, Tensor(a!) hi, Tensor(b!) lo) -> ()");
   m.def("join_master(Tensor hi, Tensor lo, Tensor(a!) out) -> ()");
@@ -1113,6 +1130,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("sqnorm", &sqnorm);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("swiglu_bwd_m", &swiglu_bwd_m);
   m.impl("adamw_step", &adamw_step);
   m.impl("split_master", &split_master);
   m.impl("join_master", &join_master);

@@ -27,7 +27,7 @@ extern "C" {
 // elementwise.hip
 int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, int64_t ldm, hipStream_t stream);
 int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
-                  hipStream_t stream);
+                  hipStream_t stream, uint16_t* m = nullptr);
 int mx_ce_inv_count(const int64_t* labels, int64_t T, int64_t ignore, float* inv_n, hipStream_t stream);
 int mx_ce_chunk(uint16_t* logits, const int64_t* labels, float* losses, const float* inv_n, int64_t T, int V,
                 int64_t ignore, hipStream_t stream);

@@ -36,10 +36,14 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restr
 }
 
 // dg = dm * u * s * (1 + g (1 - s)),  du = dm * g * s,  s = sigmoid(g)
+// WM: also re-emit m = g s u (the forward's expression: bitwise its output) for a backward that
+// recomputes the activation instead of saving it (mxllm/ops/linear.py _SwiGLULinearFn): gu is
+// read once for both
+template <bool WM>
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ dm,
                                                          const uint16_t* __restrict__ gu,
                                                          uint16_t* __restrict__ dgu, int64_t T, int F,
-                                                         int64_t ldg) {
+                                                         int64_t ldg, uint16_t* __restrict__ m) {
   const int64_t per_row = F / 8;
   const int64_t n = T * per_row;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -49,17 +53,19 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
     u16x8 g = *reinterpret_cast<const u16x8*>(row + c);
     u16x8 u = *reinterpret_cast<const u16x8*>(row + F + c);
     u16x8 d = *reinterpret_cast<const u16x8*>(dm + t * (int64_t)F + c);
-    u16x8 og, ou;
+    u16x8 og, ou, om;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
       const float s = sigmoid_f(gf);
       og[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
       ou[j] = f2bf(df * gf * s);
+      if constexpr (WM) om[j] = f2bf(gf * s * uf);
     }
     uint16_t* orow = dgu + t * ldg;
     *reinterpret_cast<u16x8*>(orow + c) = og;
     *reinterpret_cast<u16x8*>(orow + F + c) = ou;
+    if constexpr (WM) *reinterpret_cast<u16x8*>(m + t * (int64_t)F + c) = om;
   }
 }
 
@@ -322,10 +328,14 @@ extern "C" int mx_swiglu_fwd(const uint16_t* gu, uint16_t* m, int64_t T, int F, 
   return (int)hipGetLastError();
 }
 
+// m (optional, [T, F] dense): also write the recomputed activation
 extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* dgu, int64_t T, int F, int64_t ldg,
-                             hipStream_t stream) {
+                             hipStream_t stream, uint16_t* m) {
   if (F % 8 || ldg < 2 * (int64_t)F || ldg % 8) return -1;
-  swiglu_bwd_kernel<<<grid_for(T * (F / 8)), 256, 0, stream>>>(dm, gu, dgu, T, F, ldg);
+  if (m)
+    swiglu_bwd_kernel<true><<<grid_for(T * (F / 8)), 256, 0, stream>>>(dm, gu, dgu, T, F, ldg, m);
+  else
+    swiglu_bwd_kernel<false><<<grid_for(T * (F / 8)), 256, 0, stream>>>(dm, gu, dgu, T, F, ldg, nullptr);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 4 pass S: same-box A/B of the config-4 proxy, m = swiglu(gu) saved (MXLLM_RECOMPUTE_SWIGLU=0)
+# vs recomputed in the un-checkpointed layers, at 40 / 24 checkpointed layers, then recompute at 16
+OUT=gpurun_out/r4s; mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+run() {  # name recompute ck
+  C4="--model llama3.1-70b --finetune full --parallel zero3 --act-ckpt --act-ckpt-layers $3 --micro-batch 4 --emulate-world 8 --steps 3 --warmup 2 --no-calibrate"
+  MXLLM_RECOMPUTE_SWIGLU=$2 timeout -k 10 400 python -u bench.py $C4 --json-out $OUT/$1.json > $OUT/$1.log 2>&1 || { echo "$1 rc=$?"; tail -3 $OUT/$1.log; return 1; }
+  echo "$1: $(python -c "import json;j=json.load(open('$OUT/$1.json'));print(j['ms_per_step'],j['value'],j['peak_hbm_gb'],j['peak_hbm_reserved_gb'])")"
+}
+run ck40_saved 0 40 && run ck40_rec auto 40 && run ck24_saved 0 24 && run ck24_rec auto 24 && run ck16_rec auto 16 && \
+run ck40_saved_b 0 40 && run ck40_rec_b auto 40

@@ -367,23 +367,29 @@ class _SwiGLULinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         g2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
-        dw = None
-        if ctx.needs_input_grad[1]:
-            m = _swiglu_nograd(g2)
-            dw = param_weight_grad(ctx.wp, dy2, m)
-            del m
-        dgu = None
-        if ctx.needs_input_grad[0]:
+        dgu = dw = None
+        if use_native(g2):
+            # dm first: one pass over (dm, gu) then writes dgu AND the recomputed m for dW
             dm = gemm.mm("nn", dy2, w)
-            if use_native(g2):
-                dgu = native().swiglu_bwd(dm.contiguous(), g2.contiguous(), 0)
-            else:
-                with torch.enable_grad():
-                    gr = g2.detach().requires_grad_(True)
-                    from . import reference as ref
+            dgu, m = native().swiglu_bwd_m(dm.contiguous(), g2.contiguous())
+            del dm
+            if ctx.needs_input_grad[1]:
+                dw = param_weight_grad(ctx.wp, dy2, m)
+            del m
+        else:
+            from . import reference as ref
 
-                    (dgu,) = torch.autograd.grad(ref.swiglu(gr), gr, dm)
+            with torch.enable_grad():
+                gr = g2.detach().requires_grad_(True)
+                m = ref.swiglu(gr)
+            if ctx.needs_input_grad[1]:
+                dw = param_weight_grad(ctx.wp, dy2, m.detach())
+            if ctx.needs_input_grad[0]:
+                (dgu,) = torch.autograd.grad(m, gr, gemm.mm("nn", dy2, w))
+        if dgu is not None and ctx.needs_input_grad[0]:
             dgu = dgu.view(ctx.gshape)
+        else:
+            dgu = None
         return dgu, dw
 
 

@@ -64,6 +64,9 @@ def test_swiglu(gpu, T, F):
     mr.backward(dm.float())
     dgu = _ops().swiglu_bwd(dm, gu)
     assert rel_err(dgu, guf.grad) < 1e-2
+    # the recompute backward: same dgu and bitwise the forward's m from one pass over gu
+    dgu2, m2 = _ops().swiglu_bwd_m(dm, gu)
+    assert torch.equal(dgu2, dgu) and torch.equal(m2, m)
 
 
 @pytest.mark.parametrize("rbw", ["1", "2", "4"])
