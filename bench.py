@@ -356,23 +356,29 @@ def run_config3(a, world: int) -> dict:
     return res
 
 
-# config 4 per-rank HBM model (70B, micro-batch 4 x 2048, world-8 shards; profiles/r4g/c4_ck*.json):
-# reserved peak = 223.5 GB with the first 56 layers checkpointed, +1.98 GB per layer fewer;
-# margin: RCCL buffers of the two ZeRO-3 communicators + allocator slack of the real 8-rank job
-CONFIG4_RESERVED = (56, 223.5, 1.98)
+# config 4 per-rank HBM model (70B, micro-batch 4 x 2048, world-8 shards): reserved peak = r0 GB with
+# the first n0 layers checkpointed, +per GB for each layer fewer.  With m = swiglu(gu) recomputed in
+# the un-checkpointed layers (MXLLM_RECOMPUTE_SWIGLU, default) a layer costs 0.47 GB less
+# (profiles/r4_recompute/: 237.8 / 250.0 / 262.5 / 274.9 GB at 40 / 32 / 24 / 16); saving m:
+# profiles/r4g/c4_ck*.json.  Margin: RCCL buffers of the two ZeRO-3 communicators + allocator slack
+# of the real 8-rank job
+CONFIG4_RESERVED = (40, 237.8, 1.56)
+CONFIG4_RESERVED_SAVED_M = (56, 223.5, 1.98)
 CONFIG4_MARGIN_GB = 14.0
+CONFIG4_DEPTHS = (16, 24, 32, 40, 48, 56, 64, 80)
 
 
 def config4_plan(a, free_gb: float | None) -> tuple[int | None, float]:
     """(checkpointed layers, HBM needed) for the config-4 child: ``--config4-act-ckpt-layers``
-    when given, else the fewest of 40 / 48 / 56 / 64 / 80 that fit ``free_gb``; (None, need of
-    80) when even full checkpointing does not fit."""
-    n0, r0, per = CONFIG4_RESERVED
+    when given, else the fewest of CONFIG4_DEPTHS that fit ``free_gb``; (None, need of 80) when
+    even full checkpointing does not fit."""
+    saved_m = os.environ.get("MXLLM_RECOMPUTE_SWIGLU", "auto") == "0"
+    n0, r0, per = CONFIG4_RESERVED_SAVED_M if saved_m else CONFIG4_RESERVED
     need = lambda ck: r0 + (n0 - ck) * per + CONFIG4_MARGIN_GB  # noqa: E731
     if a.config4_act_ckpt_layers is not None:
         ck = a.config4_act_ckpt_layers
         return (ck if free_gb is None or free_gb >= need(ck) else None), need(ck)
-    for ck in (40, 48, 56, 64, 80):
+    for ck in CONFIG4_DEPTHS:
         if free_gb is None or free_gb >= need(ck):
             return ck, need(ck)
     return None, need(80)
@@ -380,22 +386,27 @@ def config4_plan(a, free_gb: float | None) -> tuple[int | None, float]:
 
 def run_config4_planned(a, world: int, free_gb: float | None) -> dict:
     """Config-4 child with the checkpoint depth from ``config4_plan``; a failed child (e.g. RCCL
-    buffers beyond the HBM model) is rerun once with every layer checkpointed -- insurance for the
-    one real 8-rank measurement.  The plan (and a failed first attempt) is recorded as ``hbm_plan``."""
+    buffers beyond the HBM model) is rerun with 40 layers checkpointed (~37 GB more headroom than
+    16), then with every layer -- insurance for the one real 8-rank measurement.  The plan (and the
+    failed attempts) is recorded as ``hbm_plan``."""
     ck, need = config4_plan(a, free_gb)
     if ck is None:
         return {"skipped": f"min free HBM over the ranks {free_gb:.1f} GB < {need:.0f} GB the "
                            f"config-4 child needs with every layer checkpointed"}
     res = run_config4(a, world, ck)
-    first = None
-    if "error" in res and a.config4_act_ckpt_layers is None and ck < 80:
-        first = {"checkpointed_layers": ck, "error": res["error"]}
-        ck = 80
-        res = run_config4(a, world, ck)
+    failed = []
+    if a.config4_act_ckpt_layers is None:
+        for retry in (40, 80):
+            if "error" not in res or retry <= ck:
+                continue
+            failed.append({"checkpointed_layers": ck, "error": res["error"]})
+            ck = retry
+            res = run_config4(a, world, ck)
     res["hbm_plan"] = {"min_free_hbm_gb": None if free_gb is None else round(free_gb, 1),
                        "need_gb": round(need, 1), "checkpointed_layers": ck}
-    if first is not None:
-        res["hbm_plan"]["first_attempt"] = first
+    if failed:
+        res["hbm_plan"]["first_attempt"] = failed[0]
+        res["hbm_plan"]["failed_attempts"] = failed
     return res
 
 

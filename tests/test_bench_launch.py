@@ -121,7 +121,7 @@ def test_memory_guard_checkpoints_only_when_short(monkeypatch):
     assert bench.memory_guard(a, types.SimpleNamespace(device=torch.device("cuda", 0), world_size=1)) is None
 
 
-def test_config4_plan_fits_free_hbm():
+def test_config4_plan_fits_free_hbm(monkeypatch):
     """The config-4 child checkpoints the fewest layers whose modelled per-rank peak + margin fits
     the smallest free HBM over the ranks; an explicit depth is honoured or skipped."""
     import argparse
@@ -129,34 +129,45 @@ def test_config4_plan_fits_free_hbm():
     import bench
 
     a = argparse.Namespace(config4_act_ckpt_layers=None)
-    assert bench.config4_plan(a, 308.0)[0] == 40
-    assert bench.config4_plan(a, 262.0)[0] == 48
+    assert bench.config4_plan(a, 308.0)[0] == 16
+    assert bench.config4_plan(a, 268.0)[0] == 32
     assert bench.config4_plan(a, 200.0)[0] == 80
     assert bench.config4_plan(a, 150.0)[0] is None
-    assert bench.config4_plan(a, None)[0] == 40  # CPU rehearsal: no HBM to check
+    assert bench.config4_plan(a, None)[0] == 16  # CPU rehearsal: no HBM to check
     a.config4_act_ckpt_layers = 24
     assert bench.config4_plan(a, 308.0)[0] == 24 and bench.config4_plan(a, 250.0)[0] is None
+    a.config4_act_ckpt_layers = None  # m saved (MXLLM_RECOMPUTE_SWIGLU=0): the round-3 HBM model
+    monkeypatch.setenv("MXLLM_RECOMPUTE_SWIGLU", "0")
+    assert bench.config4_plan(a, 308.0)[0] == 24 and bench.config4_plan(a, 262.0)[0] == 48
 
 
-def test_config4_failed_child_is_retried_fully_checkpointed(monkeypatch):
-    """A failed config-4 child (the one real 8-rank measurement) is rerun once with every layer
-    checkpointed, and the first attempt is recorded; an explicit depth is not second-guessed."""
+def test_config4_failed_child_is_retried_deeper(monkeypatch):
+    """A failed config-4 child (the one real 8-rank measurement) is rerun with 40 layers
+    checkpointed, then with every layer, and the failed attempts are recorded; an explicit depth
+    is not second-guessed."""
     import argparse
 
     import bench
 
     calls = []
+    fails = [1]
 
     def fake(a, world, ck):
         calls.append(ck)
-        return {"error": "child job exit code 1"} if len(calls) == 1 else {"ms_per_step": 1.0}
+        return {"error": "child job exit code 1"} if len(calls) <= fails[0] else {"ms_per_step": 1.0}
 
     monkeypatch.setattr(bench, "run_config4", fake)
     a = argparse.Namespace(config4_act_ckpt_layers=None)
     r = bench.run_config4_planned(a, 8, 308.0)
-    assert calls == [40, 80] and r["ms_per_step"] == 1.0
-    assert r["hbm_plan"]["checkpointed_layers"] == 80 and r["hbm_plan"]["first_attempt"]["checkpointed_layers"] == 40
+    assert calls == [16, 40] and r["ms_per_step"] == 1.0
+    assert r["hbm_plan"]["checkpointed_layers"] == 40 and r["hbm_plan"]["first_attempt"]["checkpointed_layers"] == 16
     calls.clear()
+    fails[0] = 2
+    r = bench.run_config4_planned(a, 8, 308.0)
+    assert calls == [16, 40, 80] and r["hbm_plan"]["checkpointed_layers"] == 80
+    assert [f["checkpointed_layers"] for f in r["hbm_plan"]["failed_attempts"]] == [16, 40]
+    calls.clear()
+    fails[0] = 1
     a.config4_act_ckpt_layers = 56
     r = bench.run_config4_planned(a, 8, 308.0)
     assert calls == [56] and "error" in r
