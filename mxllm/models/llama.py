@@ -165,6 +165,9 @@ LORA_T = tuple(x for x in os.environ.get("MXLLM_LORA_T", "").split(",") if x)
 # full fine-tuning, selective checkpointing: recompute m = swiglu(gu) in the backward of the
 # un-checkpointed layers instead of saving it (Llama._recompute_m)
 RECOMPUTE_SWIGLU = os.environ.get("MXLLM_RECOMPUTE_SWIGLU", "auto")
+# same layers: the normed inputs of the qkv and gate-up projections are recomputed from the
+# residual stream in their backward instead of saved (ops.normed_linear); 0 = save them
+RECOMPUTE_NORM = os.environ.get("MXLLM_RECOMPUTE_NORM", "auto")
 
 
 class LlamaLayer(nn.Module):
@@ -249,7 +252,9 @@ class Llama(nn.Module):
     def _layer(self, i: int, x: torch.Tensor, h: torch.Tensor, B: int, S: int):
         cfg = self.cfg
         layer = self.layers[i]
-        qkv = layer.wqkv(x)
+        rec = self._recompute_m(layer, i)
+        rec_x = rec and RECOMPUTE_NORM != "0"
+        qkv = ops.normed_linear(x, h, layer.attn_norm, cfg.norm_eps, layer.wqkv.weight) if rec_x else layer.wqkv(x)
         if self.seq_parallel is not None:
             o = self.seq_parallel(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads,
                                   cfg.head_dim, causal=True)
@@ -260,8 +265,9 @@ class Llama(nn.Module):
         a = layer.wo(o)
         x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps, out_pad=self._pad(layer.wgu),
                                 grad_pad=self._pad(layer.wo))
-        if self._recompute_m(layer, i):
-            d = ops.swiglu_linear(layer.wgu(x), layer.wd.weight)  # m = swiglu(gu) recomputed in the backward
+        if rec:  # m = swiglu(gu) (and the gate-up input x) recomputed in the backward
+            gu = ops.normed_linear(x, h, layer.mlp_norm, cfg.norm_eps, layer.wgu.weight) if rec_x else layer.wgu(x)
+            d = ops.swiglu_linear(gu, layer.wd.weight)
         else:
             tf, tb = self._swiglu_tails(layer, x)
             m = ops.swiglu(layer.wgu(x, dy_tail=tb is not None), out_pad=self._pad(layer.wd),
@@ -274,15 +280,17 @@ class Llama(nn.Module):
         return x, h
 
     def _recompute_m(self, layer, i: int) -> bool:
-        """Recompute the MLP activation m = swiglu(gu) in the backward instead of saving it, in
-        the un-checkpointed layers of a selectively checkpointed run (memory-bound by design:
-        the saved HBM buys more un-checkpointed layers; ``MXLLM_RECOMPUTE_SWIGLU`` 0 / 1 / auto)."""
+        """Recompute the MLP activation m = swiglu(gu) (and, unless ``MXLLM_RECOMPUTE_NORM`` = 0,
+        the normed qkv / gate-up inputs) in the backward instead of saving them, in the
+        un-checkpointed layers of a selectively checkpointed run -- including one that checkpoints
+        0 layers (memory-bound by design: the saved HBM buys more un-checkpointed layers;
+        ``MXLLM_RECOMPUTE_SWIGLU`` 0 / 1 / auto)."""
         if RECOMPUTE_SWIGLU == "0" or layer.wd.lora_r > 0 or not self.training or not torch.is_grad_enabled():
             return False
         if RECOMPUTE_SWIGLU == "1":
             return True
         ck = self.mlp_recompute_ckpt if self.mlp_recompute_ckpt is not None else self.activation_checkpointing
-        return not isinstance(ck, bool) and bool(ck) and not ckpt_layer(ck, i)
+        return not isinstance(ck, bool) and ck is not None and not ckpt_layer(ck, i)
 
     def _swiglu_tails(self, layer, x: torch.Tensor):
         """LoRA tails the SwiGLU pass writes itself: the down projection's s m A^T (forward)

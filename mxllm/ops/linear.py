@@ -398,6 +398,45 @@ def swiglu_linear(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return _SwiGLULinearFn.apply(gu, w)
 
 
+class _NormedLinearFn(torch.autograd.Function):
+    """y = x W^T for x = rmsnorm(h) * nw that does not save x: the backward recomputes it from the
+    residual h the norm node keeps anyway (bitwise: csrc/kernels/rmsnorm.hip normalises the stored
+    bf16 h in both variants), one [T, H] pass instead of a saved [T, H] activation per projection
+    (70B, 8,192 tokens: 134 MB each for the qkv and gate-up inputs of every layer)."""
+
+    @staticmethod
+    def forward(ctx, x, h, nw, eps, w):
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(h, nw, w)
+        ctx.wp = w if w.is_leaf else None
+        ctx.eps, ctx.xshape = eps, x.shape
+        return gemm.mm("tn", x2, w).view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, nw, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0])
+        dx = gemm.mm("nn", dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[4]:
+            h2 = h.reshape(-1, h.shape[-1])
+            if use_native(h2):
+                x2 = native().rmsnorm_fwd(h2.contiguous(), None, nw, ctx.eps, 0)[0]
+            else:
+                from . import reference as ref
+
+                x2 = ref.rms_norm(h2, nw, ctx.eps)
+            dw = param_weight_grad(ctx.wp, dy2, x2)
+            del x2
+        return dx, None, None, None, dw
+
+
+def normed_linear(x: torch.Tensor, h: torch.Tensor, nw: torch.Tensor, eps: float, w: torch.Tensor) -> torch.Tensor:
+    """Training: ``linear(x, w)`` where x = rms_norm(h, nw, eps), x recomputed in the backward
+    (_NormedLinearFn)."""
+    return _NormedLinearFn.apply(x, h, nw, eps, w)
+
+
 # decode-sized GEMMs (bf16, no autograd) on the weight-streaming HIP kernel
 # (csrc/kernels/skinny_gemm.hip) where it beat hipBLASLt inside the decode step
 # (bench/serve_bench.py A/B, profiles/r2x_skinny_gemm.md): one token row for every projection

@@ -625,23 +625,25 @@ def test_engine_embeddings_gpu_match_cpu(gpu):
 
 
 def test_swiglu_recompute_bitwise_gpu(gpu, monkeypatch):
-    """Selective checkpointing on the HIP path: recomputing m = swiglu(gu) in the backward of the
-    un-checkpointed layers gives bitwise the loss and gradients of saving m (same kernels)."""
+    """Selective checkpointing on the HIP path: recomputing m = swiglu(gu) and the normed projection
+    inputs in the backward of the un-checkpointed layers gives bitwise the loss and gradients of
+    saving them (same kernels)."""
     import mxllm.models.llama as L
     from mxllm.models import get_config
 
     cfg = get_config("tiny-d128").replace(n_layers=3)
     ids = torch.randint(0, cfg.vocab_size, (2, 128), device=gpu, generator=torch.Generator(device=gpu).manual_seed(0))
 
-    def run(policy):
+    def run(policy, ck=1):
         monkeypatch.setattr(L, "RECOMPUTE_SWIGLU", policy)
-        m = L.Llama(cfg, device=gpu, seed=4, activation_checkpointing=1)
+        m = L.Llama(cfg, device=gpu, seed=4, activation_checkpointing=ck)
         loss = m(ids, ids)
         loss.backward()
         return float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
     l0, g0 = run("0")
-    l1, g1 = run("auto")
-    assert l0 == l1
-    for k in g0:
-        assert torch.equal(g0[k], g1[k]), k
+    for ck in (1, 0):  # also the normed qkv / gate-up inputs (ops.normed_linear), every layer at ck 0
+        l1, g1 = run("auto", ck)
+        assert l0 == l1
+        for k in g0:
+            assert torch.equal(g0[k], g1[k]), (ck, k)

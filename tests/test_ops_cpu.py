@@ -362,27 +362,31 @@ def test_chunked_linear_cross_entropy_matches_reference():
 
 def test_swiglu_linear_recompute_matches_saved_activation(monkeypatch):
     """Full fine-tuning with selective checkpointing: the un-checkpointed layers recompute the MLP
-    activation m = swiglu(gu) in the backward instead of saving it (mxllm/ops/linear.py
-    _SwiGLULinearFn); loss and every gradient equal the saved-m path."""
+    activation m = swiglu(gu) (mxllm/ops/linear.py _SwiGLULinearFn) and the normed qkv / gate-up
+    inputs (_NormedLinearFn) in the backward instead of saving them; loss and every gradient equal
+    the saving path, also with 0 layers checkpointed."""
     import mxllm.models.llama as L
     from mxllm.models import get_config
 
     cfg = get_config("tiny").replace(n_layers=3)
     ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=torch.Generator().manual_seed(0))
 
-    def run(policy):
+    def run(policy, norm="auto", ck=1):
         monkeypatch.setattr(L, "RECOMPUTE_SWIGLU", policy)
-        m = L.Llama(cfg, device="cpu", dtype=torch.float32, seed=4, activation_checkpointing=1)
-        calls = []
-        real = L.ops.swiglu_linear
+        monkeypatch.setattr(L, "RECOMPUTE_NORM", norm)
+        m = L.Llama(cfg, device="cpu", dtype=torch.float32, seed=4, activation_checkpointing=ck)
+        calls, ncalls = [], []
+        real, nreal = L.ops.swiglu_linear, L.ops.normed_linear
         monkeypatch.setattr(L.ops, "swiglu_linear", lambda gu, w: calls.append(1) or real(gu, w))
+        monkeypatch.setattr(L.ops, "normed_linear", lambda *a: ncalls.append(1) or nreal(*a))
         loss = m(ids, ids)
         loss.backward()
-        return float(loss), {n: p.grad.clone() for n, p in m.named_parameters()}, len(calls)
+        return float(loss), {n: p.grad.clone() for n, p in m.named_parameters()}, len(calls), len(ncalls)
 
-    l0, g0, n0 = run("0")
-    l1, g1, n1 = run("auto")
-    assert n0 == 0 and n1 == 2  # layers 1 and 2 are not checkpointed
-    assert abs(l0 - l1) < 1e-6
-    for k in g0:
-        torch.testing.assert_close(g1[k], g0[k], rtol=1e-5, atol=1e-6)
+    l0, g0, n0, k0 = run("0")
+    for args, (n_m, n_x) in ((("auto",), (2, 4)), (("auto", "0"), (2, 0)), (("auto", "auto", 0), (3, 6))):
+        l1, g1, n1, k1 = run(*args)
+        assert (n0, k0) == (0, 0) and (n1, k1) == (n_m, n_x), args  # ck 1: layers 1 and 2 recompute
+        assert abs(l0 - l1) < 1e-6
+        for k in g0:
+            torch.testing.assert_close(g1[k], g0[k], rtol=1e-5, atol=1e-6)
