@@ -357,23 +357,29 @@ def run_config3(a, world: int) -> dict:
 
 
 # config 4 per-rank HBM model (70B, micro-batch 4 x 2048, world-8 shards): reserved peak = r0 GB with
-# the first n0 layers checkpointed, +per GB for each layer fewer.  With m = swiglu(gu) recomputed in
-# the un-checkpointed layers (MXLLM_RECOMPUTE_SWIGLU, default) a layer costs 0.47 GB less
-# (profiles/r4_recompute/: 237.8 / 250.0 / 262.5 / 274.9 GB at 40 / 32 / 24 / 16); saving m:
-# profiles/r4g/c4_ck*.json.  Margin: RCCL buffers of the two ZeRO-3 communicators + allocator slack
-# of the real 8-rank job
-CONFIG4_RESERVED = (40, 237.8, 1.56)
+# the first n0 layers checkpointed, +per GB for each layer fewer.  The un-checkpointed layers
+# recompute m = swiglu(gu) (MXLLM_RECOMPUTE_SWIGLU) and the normed qkv / gate-up inputs
+# (MXLLM_RECOMPUTE_NORM) in the backward by default: 258.2 / 268.4 / 278.6 GB at 16 / 8 / 0
+# (profiles/r4_recompute/pass_u_*.json); m only: 237.8 GB at 40, +1.52 per layer (pass R);
+# nothing recomputed: profiles/r4g/c4_ck*.json.  Margin: RCCL buffers of the two ZeRO-3
+# communicators + allocator slack of the real 8-rank job
+CONFIG4_RESERVED = (16, 258.2, 1.30)
+CONFIG4_RESERVED_M_ONLY = (40, 237.8, 1.56)
 CONFIG4_RESERVED_SAVED_M = (56, 223.5, 1.98)
 CONFIG4_MARGIN_GB = 14.0
-CONFIG4_DEPTHS = (16, 24, 32, 40, 48, 56, 64, 80)
+CONFIG4_DEPTHS = (0, 8, 16, 24, 32, 40, 48, 56, 64, 80)
 
 
 def config4_plan(a, free_gb: float | None) -> tuple[int | None, float]:
     """(checkpointed layers, HBM needed) for the config-4 child: ``--config4-act-ckpt-layers``
     when given, else the fewest of CONFIG4_DEPTHS that fit ``free_gb``; (None, need of 80) when
     even full checkpointing does not fit."""
-    saved_m = os.environ.get("MXLLM_RECOMPUTE_SWIGLU", "auto") == "0"
-    n0, r0, per = CONFIG4_RESERVED_SAVED_M if saved_m else CONFIG4_RESERVED
+    if os.environ.get("MXLLM_RECOMPUTE_SWIGLU", "auto") == "0":
+        n0, r0, per = CONFIG4_RESERVED_SAVED_M
+    elif os.environ.get("MXLLM_RECOMPUTE_NORM", "auto") == "0":
+        n0, r0, per = CONFIG4_RESERVED_M_ONLY
+    else:
+        n0, r0, per = CONFIG4_RESERVED
     need = lambda ck: r0 + (n0 - ck) * per + CONFIG4_MARGIN_GB  # noqa: E731
     if a.config4_act_ckpt_layers is not None:
         ck = a.config4_act_ckpt_layers
@@ -386,8 +392,8 @@ def config4_plan(a, free_gb: float | None) -> tuple[int | None, float]:
 
 def run_config4_planned(a, world: int, free_gb: float | None) -> dict:
     """Config-4 child with the checkpoint depth from ``config4_plan``; a failed child (e.g. RCCL
-    buffers beyond the HBM model) is rerun with 40 layers checkpointed (~37 GB more headroom than
-    16), then with every layer -- insurance for the one real 8-rank measurement.  The plan (and the
+    buffers beyond the HBM model) is rerun with 40 layers checkpointed (~50 GB more headroom than
+    0), then with every layer -- insurance for the one real 8-rank measurement.  The plan (and the
     failed attempts) is recorded as ``hbm_plan``."""
     ck, need = config4_plan(a, free_gb)
     if ck is None:

@@ -129,15 +129,17 @@ def test_config4_plan_fits_free_hbm(monkeypatch):
     import bench
 
     a = argparse.Namespace(config4_act_ckpt_layers=None)
-    assert bench.config4_plan(a, 308.0)[0] == 16
-    assert bench.config4_plan(a, 268.0)[0] == 32
+    assert bench.config4_plan(a, 308.0)[0] == 0
+    assert bench.config4_plan(a, 268.0)[0] == 24
     assert bench.config4_plan(a, 200.0)[0] == 80
     assert bench.config4_plan(a, 150.0)[0] is None
-    assert bench.config4_plan(a, None)[0] == 16  # CPU rehearsal: no HBM to check
+    assert bench.config4_plan(a, None)[0] == 0  # CPU rehearsal: no HBM to check
     a.config4_act_ckpt_layers = 24
     assert bench.config4_plan(a, 308.0)[0] == 24 and bench.config4_plan(a, 250.0)[0] is None
-    a.config4_act_ckpt_layers = None  # m saved (MXLLM_RECOMPUTE_SWIGLU=0): the round-3 HBM model
-    monkeypatch.setenv("MXLLM_RECOMPUTE_SWIGLU", "0")
+    a.config4_act_ckpt_layers = None  # only m recomputed: 237.8 GB at 40, +1.56 per layer fewer
+    monkeypatch.setenv("MXLLM_RECOMPUTE_NORM", "0")
+    assert bench.config4_plan(a, 308.0)[0] == 8 and bench.config4_plan(a, 268.0)[0] == 32
+    monkeypatch.setenv("MXLLM_RECOMPUTE_SWIGLU", "0")  # nothing recomputed: the round-3 HBM model
     assert bench.config4_plan(a, 308.0)[0] == 24 and bench.config4_plan(a, 262.0)[0] == 48
 
 
@@ -159,13 +161,13 @@ def test_config4_failed_child_is_retried_deeper(monkeypatch):
     monkeypatch.setattr(bench, "run_config4", fake)
     a = argparse.Namespace(config4_act_ckpt_layers=None)
     r = bench.run_config4_planned(a, 8, 308.0)
-    assert calls == [16, 40] and r["ms_per_step"] == 1.0
-    assert r["hbm_plan"]["checkpointed_layers"] == 40 and r["hbm_plan"]["first_attempt"]["checkpointed_layers"] == 16
+    assert calls == [0, 40] and r["ms_per_step"] == 1.0
+    assert r["hbm_plan"]["checkpointed_layers"] == 40 and r["hbm_plan"]["first_attempt"]["checkpointed_layers"] == 0
     calls.clear()
     fails[0] = 2
     r = bench.run_config4_planned(a, 8, 308.0)
-    assert calls == [16, 40, 80] and r["hbm_plan"]["checkpointed_layers"] == 80
-    assert [f["checkpointed_layers"] for f in r["hbm_plan"]["failed_attempts"]] == [16, 40]
+    assert calls == [0, 40, 80] and r["hbm_plan"]["checkpointed_layers"] == 80
+    assert [f["checkpointed_layers"] for f in r["hbm_plan"]["failed_attempts"]] == [0, 40]
     calls.clear()
     fails[0] = 1
     a.config4_act_ckpt_layers = 56
