@@ -4,6 +4,7 @@ bandwidth of ``lora_xwt`` (s x A^T / s dy B tails: the row-tiled kernel on the a
 64-row LDS-DMA kernel on all padded rows) and ``lora_grads`` (dA and every dB_i in one launch) per
 projection, the latter for several workgroup targets (MXLLM_LORA_WGS, read per launch).
 
+Both sweep the workgroup target (MXLLM_LORA_WGS, read per launch) over ``--wgs``.
 Usage: python bench/lora_probe.py [--tokens 4096] [--wgs 256,512,1024] [--rounds 5]
 """
 from __future__ import annotations
@@ -72,10 +73,12 @@ def main():
             return f
 
         for cname, X, V, tail, nbytes in (("xwt_x", x, A, xa[:, K:], T * K * 2), ("xwt_dy", dy, Bt, dya[:, N:], T * N * 2)):
-            res = {"lds": [], "lds_red64": []}
+            res = {f"lds_wgs{w}": [] for w in wgs}
             for _ in range(a.rounds):
                 for m in res:
-                    res[m].append(time_us(xwt(m, X, V, tail), a.calls))
+                    os.environ["MXLLM_LORA_WGS"] = m.split("wgs")[1]
+                    res[m].append(time_us(xwt("lds", X, V, tail), a.calls))
+            os.environ.pop("MXLLM_LORA_WGS", None)
             os.environ.pop("MXLLM_LORA_XWT", None)
             os.environ.pop("MXLLM_LORA_FUSED_RED", None)
             os.environ.pop("MXLLM_LORA_XWT_RED_ROWS", None)
@@ -86,18 +89,17 @@ def main():
             print(json.dumps(rec), flush=True)
             out.append(rec)
         fn, nbytes = (lambda: ops.lora_grads(x, dy, dya[:, N:], xa[:, K:], ga, gb, splits, r, True)), T * (K + N) * 2
-        res = {w: [] for w in wgs + ["fused"]}
+        res = {w: [] for w in wgs}
         for _ in range(a.rounds):
             for w in res:
-                os.environ["MXLLM_LORA_WGS"] = str(w if w != "fused" else 256)
-                os.environ["MXLLM_LORA_FUSED_RED"] = "1" if w == "fused" else "0"
+                os.environ["MXLLM_LORA_WGS"] = str(w)
                 res[w].append(time_us(fn, a.calls))
         os.environ.pop("MXLLM_LORA_WGS", None)
         os.environ.pop("MXLLM_LORA_FUSED_RED", None)
         rec = {"case": f"70b {name} grads T{T}", "gb": round(nbytes / 1e9, 3)}
         for w, v in res.items():
             us = statistics.median(v)
-            rec[f"wgs{w}" if w != "fused" else "wgs256_fused_red"] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
+            rec[f"wgs{w}"] = {"us": round(us, 1), "tbps": round(nbytes / (us * 1e-6) / 1e12, 2)}
         print(json.dumps(rec), flush=True)
         out.append(rec)
         del xa, dya, A, Bt, ga, gb

@@ -21,6 +21,6 @@ python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_head/run_kernel_trace.csv
 head -16 $ROOT/$OUT/step_breakdown_70b_lora.txt
 rm -f $ROOT/$OUT/prof_head/run_kernel_trace.csv
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_c4 -o run -- python3 $ROOT/bench.py $C4 > $ROOT/$OUT/prof_c4.log 2>&1 || { echo "prof c4 rc=$?"; exit 1; }
-python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_c4/run_kernel_trace.csv 40 > $ROOT/$OUT/step_breakdown_c4_ck0.txt
+python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_c4/run_kernel_trace.csv 40 embedding_fwd > $ROOT/$OUT/step_breakdown_c4_ck0.txt
 head -12 $ROOT/$OUT/step_breakdown_c4_ck0.txt
 rm -f $ROOT/$OUT/prof_c4/run_kernel_trace.csv
