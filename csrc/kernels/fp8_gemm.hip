@@ -193,15 +193,19 @@ extern "C" int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, c
   if (M > 32 || N % 16 || K % 512 || ldx % 8 || ldy % 4 || ldx < K || ldy < N) return -1;
   // two channel groups per wave for 6..16 tokens when that still leaves >= 256 workgroups
   // (70B fp8 decode step, one group -> two: 22.0 -> 21.1 ms at 8 tokens, but 18.5 -> 19.3 ms
-  // at 4; profiles/r1g_fp8_decode_ab.md).  MXLLM_W8_NC=1 forces one group (A/B switch).
+  // at 4; profiles/r1g_fp8_decode_ab.md), and for 4..5 tokens on the long-K projections
+  // (70B down, 4 tokens: 50.8 -> 44.1 us; profiles/r4x/).
   // Effective routing: mxllm/serve/quant.py sends calls of more than SMALL_M (8) tokens to
   // hipBLASLt's fp8 GEMM, so from Python the two-group variant runs at 6..8 tokens; 9..16
   // reach it only through a direct w8_linear call (or MXLLM_W8_SMALL_M=16).
-  static const bool nc1 = [] {
-    const char* e = getenv("MXLLM_W8_NC");
-    return e && e[0] == '1';
-  }();
-  if (!nc1 && M >= 6 && M <= 16 && N % 32 == 0 && N / 32 >= 256)
+  // MXLLM_W8_NC (read per call, A/B switch): 1 / 2 / 4 forces that many channel groups per wave
+  // wherever the grid keeps >= 128 workgroups
+  const char* e = getenv("MXLLM_W8_NC");
+  const int force = e && *e ? atoi(e) : 0;
+  if (force == 4 && M <= 16 && N % 64 == 0 && N / 64 >= 128)
+    w8a16_gemm_kernel<1, 8, 4><<<N / 64, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
+  else if (M <= 16 && N % 32 == 0 &&
+           ((force == 2 && N / 32 >= 128) || (!force && N / 32 >= 256 && (M >= 6 || (M >= 4 && K >= 16384)))))
     w8a16_gemm_kernel<1, 8, 2><<<N / 32, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
   else if (M <= 16) w8a16_gemm_kernel<1, 8, 1><<<N / 16, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
   else w8a16_gemm_kernel<2, 8, 1><<<N / 16, 512, 0, stream>>>(x, ldx, q, scale, y, ldy, M, N, K);
