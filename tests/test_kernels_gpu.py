@@ -427,13 +427,16 @@ def test_w8_linear(gpu, M, K):
     assert rel_err(_ops().w8_dequant(q, s), dequantize_e4m3(q, s)) < 5e-3
 
 
+@pytest.mark.parametrize("nc", ["", "4"])
 @pytest.mark.parametrize("M,K", [(1, 1536), (4, 1536), (8, 1536), (16, 1536), (8, 8192), (16, 8192),
-                                 (8, 4608)])
-def test_w8_linear_wide(gpu, M, K):
+                                 (8, 4608), (4, 16384), (5, 16384)])
+def test_w8_linear_wide(gpu, M, K, nc, monkeypatch):
     """FP8-weight decode GEMM at a projection-sized N (>= 8192: the two-channel-group
-    variant for 6..16 tokens) vs an fp32 matmul with the reference-decoded weights.
+    variant for 6..16 tokens, and for 4..5 at K >= 16384; MXLLM_W8_NC=4 the four-group one)
+    vs an fp32 matmul with the reference-decoded weights.
     K = 8192 / 4608 give every wave enough k-chunks for the unrolled batch loop
     (and, at 4608, a remainder for its tail loop)."""
+    monkeypatch.setenv("MXLLM_W8_NC", nc)
     from mxllm.serve.quant import dequantize_e4m3, quantize_e4m3
 
     torch.manual_seed(12)
