@@ -285,7 +285,8 @@ class Llama(nn.Module):
         un-checkpointed layers of a selectively checkpointed run -- including one that checkpoints
         0 layers (memory-bound by design: the saved HBM buys more un-checkpointed layers;
         ``MXLLM_RECOMPUTE_SWIGLU`` 0 / 1 / auto)."""
-        if RECOMPUTE_SWIGLU == "0" or layer.wd.lora_r > 0 or not self.training or not torch.is_grad_enabled():
+        if (RECOMPUTE_SWIGLU == "0" or any(lin.lora_r > 0 for lin in (layer.wqkv, layer.wgu, layer.wd))
+                or not self.training or not torch.is_grad_enabled()):
             return False
         if RECOMPUTE_SWIGLU == "1":
             return True
