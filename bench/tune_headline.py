@@ -91,7 +91,15 @@ def main():
     args = bench.parse(rest + ["--no-gemm-table", "--config2", "off", "--config3", "off", "--config4", "off"])
     env = runtime.init()
     out = bench.run(args, env)
-    tun.write_file(raw)
+    if hasattr(tun, "write_file"):
+        tun.write_file(raw)
+    else:  # torch >= 2.10: no write_file; write validators + results in the table's CSV format
+        with open(raw, "w", newline="") as f:
+            w = csv.writer(f)
+            for v in tun.get_validators():
+                w.writerow(["Validator", *v])
+            for r in tun.get_results():
+                w.writerow(list(r))
     stats = merge(a.base, raw, a.out)
     print({"tuned_run_ms_per_step": out["ms_per_step"], **stats}, flush=True)
     runtime.cleanup()
