@@ -669,6 +669,9 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
       t[2] = trd_off(a, s2 * 16 * ROWB);       // Q^T rows (A operand of dK)
       t[3] = trd_off(bb, s2 * 16 * ROWB);
     };
+    // the dV/dK steps below store the previous tile's dS^T (4 pieces) after this tile's DMA went
+    // out: those stores are then this wave's youngest vector-memory operations
+    const bool ds_young = spread && (prio & 64) == 0 && ds_q0 >= 0;
     issue(0, tr[0]);
 #pragma unroll
     for (int i = 0; i < 2 * DB; ++i) {
@@ -690,8 +693,19 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     ds_q0 = q0;
     ds_h = h0 + hj;
     mark(3);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for the next tile landed
-    __syncthreads();                     // ... and every wave's; this tile's buffers consumed
+    // this wave's DMA for the next tile landed.  prio & 256: counted wait -- vmcnt(4) leaves the 4
+    // dS^T stores (issued after the DMA; loads, stores and LDS-DMA retire in issue order) in flight
+    // across the barrier instead of waiting for their completion
+    static_assert(2 * DB == 8, "4 dS store pieces per tile (D = 128)");
+    if ((prio & 256) && ds_young) {
+      // raw barrier: __syncthreads()'s fence would wait for the stores (vmcnt(0)) after all; the
+      // LDS reads of this tile are retired (lgkmcnt(0)), the DMA by the counted wait
+      __builtin_amdgcn_s_waitcnt(0x0074);  // vmcnt(4) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();        // ... every wave's; this tile's buffers consumed
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      __syncthreads();                     // ... and every wave's; this tile's buffers consumed
+    }
     mark(4);
     it = nx_it;
     hj = nx_hj;
@@ -1039,12 +1053,13 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   }
   float* dqk = dq_mode == 1 ? dq : reinterpret_cast<float*>(work);
   const bool bwd8 = attn_bwd8_on();
-  // MXLLM_ATTN_BWD8_PRIO (bit flags, default 17): 1 = s_setprio 1 for waves 4-7, 16 = spread the
-  // DMA / dS-store issue over the MFMA steps; 2 = timing ablation (same q tile every step, wrong
-  // results)
+  // MXLLM_ATTN_BWD8_PRIO (bit flags, default 273): 1 = s_setprio 1 for waves 4-7, 16 = spread the
+  // DMA / dS-store issue over the MFMA steps; 256 (with 16) = counted end-of-tile wait that leaves
+  // the dS^T stores in flight (B2 S2048: 0.627 -> 0.599 ms, headline -2.9 ms; profiles/r4ad/);
+  // 2 = timing ablation (same q tile every step, wrong results)
   static const int bwd8_prio = [] {
     const char* e = getenv("MXLLM_ATTN_BWD8_PRIO");
-    return e && *e ? atoi(e) : 17;
+    return e && *e ? atoi(e) : 273;
   }();
   static const bool bwd8_prof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report of the 8-wave kernel (stderr)
     const char* e = getenv("MXLLM_ATTN_PROF");
