@@ -110,6 +110,14 @@ def parse(argv=None):
     ap.add_argument("--full-warmup", type=int, default=3)
     ap.add_argument("--grad-dtype", choices=["auto", "bf16", "fp32"], default="auto",
                     help="gradient accumulation / reduction dtype; auto = fp32 for zero3, bf16 otherwise")
+    ap.add_argument("--time-budget-s", type=float, default=float(os.environ.get("MXLLM_BENCH_BUDGET_S", "540")),
+                    help="wall-clock budget of the WHOLE command from process start (the driver's lease is "
+                         "600 s): every phase after the headline gets min(its limit, what is left - "
+                         f"{EMIT_MARGIN_S:.0f} s) and is skipped when that is below --child-min-s; the one JSON "
+                         "line is always printed")
+    ap.add_argument("--child-min-s", type=float, default=90.0,
+                    help="a phase after the headline (config 2/3/4, a config-4 retry) starts only with at least "
+                         "this much budget left")
     return ap.parse_args(argv)
 
 
@@ -121,37 +129,88 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+_T0 = time.time()  # process start: the --time-budget-s clock
+EMIT_MARGIN_S = 30.0  # kept back from every child job: killing a hung one (<= 20 s), the emit, the exit
+_STATE = {"out": None, "emitted": False, "json_out": None, "child": None}
+
+
+def remaining_s(a) -> float:
+    """Seconds left of this process's ``--time-budget-s``."""
+    return a.time_budget_s - (time.time() - _T0)
+
+
+def _kill_tree(p, grace_s: float = 20.0) -> None:
+    """SIGTERM the child's process group AND every descendant (torchrun starts each
+    worker in a session of its own, so the group alone misses them), SIGKILL what is
+    left after ``grace_s``."""
+    import signal
+    import subprocess
+
+    import psutil
+
+    try:
+        kids = psutil.Process(p.pid).children(recursive=True)
+    except psutil.Error:
+        kids = []
+    for fn in (lambda: os.killpg(p.pid, signal.SIGTERM), *[(lambda k=k: k.terminate()) for k in kids]):
+        try:
+            fn()
+        except (OSError, psutil.Error):
+            pass
+    try:
+        p.wait(timeout=grace_s)
+    except subprocess.TimeoutExpired:
+        pass
+    _, alive = psutil.wait_procs(kids, timeout=max(1.0, grace_s / 4))
+    for k in alive:
+        try:
+            k.kill()
+        except psutil.Error:
+            pass
+    try:
+        os.killpg(p.pid, signal.SIGKILL)
+    except OSError:
+        pass
+    p.wait()
+
+
 def launch_ranks(nproc: int, argv: list[str], script: str | None = None, timeout_s: float | None = None,
                  env: dict | None = None) -> int:
     """Run ``script argv`` as ``nproc`` torchrun ranks in a CHILD process group
     (one rank per GPU, rendezvous on 127.0.0.1) and relay its stdout.
 
     The parent never touches the GPU (``import torch`` does not initialise HIP)
-    and never re-execs itself: it waits for the child and returns its exit code.
+    and never re-execs itself: it waits for the child and returns its exit code
+    (124 when ``timeout_s`` expired: the whole tree is killed).  The stdout relay
+    runs on a thread, so a child that hangs WITHOUT printing still times out.
     Reference contract: /root/reference/scripts/run_node0.sh:10-16 (torchrun,
     one process per device)."""
-    import signal
     import subprocess
+    import threading
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script or os.path.abspath(__file__)]
     p = subprocess.Popen(cmd + list(argv), stdout=subprocess.PIPE, text=True, start_new_session=True,
                          env=env if env is not None else os.environ.copy())
-    t_end = None if timeout_s is None else time.time() + timeout_s
-    try:
+    _STATE["child"] = p
+    out = sys.stdout  # bound now: the caller may redirect stdout around this call
+
+    def pump():
         for line in p.stdout:
-            print(line, end="", flush=True)
-            if t_end is not None and time.time() > t_end:
-                raise TimeoutError
-        return p.wait(timeout=None if t_end is None else max(1.0, t_end - time.time()))
-    except (KeyboardInterrupt, TimeoutError, subprocess.TimeoutExpired):
-        os.killpg(p.pid, signal.SIGTERM)
-        try:
-            p.wait(timeout=20)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait()
+            out.write(line)
+            out.flush()
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    try:
+        rc = p.wait(timeout=timeout_s)
+        t.join(timeout=5)
+        return rc
+    except (KeyboardInterrupt, subprocess.TimeoutExpired):
+        _kill_tree(p, grace_s=15.0)
         return 124
+    finally:
+        _STATE["child"] = None
 
 
 def check_world(gpus: int) -> str:
@@ -182,66 +241,122 @@ def main(argv=None):
     os.environ.setdefault("MXLLM_XGMI", "0")
     env = runtime.init()
     out = run(a, env)
+    if env.is_main:
+        # from here on the headline is never lost: a SIGTERM (the driver's lease expiring) prints
+        # whatever has been measured, and every later phase runs inside try/finally + the budget
+        _arm_emit_on_signal(out, a.json_out)
     cuda = env.device.type == "cuda"
-    if cuda and a.calibrate:
-        # box speed next to the number: fixed GEMM + copy after the timed steps
-        from mxllm.utils.calibrate import calibrate
-
-        _free_gpu_memory(env)
-        out["calibration"] = calibrate(env.device)
     headline = a.model == "llama3.1-70b" and a.finetune == "lora" and a.parallel == "ddp" and not a.layers
     c2 = a.config2 == "on" or (a.config2 == "auto" and env.world_size == 1 and headline and cuda)
     c3 = a.config3 == "on" or (a.config3 == "auto" and env.world_size == 8 and headline and cuda)
     c4 = a.config4 == "on" or (a.config4 == "auto" and env.world_size == 8 and headline and cuda)
-    if c2 and env.world_size == 1:
-        # single process: an exception (e.g. out of memory) is caught and recorded, nothing can strand
-        out["config2_8b_full"] = run_full(a, env)
-        if a.config2_mb4 == "on" or (a.config2_mb4 == "auto" and cuda):
-            # the reference's batch of 4 sequences per rank (/root/reference/src/distributed_inference.py:59)
-            out["config2_8b_full_mb4"] = run_full(a, env, micro_batch=4)
     children = []
     if c3 and env.world_size > 1:
         children.append(("config3", f"config3_8b_full_dp{env.world_size}"))
     if c4:
         children.append(("config4", "config4_full_zero3"))
-    if not children:
-        if env.is_main:
-            emit(out, a.json_out)
-        runtime.cleanup()
-        return 0
-    # Multi-rank phases run as FRESH child jobs (an exception on one rank of an in-process
-    # DDP phase would strand the others in a collective): this job's ranks free their HBM, report the
-    # smallest free HBM and their PIDs, non-zero ranks exit, and local rank 0 confirms every other
-    # rank's process has exited (its HBM released) before it starts a child.
-    _free_gpu_memory(env)
-    free_gb = _min_free_gb(env)
-    import socket
+    try:
+        if cuda and a.calibrate:
+            # box speed next to the number: fixed GEMM + copy after the timed steps
+            from mxllm.utils.calibrate import calibrate
 
-    pids = runtime.all_gather_objects((socket.gethostname(), os.getpid()))
-    runtime.cleanup()
-    if not env.is_main:
+            _free_gpu_memory(env)
+            try:
+                out["calibration"] = calibrate(env.device)
+            except Exception as e:  # noqa: BLE001
+                out["calibration"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if c2 and env.world_size == 1:
+            # single process: an exception (e.g. out of memory) is caught and recorded, nothing can strand
+            for key, mb in (("config2_8b_full", None), ("config2_8b_full_mb4", 4)):
+                if mb is not None and not (a.config2_mb4 == "on" or (a.config2_mb4 == "auto" and cuda)):
+                    continue  # mb 4: the reference's batch of 4 (/root/reference/src/distributed_inference.py:59)
+                if remaining_s(a) < a.child_min_s + EMIT_MARGIN_S:
+                    out[key] = {"skipped": f"time budget: {remaining_s(a):.0f} s of --time-budget-s "
+                                           f"{a.time_budget_s:.0f} left"}
+                    continue
+                out[key] = run_full(a, env, micro_batch=mb)
+        if not children:
+            return 0
+        # Multi-rank phases run as FRESH child jobs (an exception on one rank of an in-process
+        # DDP phase would strand the others in a collective): this job's ranks free their HBM, report the
+        # smallest free HBM and their PIDs, non-zero ranks exit, and local rank 0 confirms every other
+        # rank's process has exited (its HBM released) before it starts a child.
+        _free_gpu_memory(env)
+        free_gb = _min_free_gb(env)
+        import socket
+
+        pids = runtime.all_gather_objects((socket.gethostname(), os.getpid()))
+        runtime.cleanup()
+        if not env.is_main:
+            return 0
+        host = socket.gethostname()
+        released = _wait_exited([p for h, p in pids if h == host and p != os.getpid()],
+                                timeout_s=min(120.0, max(1.0, remaining_s(a) - EMIT_MARGIN_S)))
+        out["child_phases"] = {"headline_ranks_exited_s": released, "min_free_hbm_gb_before": (
+            round(free_gb, 1) if free_gb is not None else None), "time_budget_s": a.time_budget_s}
+        for kind, key in children:
+            out[key] = {"skipped": "not reached"}  # replaced below; what a SIGTERM emit reports
+        for kind, key in children:
+            try:
+                if kind == "config4":
+                    out[key] = run_config4_planned(a, env.world_size, free_gb)
+                else:
+                    out[key] = run_config3(a, env.world_size)
+            except Exception as e:  # noqa: BLE001  the headline (and later phases) survive any phase error
+                out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        out["child_phases"]["elapsed_s"] = round(time.time() - _T0, 1)
         return 0
-    host = socket.gethostname()
-    released = _wait_exited([p for h, p in pids if h == host and p != os.getpid()], timeout_s=120.0)
-    out["child_phases"] = {"headline_ranks_exited_s": released, "min_free_hbm_gb_before": (
-        round(free_gb, 1) if free_gb is not None else None)}
-    for kind, key in children:
-        if kind == "config4":
-            out[key] = run_config4_planned(a, env.world_size, free_gb)
-        else:
-            out[key] = run_config3(a, env.world_size)
-    emit(out, a.json_out)
-    return 0
+    finally:
+        if env.is_main:
+            _emit_once()
+        runtime.cleanup()
+
+
+def _arm_emit_on_signal(out: dict, json_out: str | None) -> None:
+    """Register ``out`` as THE result line; SIGTERM/SIGINT/SIGHUP print it (once), stop a
+    running child job and exit 0 — a lease that expires during the child phases still gets
+    the headline."""
+    import signal
+
+    _STATE.update(out=out, json_out=json_out, emitted=False)
+
+    def on_signal(signum, frame):  # noqa: ARG001
+        out.setdefault("interrupted", f"signal {signum} after {time.time() - _T0:.0f} s; later phases not run")
+        _emit_once()
+        p = _STATE.get("child")
+        if p is not None and p.poll() is None:
+            _kill_tree(p, grace_s=5.0)
+        os._exit(0)
+
+    for s in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        try:
+            signal.signal(s, on_signal)
+        except (ValueError, OSError):  # not the main thread (tests calling main() from a thread)
+            pass
+
+
+def _emit_once() -> None:
+    if _STATE["out"] is not None and not _STATE["emitted"]:
+        _STATE["emitted"] = True
+        emit(_STATE["out"], _STATE["json_out"])
 
 
 def _wait_exited(pids: list[int], timeout_s: float) -> float | None:
-    """Seconds until every PID in ``pids`` has exited (same node), None on timeout."""
+    """Seconds until every PID in ``pids`` has exited (same node), None on timeout.  A PID
+    that exits between the checks (NoSuchProcess) counts as exited."""
     import psutil
+
+    def alive(p: int) -> bool:
+        try:
+            return psutil.Process(p).status() != psutil.STATUS_ZOMBIE
+        except (psutil.NoSuchProcess, psutil.ZombieProcess):
+            return False
+        except psutil.Error:
+            return psutil.pid_exists(p)
 
     t0 = time.time()
     while time.time() - t0 < timeout_s:
-        alive = [p for p in pids if psutil.pid_exists(p) and psutil.Process(p).status() != psutil.STATUS_ZOMBIE]
-        if not alive:
+        if not any(alive(p) for p in pids):
             return round(time.time() - t0, 2)
         time.sleep(0.1)
     return None
@@ -296,23 +411,44 @@ def run_full(a, env, micro_batch: int | None = None) -> dict:
     return res
 
 
+_STDOUT = sys.stdout  # the real stdout: a child phase redirects sys.stdout while it runs
+
+
 def emit(out: dict, json_out: str | None):
     line = json.dumps(out)
-    print(line, flush=True)
+    print(line, file=_STDOUT, flush=True)
     if json_out:
         with open(json_out, "w") as f:
             f.write(line + "\n")
 
 
-def _run_child(a, world: int, argv: list[str], timeout_s: float) -> dict:
+def child_timeout(a, limit_s: float) -> float | None:
+    """The time a child phase may take: ``min(limit_s, budget left - EMIT_MARGIN_S)``, or
+    None when that is below ``--child-min-s`` (the phase is skipped)."""
+    t = min(limit_s, remaining_s(a) - EMIT_MARGIN_S)
+    return t if t >= a.child_min_s else None
+
+
+def _budget_skip(a) -> dict:
+    return {"skipped": f"time budget: {max(0.0, remaining_s(a)):.0f} s of --time-budget-s {a.time_budget_s:.0f} "
+                       f"left (a phase needs --child-min-s {a.child_min_s:.0f} + {EMIT_MARGIN_S:.0f})"}
+
+
+def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "") -> dict:
     """Run bench.py ``argv`` as a fresh ``world``-rank torchrun child job (rendezvous on
-    127.0.0.1) and return its parsed JSON line (or the error)."""
+    127.0.0.1) and return its parsed JSON line (or the error).  ``timeout_s`` is capped by
+    the remaining ``--time-budget-s``; below ``--child-min-s`` the job is not started.
+    ``MXLLM_BENCH_CHILD_FAULT=<tag>:<kind>`` injects ``kind`` (hang | exit | raise) into rank 0
+    of the child tagged ``tag`` at its first timed step (budget drills)."""
     import contextlib
     import io
     import tempfile
 
     if a.device != "cpu" and torch.cuda.device_count() < world:
         return {"skipped": f"this process sees {torch.cuda.device_count()} GPU(s), the child job needs {world}"}
+    limit = child_timeout(a, timeout_s)
+    if limit is None:
+        return _budget_skip(a)
     fd, path = tempfile.mkstemp(suffix=".json", prefix="mxllm_child_")
     os.close(fd)
     argv = ["--gpus", str(world)] + argv + ["--config2", "off", "--config3", "off", "--config4", "off",
@@ -322,11 +458,16 @@ def _run_child(a, world: int, argv: list[str], timeout_s: float) -> dict:
             if not (k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                           "ROLE_WORLD_SIZE", "ROLE_NAME", "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
                     or k.startswith("TORCHELASTIC_") or k.startswith("TORCH_ELASTIC"))}
+    fault = os.environ.get("MXLLM_BENCH_CHILD_FAULT", "")
+    if fault and tag and fault.split(":")[0] == tag:
+        keep.update(MXLLM_FAULT_KIND=fault.split(":", 1)[1], MXLLM_FAULT_RANK="0", MXLLM_FAULT_STEP="0")
+    keep.pop("MXLLM_BENCH_CHILD_FAULT", None)
     t0 = time.time()
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):  # the child's own JSON line must not become a second output line
-        rc = launch_ranks(world, argv, timeout_s=timeout_s, env=keep)
-    res = {"error": f"child job exit code {rc}", "wall_s": round(time.time() - t0, 1)}
+        rc = launch_ranks(world, argv, timeout_s=limit, env=keep)
+    res = {"error": f"child job exit code {rc}" + (f" (killed at its {limit:.0f} s limit)" if rc == 124 else ""),
+           "wall_s": round(time.time() - t0, 1)}
     try:
         with open(path) as f:
             txt = f.read().strip()
@@ -348,7 +489,7 @@ def run_config3(a, world: int) -> dict:
     argv = ["--model", a.full_model, "--finetune", "full", "--parallel", "ddp", "--micro-batch",
             str(a.micro_batch), "--seq-len", str(a.seq_len), "--steps", str(a.full_steps), "--warmup",
             str(a.full_warmup)]
-    res = _run_child(a, world, argv, a.config3_timeout)
+    res = _run_child(a, world, argv, a.config3_timeout, tag="config3")
     name = PRETTY.get(a.full_model, a.full_model)
     res["metric"] = f"fine-tune tokens/sec (whole node) {name} FULL-parameter DDP"
     res["label"] = (f"BASELINE config 3: {name} full-parameter fine-tune, DDP over {world} GPUs, "
@@ -405,6 +546,9 @@ def run_config4_planned(a, world: int, free_gb: float | None) -> dict:
         for retry in (40, 80):
             if "error" not in res or retry <= ck:
                 continue
+            if child_timeout(a, a.config4_timeout) is None:  # a retry only when the budget covers it
+                res["retry_skipped"] = _budget_skip(a)["skipped"]
+                break
             failed.append({"checkpointed_layers": ck, "error": res["error"]})
             ck = retry
             res = run_config4(a, world, ck)
@@ -424,7 +568,7 @@ def run_config4(a, world: int, ckpt_layers: int = 40) -> dict:
             "--act-ckpt", "--micro-batch", str(a.config4_micro_batch), "--seq-len", str(a.seq_len),
             "--act-ckpt-layers", str(ckpt_layers),
             "--steps", str(a.config4_steps), "--warmup", str(a.config4_warmup)]
-    res = _run_child(a, world, argv, a.config4_timeout)
+    res = _run_child(a, world, argv, a.config4_timeout, tag="config4")
     name = PRETTY.get(a.config4_model, a.config4_model)
     res["label"] = (f"BASELINE config 4: {name} FULL-parameter fine-tune, ZeRO-3 sharded over "
                     f"{world} GPUs, activation checkpointing, measured after the headline in a separate job")
@@ -549,6 +693,15 @@ def run(a, env) -> dict:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    fault = None
+    if os.environ.get("MXLLM_FAULT_KIND"):  # drills (MXLLM_BENCH_CHILD_FAULT): misbehave at a timed step
+        import types
+
+        from mxllm.utils.faults import maybe_inject
+
+        fault = types.SimpleNamespace(fault_kind=os.environ["MXLLM_FAULT_KIND"],
+                                      fault_rank=int(os.environ.get("MXLLM_FAULT_RANK", "0")),
+                                      fault_step=int(os.environ.get("MXLLM_FAULT_STEP", "0")))
     loss = None
     for _ in range(a.warmup):
         loss = step()
@@ -556,7 +709,9 @@ def run(a, env) -> dict:
     runtime.barrier()
     sync()
     t_start = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
+        if fault is not None:
+            maybe_inject(fault, env.rank, i)
         loss = step()
     sync()
     runtime.barrier()

@@ -173,3 +173,83 @@ def test_config4_failed_child_is_retried_deeper(monkeypatch):
     a.config4_act_ckpt_layers = 56
     r = bench.run_config4_planned(a, 8, 308.0)
     assert calls == [56] and "error" in r
+
+
+def test_world8_hung_config4_child_keeps_headline_inside_budget():
+    """the first 8-GPU driver run must not be lost to a slow child.  A
+    config-4 child forced to hang (MXLLM_BENCH_CHILD_FAULT=config4:hang) is killed at the
+    remaining budget, its retry is skipped for lack of budget, and rank 0 still prints exactly
+    ONE JSON line with the headline, inside --time-budget-s."""
+    import time
+
+    budget = 150.0
+    env = dict(os.environ, MXLLM_BENCH_CHILD_FAULT="config4:hang")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    t0 = time.time()
+    r = _bench("--gpus", "8", "--config3", "off", "--config4", "on", "--config4-model", "tiny",
+               "--config4-steps", "1", "--config4-warmup", "1", "--time-budget-s", str(budget),
+               "--child-min-s", "20", env=env, timeout=300)
+    wall = time.time() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert wall < budget + 10, wall
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-2000:]
+    j = lines[0]
+    assert j["n_gpus"] == 8 and j["value"] > 0 and j["config"]["parallelism"] == "dp8"
+    c4 = j["config4_full_zero3"]
+    assert "error" in c4 and "124" in c4["error"], c4
+    assert "retry_skipped" in c4 and "time budget" in c4["retry_skipped"], c4
+
+
+def test_child_phases_skipped_when_budget_is_spent():
+    """With no budget left after the headline, the child phases are not started at all."""
+    r = _bench("--gpus", "2", "--config4", "on", "--config4-model", "tiny", "--time-budget-s", "1",
+               "--child-min-s", "5")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    assert "time budget" in lines[0]["config4_full_zero3"]["skipped"]
+
+
+def test_sigterm_during_child_phase_prints_headline():
+    """The driver's lease expiring (SIGTERM to bench.py) while a child job runs: the headline
+    line is printed once, the child tree is killed, exit code 0."""
+    import signal
+    import time
+
+    import psutil
+
+    env = dict(os.environ, MXLLM_BENCH_CHILD_FAULT="config4:hang")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    # world 1 (no torchrun parent): the bench process itself runs the headline, then the child
+    p = subprocess.Popen([sys.executable, "bench.py", "--device", "cpu", "--model", "tiny", "--steps", "2",
+                          "--warmup", "1", "--seq-len", "64", "--gpus", "1", "--config4", "on",
+                          "--config4-model", "tiny", "--child-min-s", "5"],
+                         cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        t_end = time.time() + 240
+        seen = False
+        while time.time() < t_end and p.poll() is None and not seen:
+            try:
+                kids = psutil.Process(p.pid).children(recursive=True)
+                seen = any("zero3" in " ".join(k.cmdline()) for k in kids)
+            except psutil.Error:
+                pass
+            time.sleep(0.5)
+        assert seen, "the config-4 child job never started"
+        time.sleep(3)
+        kids = psutil.Process(p.pid).children(recursive=True)
+        p.send_signal(signal.SIGTERM)
+        out, err = p.communicate(timeout=60)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode == 0, err[-3000:]
+    lines = _json_lines(out)
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["value"] > 0 and "interrupted" in j and j["config4_full_zero3"] == {"skipped": "not reached"}
+    _, alive = psutil.wait_procs(kids, timeout=30)
+    assert not alive, [k.pid for k in alive]
