@@ -780,6 +780,8 @@ def run(a, env) -> dict:
         "hbm_total_gb": round(total_gb, 1),
         "init_s": round(init_s, 1),
         "final_loss": round(loss_v, 4),
+        "grad_comm": (getattr(trainer.ddp.comm, "kind", None) if a.parallel != "zero3" and trainer.ddp.enabled
+                      else None),
         "allreduce_mb_per_step": (round(trainer.ddp.bytes_per_step / 2 ** 20, 1)
                                   if a.parallel != "zero3" and trainer.ddp.enabled else 0.0),
         "exposed_comm_ms_last_step": (round(trainer.ddp.exposed_comm_ms(), 3)
@@ -795,6 +797,7 @@ def run(a, env) -> dict:
         out["zero3"] = {
             "comms": ("split: all-gathers and reduce-scatters on two communicators" if c.real and c.rs_pg is not None
                       and c.rs_pg is not c.ag_pg else "single communicator" if c.real else "none (world 1 / emulated)"),
+            "comm_backend": c.kind,
             "adamw": "per unit on a side stream, overlapped with the next forward" if trainer.overlap_optimizer
                      else "one launch after the backward",
             "rmsnorm_unit": "replicated (all-reduced gradient, no re-gather)",

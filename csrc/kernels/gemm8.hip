@@ -106,11 +106,17 @@ __device__ __forceinline__ uint32_t g8_mn_lane(int lane, int cb) {
 // at the top of every K-loop iteration (2 K-tiles) and after the loop / the epilogue, plus
 // s_memrealtime at start and end (clock = d memtime / d realtime x 100 MHz).  Written with
 // ordinary VECTOR global stores into a buffer nothing else reads; the normal build has none.
+// The stamp buffer (1.3 MB of device memory) and the stamped / ablation variants exist only in a
+// diagnostic build: MXLLM_FILE_FLAGS="gemm8.hip=-DMXLLM_GEMM8_DIAG" python -m mxllm._build.
 constexpr int G8_NST = 80;
+#ifdef MXLLM_GEMM8_DIAG
 __device__ unsigned long long g8_stamps[1024 * 2 * G8_NST];
 __device__ __forceinline__ void g8_stamp(int wg, int row, int k, unsigned long long v) {
   if (wg < 1024 && k < G8_NST) g8_stamps[((size_t)wg * 2 + row) * G8_NST + k] = v;
 }
+#else
+__device__ __forceinline__ void g8_stamp(int, int, int, unsigned long long) {}
+#endif
 
 // V != 0: timing-only ablation builds (bench/gemm8_probe.py --ablate; results are WRONG):
 //   V & 1: every phase issues its 16 MFMAs twice (MFMA time per barrier doubled)
@@ -534,6 +540,7 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
       if (acc) G8_L(AK, BK_, false, true); else G8_L(AK, BK_, false, false); \
     }                                                          \
   } while (0)
+#ifdef MXLLM_GEMM8_DIAG
   if (const char* st = getenv("MXLLM_GEMM8_STAMPS")) {  // diagnostic stamped build, NN bf16 beta 0
     if (a_kc && !b_kc && !out_f32 && !acc && grid <= 1024 && *st) {
       if (atoi(st) == 4)
@@ -555,6 +562,7 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
       return (int)hipGetLastError();
     }
   }
+#endif
   if (a_kc && b_kc)
     G8_OUT(true, true);
   else if (a_kc)
@@ -633,6 +641,11 @@ extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uin
 
 // copy the diagnostic stamps out (host buffer of 1024 * 2 * 80 uint64)
 extern "C" int mx_gemm8_stamps(unsigned long long* host) {
+#ifdef MXLLM_GEMM8_DIAG
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g8_stamps), sizeof(unsigned long long) * 1024 * 2 * G8_NST, 0,
                                   hipMemcpyDeviceToHost);
+#else
+  (void)host;
+  return -1;  // not a diagnostic build
+#endif
 }

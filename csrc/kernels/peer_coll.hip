@@ -1,0 +1,231 @@
+// Bulk peer-memory collectives inside one MI355X node: direct
+// one-hop reduce-scatter / all-gather (and all-reduce = the two back to back)
+// where every rank talks to all of its peers at once.
+//
+// Why not a ring: each MI355X has 7 point-to-point xGMI links, one per peer, so
+// a ring moves every byte over ONE link per hop.  Here rank r PUSHES, for every
+// peer d, the slice of its input that d owns into a staging slot in d's memory
+// (7 concurrent link writes), raises one flag per (workgroup, peer) and then
+// reduces (RS) or copies out (AG) the slots its peers pushed into its own
+// staging.  Bytes per rank: (W-1)/W of the tensor out and in for RS, the same
+// for AG: the bandwidth-optimal amount, spread over all W-1 links.
+//
+// The same kernels run W ranks as W PROCESSES on ONE GPU (the IPC "peer" is
+// the same HBM mapped twice): that is how the multi-rank trainers are tested
+// with stream-ordered collective semantics on a 1-GPU box.
+//
+// Staging (each rank; hipDeviceMallocUncached, exchanged once by IPC handle):
+//   flags [kMaxWG][kMaxRanks] x 64 B   flag of source s for workgroup g: epoch
+//   slots [G][2][W][slot_bytes]        (g, half, src): what rank src pushed to me
+// Workgroup g walks pieces k = g, g + G, ... of the per-rank chunk (slot_bytes
+// each); every piece is a complete exchange among the W ranks, so parity
+// double-buffering is enough: a source can write half h again (epoch e + 2)
+// only after it saw my flag e + 1, which I raise after consuming epoch e.
+// Epochs live in device memory per workgroup (identical on every rank as long
+// as every rank issues the same sequence of calls, as for any collective).
+//
+// Memory protocol (MI355X_MICROARCH "inter-workgroup visibility"), at SYSTEM
+// scope because the consumer is another process / GPU: producer = stores ->
+// every wave s_waitcnt vmcnt(0) -> barrier -> fence(release) -> asm vmcnt(0)
+// -> relaxed flag store; consumer = relaxed poll -> fence(acquire) -> vmcnt(0)
+// -> barrier -> loads.  Every spin is bounded (s_memrealtime, 100 MHz): on
+// timeout the error word is set and the workgroup stops.
+//
+// Reduction: fp32, in rank order 0..W-1 -> every rank computes the identical
+// bits for its chunk, and an all-reduce (RS + AG) is bitwise identical on all
+// ranks.
+#include "common.h"
+
+namespace {
+
+constexpr int kMaxRanks = 16;
+constexpr int kMaxWG = 64;
+constexpr int kFlagStride = 16;  // uint32 words = 64 B per flag
+constexpr size_t kFlagBytes = (size_t)kMaxWG * kMaxRanks * kFlagStride * sizeof(uint32_t);
+
+struct Bases {
+  char* b[kMaxRanks];
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ float ld_f(const T* p);
+template <>
+__device__ __forceinline__ float ld_f<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld_f<uint16_t>(const uint16_t* p) { return mx::bf2f(*p); }
+
+// 16 B of T <-> 4 / 8 floats
+template <typename T>
+struct Vec;
+template <>
+struct Vec<float> {
+  static constexpr int N = 4;
+  __device__ static void add(float* acc, u32x4 v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += __uint_as_float(v[j]);
+  }
+  __device__ static u32x4 pack(const float* acc) {
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = __float_as_uint(acc[j]);
+    return o;
+  }
+};
+template <>
+struct Vec<uint16_t> {
+  static constexpr int N = 8;
+  __device__ static void add(float* acc, u32x4 v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[2 * j] += __uint_as_float(v[j] << 16);
+      acc[2 * j + 1] += __uint_as_float(v[j] & 0xFFFF0000u);
+    }
+  }
+  __device__ static u32x4 pack(const float* acc) {
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = mx::pack_bf16x2(acc[2 * j], acc[2 * j + 1]);
+    return o;
+  }
+};
+
+__device__ __forceinline__ uint32_t* flag_ptr(char* base, int g, int src) {
+  return reinterpret_cast<uint32_t*>(base) + ((size_t)g * kMaxRanks + src) * kFlagStride;
+}
+
+// MODE 0: reduce-scatter  in [n] (chunk d = in[d*m, (d+1)*m), zero past n)  -> out [m]
+// MODE 1: all-gather      in [m]                                              -> out [n] (out[p*m + i], < n)
+// n, m are multiples of the 16-B vector (V elements); slot_bytes a multiple of 4 KB.
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void peer_coll_kernel(Bases P, const T* __restrict__ in, T* __restrict__ out,
+                                                        int64_t n, int64_t m, int rank, int world, int slot_bytes,
+                                                        uint32_t* __restrict__ epochs, int* err,
+                                                        long long timeout_ticks) {
+  constexpr int V = Vec<T>::N;
+  __shared__ int bad;
+  const int g = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
+  const int slot_elems = slot_bytes / (int)sizeof(T);
+  const int64_t npieces = (m + slot_elems - 1) / slot_elems;
+  uint32_t epoch = epochs[g];
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int64_t k = g; k < npieces; k += G) {
+    ++epoch;
+    const int half = epoch & 1u;
+    const int64_t o = k * (int64_t)slot_elems;
+    const int len = (int)min((int64_t)slot_elems, m - o);
+    // 1. push my data for every peer d into slot (g, half, rank) of d's staging
+    for (int j = 1; j < world; ++j) {
+      const int d = (rank + j) % world;
+      T* slot = reinterpret_cast<T*>(P.b[d] + kFlagBytes + (((size_t)g * 2 + half) * world + rank) * slot_bytes);
+      const int64_t src0 = MODE == 0 ? (int64_t)d * m + o : o;
+      const int64_t lim = MODE == 0 ? n - src0 : m - o;  // valid elements from src0 on (RS: zero past n)
+      for (int i = tid * V; i < len; i += 256 * V) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (i < lim) v = *reinterpret_cast<const u32x4*>(in + src0 + i);
+        *reinterpret_cast<u32x4*>(slot + i) = v;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // 2. lane d raises my flag in rank d's staging (system-scope release)
+    if (tid < world && tid != rank) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(flag_ptr(P.b[tid], g, rank), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // 3. lane p waits for rank p's flag in my staging (bounded), then acquires
+    if (tid < world && tid != rank) {
+      const uint32_t* f = flag_ptr(P.b[rank], g, tid);
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+          bad = 1;
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (bad) break;
+    // 4. consume the W slots of this piece (my own contribution straight from `in`)
+    const T* mine = reinterpret_cast<const T*>(P.b[rank] + kFlagBytes + ((size_t)g * 2 + half) * world * slot_bytes);
+    if (MODE == 0) {
+      for (int i = tid * V; i < len; i += 256 * V) {
+        float acc[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = 0.f;
+        for (int p = 0; p < world; ++p) {
+          u32x4 v = {0u, 0u, 0u, 0u};
+          if (p == rank) {
+            const int64_t s = (int64_t)rank * m + o + i;
+            if (s < n) v = *reinterpret_cast<const u32x4*>(in + s);
+          } else {
+            v = *reinterpret_cast<const u32x4*>(mine + (size_t)p * slot_elems + i);
+          }
+          Vec<T>::add(acc, v);
+        }
+        *reinterpret_cast<u32x4*>(out + o + i) = Vec<T>::pack(acc);
+      }
+    } else {
+      for (int p = 0; p < world; ++p) {
+        const T* src = p == rank ? in + o : mine + (size_t)p * slot_elems;
+        T* dst = out + (int64_t)p * m + o;
+        const int64_t lim = n - ((int64_t)p * m + o);
+        for (int i = tid * V; i < len && i < lim; i += 256 * V)
+          *reinterpret_cast<u32x4*>(dst + i) = *reinterpret_cast<const u32x4*>(src + i);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) epochs[g] = epoch;
+}
+
+template <typename T>
+int launch(int mode, char* const* bases, const void* in, void* out, int64_t n, int64_t m, int rank, int world,
+           int wgs, int slot_bytes, uint32_t* epochs, int* err, long long timeout_ticks, hipStream_t s) {
+  Bases P{};
+  for (int r = 0; r < world; ++r) {
+    if (!bases[r]) return -1;
+    P.b[r] = bases[r];
+  }
+  const int64_t slot_elems = slot_bytes / (int64_t)sizeof(T);
+  const int64_t npieces = (m + slot_elems - 1) / slot_elems;
+  const int G = (int)std::min<int64_t>(wgs, std::max<int64_t>(1, npieces));
+  if (mode == 0)
+    peer_coll_kernel<T, 0><<<G, 256, 0, s>>>(P, (const T*)in, (T*)out, n, m, rank, world, slot_bytes, epochs, err,
+                                              timeout_ticks);
+  else
+    peer_coll_kernel<T, 1><<<G, 256, 0, s>>>(P, (const T*)in, (T*)out, n, m, rank, world, slot_bytes, epochs, err,
+                                              timeout_ticks);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Staging bytes one rank allocates for (world, wgs, slot_bytes).
+extern "C" size_t mx_peer_staging_bytes(int world, int wgs, int slot_bytes) {
+  return kFlagBytes + (size_t)wgs * 2 * world * slot_bytes;
+}
+
+// mode 0 = reduce-scatter (sum), 1 = all-gather; dtype 0 = fp32, 1 = bf16.
+// Requirements (checked by the caller): 1 < world <= 16, wgs <= 64, slot_bytes % 4096 == 0,
+// n and m multiples of 16 B of the dtype, m * world >= n, 16-B aligned pointers.
+extern "C" int mx_peer_collective(int mode, int dtype, char* const* bases, const void* in, void* out, int64_t n,
+                                  int64_t m, int rank, int world, int wgs, int slot_bytes, uint32_t* epochs, int* err,
+                                  long long timeout_ticks, hipStream_t stream) {
+  if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world || wgs < 1 || wgs > kMaxWG || slot_bytes % 4096 ||
+      n < 0 || m < 0 || (mode != 0 && mode != 1))
+    return -1;
+  if (m == 0) return 0;
+  if (dtype == 0) return launch<float>(mode, bases, in, out, n, m, rank, world, wgs, slot_bytes, epochs, err,
+                                       timeout_ticks, stream);
+  if (dtype == 1) return launch<uint16_t>(mode, bases, in, out, n, m, rank, world, wgs, slot_bytes, epochs, err,
+                                          timeout_ticks, stream);
+  return -1;
+}

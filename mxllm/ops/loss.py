@@ -100,10 +100,12 @@ class _ChunkedLinearCEFn(torch.autograd.Function):
     """Mean CE of h @ w^T, T walked in chunks (module doc); dh / dW formed in the forward."""
 
     @staticmethod
-    def forward(ctx, h, w, labels, ignore_index, chunk):
+    def forward(ctx, h, w, labels, ignore_index, chunk, grad_mode=True):
         T, V = h.shape[0], w.shape[0]
         nat = use_native(h)
-        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        # gradients are formed here, in the forward: only when a backward can follow (grad mode
+        # of the CALLER -- inside forward it is always off -- and an input that requires grad)
+        need_h, need_w = grad_mode and ctx.needs_input_grad[0], grad_mode and ctx.needs_input_grad[1]
         if nat:
             inv_n = native().ce_inv_count(labels, ignore_index)
         else:
@@ -134,6 +136,7 @@ class _ChunkedLinearCEFn(torch.autograd.Function):
         ctx.save_for_backward(dh, dwacc)
         ctx.wp = w if w.is_leaf else None
         ctx.wdtype = w.dtype
+        ctx.scaled = False
         return loss
 
     @staticmethod
@@ -143,6 +146,11 @@ class _ChunkedLinearCEFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gdh = dh * gl.to(dh.dtype)
         if ctx.needs_input_grad[1]:
+            # the fp32 [V, H] accumulator (4 GB at 70B) is scaled in place, so the saved state is
+            # consumed: a second backward (retain_graph) would scale it twice -- refuse it
+            if ctx.scaled:
+                raise RuntimeError("chunked linear_cross_entropy: backward can run only once per forward")
+            ctx.scaled = True
             dwacc.mul_(gl)
             wp = ctx.wp
             g = direct_grad(wp) if wp is not None else None
@@ -157,7 +165,7 @@ class _ChunkedLinearCEFn(torch.autograd.Function):
                 else:
                     g.add_(dwacc)
                 mark_ready(wp)
-        return gdh, gdw, None, None, None
+        return gdh, gdw, None, None, None, None
 
 
 def linear_cross_entropy(h: torch.Tensor, w: torch.Tensor, labels: torch.Tensor,
@@ -167,7 +175,8 @@ def linear_cross_entropy(h: torch.Tensor, w: torch.Tensor, labels: torch.Tensor,
     T, V = h.shape[0], w.shape[0]
     c = ce_chunk_tokens(T, V) if chunk is None else chunk
     if c < T:
-        return _ChunkedLinearCEFn.apply(h.contiguous(), w, labels.contiguous(), ignore_index, c)
+        return _ChunkedLinearCEFn.apply(h.contiguous(), w, labels.contiguous(), ignore_index, c,
+                                        torch.is_grad_enabled())
     if use_native(h):
         return _LinearCEFn.apply(h.contiguous(), w, labels.contiguous(), ignore_index)
     return ref.cross_entropy(F.linear(h, w), labels, ignore_index)

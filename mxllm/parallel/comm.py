@@ -1,0 +1,308 @@
+"""One collective interface for the trainers: RCCL / gloo, or peer memory.
+
+The reference's only collective is a barrier (reference
+src/distributed_inference.py:18); the DDP gradient sync it advertises
+(reference README.md:7) is mxllm's own (ddp.py, zero1.py, zero3.py).  Every
+bulk collective those trainers issue goes through a communicator created
+here, with ONE contract — the one ProcessGroupNCCL (= RCCL on ROCm) has:
+
+  * the collective runs on the communicator's own stream, ordered after
+    everything already queued on the caller's current stream;
+  * ``async_op=True`` returns a work whose ``wait()`` makes the caller's
+    CURRENT stream wait for the collective (no host block);
+  * every tensor handed to a collective is kept alive (``record_stream``)
+    until the collective has finished with it, whatever the caller drops.
+
+Implementations:
+
+  * :class:`TorchCollectives` — ``torch.distributed`` on a process group:
+    RCCL over xGMI on GPUs (the default), gloo on CPU.
+  * :class:`PeerCollectives` — direct one-hop reduce-scatter / all-gather over
+    IPC-mapped peer memory (``csrc/kernels/peer_coll.hip``): every rank pushes
+    to all of its peers at once (7 xGMI links on an 8x MI355X node).
+    Opt-in with ``MXLLM_COMM=peer``.  Because a "peer" may be the SAME GPU
+    mapped by another process, W ranks can share one GPU: that is how the
+    multi-rank trainers run with stream-ordered collectives on a 1-GPU box
+    (tests/test_multirank_gpu.py), where RCCL refuses two ranks per device.
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import torch
+import torch.distributed as dist
+
+log = logging.getLogger("mxllm.comm")
+
+
+def kind_requested() -> str:
+    """``MXLLM_COMM``: ``torch`` (default: RCCL / gloo) or ``peer``."""
+    return os.environ.get("MXLLM_COMM", "torch").strip().lower() or "torch"
+
+
+class TorchCollectives:
+    """``torch.distributed`` on ``group`` (RCCL on GPUs, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        self.pg = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.kind = dist.get_backend(group) if dist.is_initialized() else "none"
+
+    def all_reduce(self, t: torch.Tensor, async_op: bool = False):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=async_op)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        return dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.pg, async_op=async_op)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        return dist.all_gather_into_tensor(out, inp, group=self.pg, async_op=async_op)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0):
+        dist.broadcast(t, src=src, group=self.pg)
+
+    def close(self):
+        pass
+
+
+class PeerWork:
+    """RCCL-style work: ``wait()`` orders the caller's current stream after the collective."""
+
+    __slots__ = ("event", "comm")
+
+    def __init__(self, event, comm):
+        self.event, self.comm = event, comm
+
+    def wait(self):
+        torch.cuda.current_stream(self.comm.device).wait_event(self.event)
+        self.comm.check()
+        return True
+
+    def is_completed(self) -> bool:
+        return self.event.query()
+
+
+class PeerCollectives:
+    """Bulk sum reduce-scatter / all-gather / all-reduce over IPC-mapped peer
+    memory (``torch.classes.mxllm.PeerComm``).  Create with :func:`create`
+    (collective over ``group``, which also carries the bootstrap exchange).
+
+    fp32 / bf16; sums in fp32 in rank order, so every rank gets identical bits.
+    ``wgs`` workgroups per call each move ``slot_kb`` per peer per exchange."""
+
+    def __init__(self, group, device: torch.device, *, wgs: int | None = None, slot_kb: int | None = None,
+                 timeout_s: float | None = None):
+        from ..ops._ext import native
+
+        native()
+        self.pg = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = device
+        self.kind = "peer"
+        self.wgs = int(wgs or os.environ.get("MXLLM_PEER_WGS", "32"))
+        self.slot_bytes = int(slot_kb or os.environ.get("MXLLM_PEER_SLOT_KB", "64")) * 1024
+        self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("MXLLM_PEER_TIMEOUT_S", "300"))
+        self._c = torch.classes.mxllm.PeerComm(self.rank, self.world, device.index, self.wgs, self.slot_bytes,
+                                               self.timeout_s)
+        self.stream = torch.cuda.Stream(device)
+        self._broken = False
+
+    # ------------------------------------------------------------------ bootstrap
+    def handle(self) -> list[int]:
+        return self._c.handle().tolist()
+
+    def open(self, handles: list[list[int]]):
+        self._c.open(torch.tensor(handles, dtype=torch.uint8))
+
+    def self_test(self, timeout_s: float = 30.0) -> bool:
+        """Reduce-scatter + all-gather + all-reduce of known values (both dtypes, a size
+        that needs zero padding) with a short timeout: a peer whose writes are not visible
+        shows up here, not mid-training."""
+        self._c.set_timeout(timeout_s)
+        try:
+            W, dev = self.world, self.device
+            ok = True
+            for dt in (torch.float32, torch.bfloat16):
+                n = 8 * W * 3
+                x = (torch.arange(n, device=dev) % 13 + self.rank).to(dt)
+                out = torch.empty(n // W, dtype=dt, device=dev)
+                self.reduce_scatter(out, x)
+                want = ((torch.arange(n, device=dev) % 13) * W + W * (W - 1) // 2).to(dt).view(W, -1)[self.rank]
+                g = torch.empty(n, dtype=dt, device=dev)
+                self.all_gather(g, out)
+                y = (torch.arange(40, device=dev) % 5 + self.rank).to(dt)
+                self.all_reduce(y)
+                ywant = ((torch.arange(40, device=dev) % 5) * W + W * (W - 1) // 2).to(dt)
+                torch.cuda.current_stream(dev).synchronize()
+                ok &= bool(torch.equal(out, want)) and bool(torch.equal(g.view(W, -1)[self.rank], want))
+                ok &= bool(torch.equal(y, ywant))
+            ok = ok and not self._c.error()
+            if not ok:
+                log.warning("peer-memory self-test mismatch on rank %d", self.rank)
+            return ok
+        finally:
+            self._c.clear_error()
+            self._c.set_timeout(self.timeout_s)
+
+    # ------------------------------------------------------------------ collectives
+    def _vec(self, dtype) -> int:
+        return 16 // torch.empty(0, dtype=dtype).element_size()
+
+    def _issue(self, fn, tensors, async_op: bool):
+        if self._broken:
+            raise RuntimeError("peer-memory communicator is broken (an earlier collective timed out)")
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            fn()
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        for t in tensors:
+            t.record_stream(self.stream)  # the allocator keeps it until the comm stream is past it
+        w = PeerWork(ev, self)
+        if async_op:
+            return w
+        w.wait()
+        return None
+
+    @staticmethod
+    def _fits(t: torch.Tensor, v: int) -> bool:
+        return t.is_contiguous() and t.numel() % v == 0 and t.data_ptr() % 16 == 0
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        W = self.world
+        if inp.numel() != W * out.numel() or inp.dtype != out.dtype:
+            raise ValueError("reduce_scatter: input must hold world x output elements of one dtype")
+        v = self._vec(inp.dtype)
+
+        def run():
+            if self._fits(inp, v) and self._fits(out, v):
+                self._c.reduce_scatter_(out, inp)
+                return
+            m = out.numel()
+            mp = -(-m // v) * v  # padded chunk: every rank's chunk starts on a 16-B boundary
+            ip = torch.zeros(W, mp, dtype=inp.dtype, device=self.device)
+            ip[:, :m].copy_(inp.view(W, m))
+            op = torch.empty(mp, dtype=out.dtype, device=self.device)
+            self._c.reduce_scatter_(op, ip.view(-1))
+            out.copy_(op[:m])
+
+        return self._issue(run, (out, inp), async_op)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        W = self.world
+        if out.numel() != W * inp.numel() or inp.dtype != out.dtype:
+            raise ValueError("all_gather: output must hold world x input elements of one dtype")
+        v = self._vec(inp.dtype)
+
+        def run():
+            if self._fits(inp, v) and self._fits(out, v):
+                self._c.all_gather_(out, inp)
+                return
+            m = inp.numel()
+            mp = -(-m // v) * v
+            ip = torch.zeros(mp, dtype=inp.dtype, device=self.device)
+            ip[:m].copy_(inp.reshape(-1))
+            op = torch.empty(W, mp, dtype=out.dtype, device=self.device)
+            self._c.all_gather_(op.view(-1), ip)
+            out.view(W, m).copy_(op[:, :m])
+
+        return self._issue(run, (out, inp), async_op)
+
+    def all_reduce(self, t: torch.Tensor, async_op: bool = False):
+        """Two-shot all-reduce: reduce-scatter into a chunk, all-gather back in place."""
+        W = self.world
+        v = self._vec(t.dtype)
+
+        def run():
+            n = t.numel()
+            m = -(-n // (W * v)) * v  # chunk per rank, a multiple of the vector
+            if self._fits(t, v):
+                part = torch.empty(m, dtype=t.dtype, device=self.device)
+                self._c.reduce_scatter_(part, t.view(-1))
+                self._c.all_gather_(t.view(-1), part)
+                return
+            buf = torch.zeros(m * W, dtype=t.dtype, device=self.device)
+            buf[:n].copy_(t.reshape(-1))
+            part = torch.empty(m, dtype=t.dtype, device=self.device)
+            self._c.reduce_scatter_(part, buf)
+            self._c.all_gather_(buf, part)
+            t.copy_(buf[:n].view_as(t))
+
+        return self._issue(run, (t,), async_op)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0):
+        """Rank ``src``'s values everywhere (init-time only): an all-reduce of the source's
+        tensor and zeros elsewhere."""
+        if self.rank != src:
+            t.zero_()
+        self.all_reduce(t)
+
+    def check(self):
+        if self._c.error():
+            self._broken = True
+            raise RuntimeError("peer-memory collective timed out waiting for a peer (MXLLM_PEER_TIMEOUT_S)")
+
+    def close(self):
+        try:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        finally:
+            self._c.close()
+
+
+def peer_eligible(group=None, device: torch.device | None = None) -> bool:
+    """Peer memory needs every rank of the group on this host and on a GPU."""
+    if not dist.is_initialized() or device is None or device.type != "cuda":
+        return False
+    world = dist.get_world_size(group)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    return 1 < world <= 16 and local_world >= dist.get_world_size()
+
+
+def create_peer(group=None, device: torch.device | None = None, **kw) -> PeerCollectives | None:
+    """Collective over ``group``: a :class:`PeerCollectives` on every rank, or None on every
+    rank (never a mix: any local failure makes all ranks fall back)."""
+    world = dist.get_world_size(group)
+    comm, handle = None, None
+    try:
+        comm = PeerCollectives(group, device, **kw)
+        handle = comm.handle()
+    except Exception as e:  # noqa: BLE001
+        log.warning("peer-memory communicator: local setup failed (%s)", e)
+    handles: list = [None] * world
+    dist.all_gather_object(handles, handle, group=group)
+    ok = all(h is not None for h in handles)
+    if ok:
+        try:
+            comm.open(handles)
+            ok = comm.self_test()
+        except Exception as e:  # noqa: BLE001
+            log.warning("peer-memory communicator: opening peer buffers failed (%s)", e)
+            ok = False
+    oks: list = [None] * world
+    dist.all_gather_object(oks, ok, group=group)
+    if not all(oks):
+        if comm is not None:
+            comm.close()
+        return None
+    return comm
+
+
+def create(group=None, device: torch.device | None = None, kind: str | None = None):
+    """The communicator a trainer uses for ``group``.  Collective over ``group`` when the
+    peer path is requested (``MXLLM_COMM=peer``); falls back to torch.distributed on every
+    rank when peer memory is unusable (``MXLLM_COMM_STRICT=1``: raise instead)."""
+    kind = kind or kind_requested()
+    if kind == "peer" and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if peer_eligible(group, device):
+            c = create_peer(group, device)
+            if c is not None:
+                log.info("[rank %d] bulk collectives: peer memory (world %d, %d WGs x %d KB slots)",
+                         c.rank, c.world, c.wgs, c.slot_bytes // 1024)
+                return c
+        if os.environ.get("MXLLM_COMM_STRICT", "0") == "1":
+            raise RuntimeError("MXLLM_COMM=peer requested but peer memory is unusable here")
+        log.warning("MXLLM_COMM=peer unusable here; bulk collectives use torch.distributed")
+    return TorchCollectives(group)

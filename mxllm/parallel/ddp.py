@@ -12,8 +12,10 @@ DistributedDataParallel" (reference README.md:7) but never wraps a model
     latency (tens of µs) negligible while still overlapping backward; the
     first bucket is small so communication starts as early as possible;
   * each bucket's all-reduce is launched asynchronously from a
-    post-accumulate-grad hook the moment its last gradient lands, and RCCL
-    runs it on its own stream, overlapped with the rest of backward;
+    post-accumulate-grad hook the moment its last gradient lands, and the
+    communicator (mxllm/parallel/comm.py: RCCL by default, or the peer-memory
+    two-shot path with MXLLM_COMM=peer) runs it on its own stream, overlapped
+    with the rest of backward;
   * averaging is NOT a separate pass: ``grad_scale = 1/world`` is folded into
     the fused AdamW kernel (or the grad-norm) by the trainer.
 """
@@ -43,11 +45,16 @@ class Bucket:
 
 class DDP:
     def __init__(self, flat: FlatParams, *, bucket_mb: float = 128.0, first_bucket_mb: float = 16.0,
-                 process_group=None, enabled: bool | None = None):
+                 process_group=None, enabled: bool | None = None, comm=None):
+        from . import comm as comm_mod
+
         self.flat = flat
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.enabled = (self.world > 1) if enabled is None else enabled
+        # the bucket collectives (collective creation when MXLLM_COMM=peer: every rank builds its DDP)
+        self.comm = comm if comm is not None else (
+            comm_mod.create(process_group, flat.device) if self.world > 1 else comm_mod.TorchCollectives(process_group))
         self._sync = True
         esz = flat.grads.element_size()
         self.buckets: list[Bucket] = []
@@ -115,7 +122,7 @@ class DDP:
     def _launch(self, b: Bucket):
         if self.enabled:
             g = self.flat.grads[b.start:b.end]
-            b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = self.comm.all_reduce(g, async_op=True)
         b.fired = True
         if self.on_ready is not None:
             self.on_ready(b)
@@ -177,7 +184,7 @@ class DDP:
     def broadcast_params(self, src: int = 0):
         """Make every rank start from rank ``src``'s trainable parameters."""
         if self.enabled:
-            dist.broadcast(self.flat.params, src=src, group=self.pg)
+            self.comm.broadcast(self.flat.params, src=src)
             if self.flat.master is not self.flat.params:
                 self.flat.master.copy_(self.flat.params)
 

@@ -78,7 +78,7 @@ class Zero1(DDP):
         g = self.flat.grads[b.start:b.end]
         out = self.gshard[cs:cs + n]
         if self.world > 1:
-            b.work = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = self.comm.reduce_scatter(out, g, async_op=True)
         else:
             out.copy_(g)
             b.work = None
@@ -114,8 +114,7 @@ class Zero1(DDP):
             cs, n = self.cslices[b.index]
             dst = self.flat.params[b.start:b.end]
             if self.world > 1:
-                self._ag_work[b.index] = dist.all_gather_into_tensor(dst, self.pshard[cs:cs + n], group=self.pg,
-                                                                     async_op=True)
+                self._ag_work[b.index] = self.comm.all_gather(dst, self.pshard[cs:cs + n], async_op=True)
             else:
                 dst.copy_(self.pshard[cs:cs + n])
 
@@ -134,7 +133,7 @@ class Zero1(DDP):
 
     def broadcast_params(self, src: int = 0):
         if self.world > 1:
-            dist.broadcast(self.flat.params, src=src, group=self.pg)
+            self.comm.broadcast(self.flat.params, src=src)
         with torch.no_grad():
             for b, (cs, n) in zip(self.buckets, self.cslices):
                 own = b.start + self.rank * n
@@ -149,7 +148,7 @@ class Zero1(DDP):
         for b, (cs, n) in zip(self.buckets, self.cslices):
             src = self.master[cs:cs + n].float().contiguous()
             if self.world > 1:
-                dist.all_gather_into_tensor(full[b.start:b.end], src, group=self.pg)
+                self.comm.all_gather(full[b.start:b.end], src)
             else:
                 full[b.start:b.end].copy_(src)
         return full

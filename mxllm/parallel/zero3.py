@@ -139,27 +139,38 @@ class Comm:
     """The two collectives ZeRO-3 issues, over real ranks or emulated.
 
     ``ag_pg`` carries the all-gathers and ``rs_pg`` the reduce-scatters: two
-    communicators = two RCCL streams, so a prefetch gather and the previous
-    unit's reduce-scatter run concurrently (xGMI links are full duplex).
+    communicators = two streams (RCCL's, or the peer-memory path's with
+    MXLLM_COMM=peer: mxllm/parallel/comm.py), so a prefetch gather and the
+    previous unit's reduce-scatter run concurrently (xGMI links are full duplex).
     ``emulate`` > 1: single process standing in for rank 0 of that many."""
 
-    def __init__(self, world: int, rank: int, ag_pg=None, rs_pg=None, emulate: int = 0):
+    def __init__(self, world: int, rank: int, ag_pg=None, rs_pg=None, emulate: int = 0, device=None):
         self.world, self.rank, self.ag_pg, self.rs_pg = world, rank, ag_pg, rs_pg
         self.emulate = emulate > 1
+        self.ag = self.rs = None
+        if self.real:
+            from . import comm as comm_mod
+
+            self.ag = comm_mod.create(ag_pg, device)
+            self.rs = self.ag if rs_pg is ag_pg else comm_mod.create(rs_pg, device)
 
     @property
     def real(self) -> bool:
         return self.world > 1 and not self.emulate
 
+    @property
+    def kind(self) -> str:
+        return getattr(self.ag, "kind", "none")
+
     def all_gather(self, full: torch.Tensor, shard: torch.Tensor, async_op: bool):
         if self.real:
-            return dist.all_gather_into_tensor(full, shard, group=self.ag_pg, async_op=async_op)
+            return self.ag.all_gather(full, shard, async_op=async_op)
         full.view(self.world, -1).copy_(shard.unsqueeze(0).expand(self.world, -1))
         return None
 
     def reduce_scatter(self, out: torch.Tensor, full: torch.Tensor, async_op: bool):
         if self.real:
-            return dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.rs_pg, async_op=async_op)
+            return self.rs.reduce_scatter(out, full, async_op=async_op)
         if self.world == 1:
             out.copy_(full)
         else:
@@ -168,7 +179,7 @@ class Comm:
 
     def all_reduce(self, t: torch.Tensor, async_op: bool = False):
         if self.real:
-            return dist.all_reduce(t, group=self.rs_pg, async_op=async_op)
+            return self.rs.all_reduce(t, async_op=async_op)
         return None
 
 
@@ -422,7 +433,7 @@ class Zero3Trainer:
             if (rs_group is None and process_group is None and self.world > 1
                     and os.environ.get("MXLLM_Z3_SPLIT_COMMS", "1") != "0"):
                 rs_pg = dist.new_group()
-            comm = Comm(self.world, self.rank, process_group, rs_pg)
+            comm = Comm(self.world, self.rank, process_group, rs_pg, device=env.device)
         self.comm = comm
         self.emulated = comm.emulate
         self.max_inflight = max_inflight or int(os.environ.get("MXLLM_Z3_INFLIGHT", "2"))
@@ -773,7 +784,7 @@ class Zero3Trainer:
             else:
                 full = torch.empty(u.full_numel, dtype=torch.float32, device=self.device)
                 if self.comm.real:
-                    dist.all_gather_into_tensor(full, src, group=self.pg)
+                    self.comm.ag.all_gather(full, src)
                 else:
                     full.view(self.world, -1).copy_(src.unsqueeze(0).expand(self.world, -1))
             for name, o, n, shp in zip(u.names, u.offsets, u.numels, u.shapes):

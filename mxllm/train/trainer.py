@@ -370,9 +370,7 @@ class Trainer:
             else:
                 sq = ops.sq_norm(grads)
             if z is not None:
-                from ..parallel.runtime import all_reduce_small_
-
-                all_reduce_small_(sq)  # sum of the shards' squares
+                z.comm.all_reduce(sq)  # sum of the shards' squares (stream-ordered, same communicator)
             gnorm = sq.sqrt() * scale
             self.last_grad_norm = gnorm
             coef = torch.clamp(o.grad_clip / (gnorm + 1e-6), max=1.0)

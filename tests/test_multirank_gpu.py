@@ -1,0 +1,270 @@
+"""Multi-rank trainers on ONE GPU with RCCL's collective semantics (VERDICT r4 Missing 2).
+
+RCCL refuses two ranks on one device, and gloo's ``wait()`` blocks the host, so
+the overlaps the trainers depend on — bucket all-reduces under the backward,
+the AdamW on a side stream issued after ``ddp.finish()``, ZeRO-3's in-flight
+reduce-scatters folded after ``work.wait()``, gathers racing the per-unit
+overlapped AdamW — had never run multi-rank with stream-ordered collectives.
+Here W = 2 and 4 PROCESSES share the box's one MI355X and their bulk
+collectives run through the peer-memory path (``MXLLM_COMM=peer``,
+csrc/kernels/peer_coll.hip): each collective on the communicator's own stream,
+``wait()`` = the caller's stream waits on an event, every tensor kept alive by
+``record_stream`` — the contract ProcessGroupNCCL has.  gloo only carries the
+bootstrap (handle exchange, desync checksums).
+
+* kernel level: reduce-scatter / all-gather / all-reduce, fp32 and bf16, sizes
+  that need padding, two communicators in flight at once, uneven arrival,
+  inputs dropped right after an async call (the allocator must not hand their
+  memory out before the collective is done), the bounded-spin timeout;
+* trainer level: the DDP trainer (full fine-tune, overlapped AdamW) and the
+  ZeRO-3 trainer (split communicators, overlapped per-unit AdamW, gradient
+  accumulation 2, one checkpointed layer) at world 2 and 4 equal the world-1
+  run over the same micro-batches per parameter, and the replicas pass
+  ``check_in_sync`` after 5 steps.
+Reference: /root/reference/docs/troubleshooting.md:55-63 (nodes out of sync);
+/root/reference/README.md:7,9 (DDP over NCCL).
+"""
+import os
+import queue as _q
+import socket
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _peer_env(port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MXLLM_BACKEND="gloo", MXLLM_COMM="peer",
+                      MXLLM_COMM_STRICT="1", MXLLM_PEER_TIMEOUT_S="60", MXLLM_PEER_WGS="8", MXLLM_PG_TIMEOUT_S="180")
+
+
+def _launch(target, world, *args, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    res, deadline = {}, time.time() + timeout
+    try:
+        while len(res) < world:
+            try:
+                o = q.get(timeout=2)
+                res[o["rank"]] = o
+            except _q.Empty:
+                dead = [p.exitcode for p in ps if p.exitcode not in (None, 0)]
+                assert not dead, f"worker crashed: exit codes {dead}; results so far {res}"
+                assert time.time() < deadline, f"timeout; results so far {res}"
+        for p in ps:
+            p.join(60)
+            assert p.exitcode == 0
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+# ---------------------------------------------------------------------------- kernel level
+
+
+def _coll_worker(rank, world, port, q):
+    _peer_env(port)
+    out = {"rank": rank}
+    try:
+        from mxllm.parallel import runtime
+        from mxllm.parallel.comm import PeerCollectives, create
+
+        env = runtime.init(rank=rank, world_size=world)
+        dev = env.device
+        import torch.distributed as dist
+
+        a = create(None, dev)
+        b = create(dist.new_group(), dev)  # a second communicator: its own stream and staging
+        out["kinds"] = (a.kind, b.kind)
+        assert isinstance(a, PeerCollectives) and isinstance(b, PeerCollectives)
+
+        def vals(n, seed, dt):
+            return [torch.randn(n, generator=torch.Generator().manual_seed(seed * 97 + r)).to(dt) for r in range(world)]
+
+        def rsum(vs):  # the kernel's order: fp32, rank 0..W-1, one rounding
+            acc = torch.zeros_like(vs[0], dtype=torch.float32)
+            for v in vs:
+                acc = acc + v.float()
+            return acc.to(vs[0].dtype)
+
+        ok, it = True, 0
+        for dt in (torch.float32, torch.bfloat16):
+            for m in (8, 40, 1000, 4096 * 9 + 8, 300_001):  # chunk elements (1000, 300001: padded path)
+                it += 1
+                n = m * world
+                vs = vals(n, it, dt)
+                if rank == 1 and it % 3 == 0:
+                    time.sleep(0.05)  # uneven arrival: peers spin on the flags
+                x = vs[rank].to(dev)
+                rs = torch.empty(m, dtype=dt, device=dev)
+                w1 = a.reduce_scatter(rs, x, async_op=True)
+                # the second communicator at the same time: all-gather of a different tensor
+                vg = vals(m, it + 500, dt)
+                ag = torch.empty(n, dtype=dt, device=dev)
+                w2 = b.all_gather(ag, vg[rank].to(dev), async_op=True)  # input dropped right away
+                junk = [torch.full((m,), 7.0, dtype=dt, device=dev) for _ in range(4)]  # reuse bait
+                w1.wait()
+                w2.wait()
+                want_rs = rsum(vs).view(world, m)[rank]
+                ok &= bool(torch.equal(rs.cpu(), want_rs))
+                ok &= bool(torch.equal(ag.cpu(), torch.cat(vg)))
+                ar = vs[rank].to(dev)
+                a.all_reduce(ar)  # sync form: stream-ordered, no host wait
+                ok &= bool(torch.equal(ar.cpu().view(world, m)[rank], want_rs))
+                del junk
+        out["ok"] = ok
+        # every rank gets identical all-reduce bits
+        t = torch.randn(5000, generator=torch.Generator().manual_seed(rank)).to(dev)
+        a.all_reduce(t)
+        allv: list = [None] * world
+        dist.all_gather_object(allv, t.cpu().double().sum().item())
+        out["identical"] = len(set(allv)) == 1
+        # bounded spin: rank 0 issues alone with a short limit -> error on the next wait
+        dist.barrier()
+        if rank == 0:
+            a._c.set_timeout(0.5)
+            t = torch.ones(64, device=dev)
+            a.all_reduce(t, async_op=True)
+            torch.cuda.synchronize()
+            try:
+                a.all_reduce(torch.ones(64, device=dev), async_op=True).wait()
+                out["timeout_raised"] = False
+            except RuntimeError:
+                out["timeout_raised"] = True
+        dist.barrier()
+        runtime.cleanup()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        out["exc"] = traceback.format_exc()[-3000:]
+    finally:
+        q.put(out)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_collectives_exact_on_shared_gpu(gpu, world):
+    res = _launch(_coll_worker, world)
+    for r in range(world):
+        assert "exc" not in res[r], res[r]["exc"]
+        assert res[r]["kinds"] == ("peer", "peer") and res[r]["ok"] and res[r]["identical"], res[r]
+    assert res[0]["timeout_raised"], res[0]
+
+
+# ---------------------------------------------------------------------------- trainer level
+
+
+STEPS = 5
+
+
+def _batches(cfg, world, steps, per_rank, seq):
+    g = torch.Generator().manual_seed(5)
+    return [torch.randint(0, cfg.vocab_size, (world, per_rank, seq), generator=g) for _ in range(steps)]
+
+
+def _trainer_worker(rank, world, port, q, mode, ref_world):
+    """``mode``: ddp | zero3.  ``world`` ranks train on the same global batches; at world 1
+    the ``ref_world`` ranks' micro-batches become gradient-accumulation micro-batches."""
+    if world > 1:
+        _peer_env(port)
+    out = {"rank": rank}
+    try:
+        from mxllm.models import Llama, get_config
+        from mxllm.parallel import runtime
+        from mxllm.parallel.consistency import check_in_sync
+        from mxllm.train.trainer import OptimConfig, Trainer
+
+        env = runtime.init(rank=rank, world_size=world)
+        dev = env.device
+        cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
+        opt = OptimConfig(lr=1e-3, grad_clip=1.0, weight_decay=0.01)
+        seq = 128
+        if mode == "ddp":
+            model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=1234)
+            tr = Trainer(model, env, opt)
+            out["overlap"] = tr.overlap_optimizer
+            out["comm"] = getattr(tr.ddp.comm, "kind", None)
+            per_rank = 2
+        else:
+            from mxllm.parallel.zero3 import Zero3Trainer
+
+            tr = Zero3Trainer(cfg, env, opt, seed=7, activation_checkpointing=1)
+            out["overlap"] = tr.overlap_optimizer
+            out["comm"] = tr.comm.kind if tr.comm.real else None
+            out["split"] = tr.comm.real and tr.comm.rs is not tr.comm.ag
+            per_rank = 2  # two micro-batches of 1 sequence: gradient accumulation 2
+        data = _batches(cfg, ref_world, STEPS, per_rank, seq)
+        losses = []
+        for s in range(STEPS):
+            ranks = range(ref_world) if world == 1 else [rank]
+            if mode == "ddp":
+                mbs = [(data[s][r].to(dev), data[s][r].to(dev)) for r in ranks]
+            else:
+                mbs = [(data[s][r][i:i + 1].to(dev), data[s][r][i:i + 1].to(dev)) for r in ranks for i in range(2)]
+            losses.append(tr.train_step(mbs))
+        losses = [float(x) for x in losses]
+        if mode == "ddp":
+            tr.params_ready()
+            out["in_sync"] = check_in_sync([tr.flat.params], raise_on_mismatch=False)
+            master = {s.name: tr.flat.master[s.offset:s.offset + s.numel].float().view(s.shape).cpu()
+                      for s in tr.flat.slots}
+        else:
+            tr.params_ready()
+            out["in_sync"] = check_in_sync([tr.units[0].shard], raise_on_mismatch=False)  # replicated norms
+            master = {k: v.cpu() for k, v in tr.full_master_state().items()}
+        tot = runtime.all_reduce_scalars(losses, "sum")
+        out["losses"] = [t / world for t in tot]
+        if rank == 0:
+            out["master"] = {k: v.numpy().copy() for k, v in master.items()}
+        runtime.cleanup()
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        out["exc"] = traceback.format_exc()[-3000:]
+    finally:
+        q.put(out)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["ddp", "zero3"])
+def test_trainers_multirank_on_shared_gpu_match_world1(gpu, mode):
+    ref = None
+    for world in (2, 4):
+        r1 = _launch(_trainer_worker, 1, mode, world)[0]
+        assert "exc" not in r1, r1["exc"]
+        res = _launch(_trainer_worker, world, mode, world)
+        for r in range(world):
+            assert "exc" not in res[r], res[r]["exc"]
+            assert res[r]["comm"] == "peer" and res[r]["overlap"], res[r]
+            assert res[r]["in_sync"], (world, r)
+            if mode == "zero3":
+                assert res[r]["split"]
+        got = res[0]
+        assert r1["losses"][-1] < r1["losses"][0]  # it trains
+        for x, y in zip(r1["losses"], got["losses"]):
+            assert abs(x - y) < 3e-3 * max(1.0, abs(x)), (world, r1["losses"], got["losses"])
+        assert set(r1["master"]) == set(got["master"])
+        for n, w in r1["master"].items():
+            # 5 AdamW steps of lr 1e-3: the two runs differ only by gradient summation order
+            # (rank-ordered two-shot sum vs micro-batch accumulation); an element whose summed
+            # gradient is ~0 can flip sign, moving by up to 2 lr per step
+            d = abs(w - got["master"][n])
+            bad = int((d > 2e-3).sum())
+            assert bad <= max(4, 5e-3 * d.size) and float(d.mean()) < 2e-4, (world, n, bad, float(d.max()))
+        ref = r1
+    assert ref is not None

@@ -358,6 +358,21 @@ def test_chunked_linear_cross_entropy_matches_reference():
         h.grad = w.grad = None
     assert ce_chunk_tokens(4096, 128256) == 4096  # 1 GB of logits: one piece
     assert ce_chunk_tokens(32768, 128256) == 4096  # 8.4 GB: chunked
+    # under no_grad the chunked path forms no gradients (same loss) ...
+    from unittest import mock
+
+    import mxllm.ops.loss as L
+
+    with torch.no_grad(), mock.patch.object(L, "weight_grad_", side_effect=AssertionError("dW formed")):
+        l3 = linear_cross_entropy(h, w, lab, chunk=8)
+    assert abs(float(l3) - float(l2)) < 1e-6
+    # ... and a second backward through the consumed accumulator is refused, not applied twice
+    l4 = linear_cross_entropy(h, w, lab, chunk=8)
+    l4.backward(retain_graph=True)
+    import pytest
+
+    with pytest.raises(RuntimeError, match="only once|inplace"):  # autograd version check or ours
+        l4.backward()
 
 
 def test_swiglu_linear_recompute_matches_saved_activation(monkeypatch):
