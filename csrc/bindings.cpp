@@ -220,6 +220,63 @@ bool gemm8_tail(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, 
   return true;
 }
 
+// Forward qkv projection with RoPE and the head split in the GEMM epilogue (gemm8 G8_EPI_ROPE):
+// x [B*S, K] (row-strided), w [(Hq + 2 Hkv) * 128, K] -> q [B, Hq, S, 128], k / v [B, Hkv, S, 128]
+// (preallocated, contiguous), rotated with the f32 tables cos / sin [>= S, 64] at positions 0..S-1.
+// Returns false (nothing launched) for shapes the kernel does not take.
+bool gemm8_rope(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
+                int64_t S, int64_t Hq, int64_t Hkv, at::Tensor& q, at::Tensor& k, at::Tensor& v) {
+  MX_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+           "gemm8_rope: bf16 GPU operands");
+  MX_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1) && x.size(0) == B * S, "gemm8_rope: shapes");
+  MX_CHECK(w.size(0) == (Hq + 2 * Hkv) * 128, "gemm8_rope: head dim 128");
+  MX_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+               sin.is_contiguous() && cos.size(-1) == 64 && cos.size(0) >= S && sin.sizes() == cos.sizes(),
+           "gemm8_rope: f32 [>= S, 64] tables");
+  for (const at::Tensor* t : {&q, &k, &v})
+    MX_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous(), "gemm8_rope: bf16 outputs");
+  MX_CHECK(q.numel() == B * Hq * S * 128 && k.numel() == B * Hkv * S * 128 && v.numel() == k.numel(),
+           "gemm8_rope: output sizes");
+  if (x.stride(1) != 1 || w.stride(1) != 1) return false;
+  DevGuard g(x.device());
+  MxG8Epi ep{};
+  ep.q = bfm(q);
+  ep.k = bfm(k);
+  ep.v = bfm(v);
+  ep.cosb = cos.data_ptr<float>();
+  ep.sinb = sin.data_ptr<float>();
+  ep.S = (int)S;
+  ep.Hq = (int)Hq;
+  ep.Hkv = (int)Hkv;
+  const int rc = mx_gemm8_epi(bf(x), x.stride(0), bf(w), w.stride(0), nullptr, 0, (int)x.size(0), (int)w.size(0),
+                              (int)x.size(1), 1, ep, cur_stream());
+  if (rc == -1) return false;
+  MX_OK(rc);
+  return true;
+}
+
+// Forward gate-up projection with SwiGLU in the GEMM epilogue (gemm8 G8_EPI_SWIGLU): x [T, K],
+// w = [gate; up] [2F, K] -> gu [T, 2F] (the projection output, kept for the backward) and
+// m = silu(gate) * up [T, F].  Returns false (nothing launched) for shapes the kernel does not take.
+bool gemm8_swiglu(const at::Tensor& x, const at::Tensor& w, at::Tensor& gu, at::Tensor& m) {
+  MX_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+               gu.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kBFloat16,
+           "gemm8_swiglu: bf16 GPU tensors");
+  MX_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1) && gu.size(0) == x.size(0) &&
+               gu.size(1) == w.size(0) && m.size(0) == x.size(0) && 2 * m.size(1) == w.size(0),
+           "gemm8_swiglu: shapes");
+  if (x.stride(1) != 1 || w.stride(1) != 1 || gu.stride(1) != 1 || m.stride(1) != 1) return false;
+  DevGuard g(x.device());
+  MxG8Epi ep{};
+  ep.m = bfm(m);
+  ep.ldm = m.stride(0);
+  const int rc = mx_gemm8_epi(bf(x), x.stride(0), bf(w), w.stride(0), bfm(gu), gu.stride(0), (int)x.size(0),
+                              (int)w.size(0), (int)x.size(1), 2, ep, cur_stream());
+  if (rc == -1) return false;
+  MX_OK(rc);
+  return true;
+}
+
 // the gemm8 diagnostic build's cycle stamps (MXLLM_GEMM8_STAMPS): int64 [1024, 2, 80] on the host
 at::Tensor gemm8_stamps() {
   auto out = at::empty({1024, 2, 80}, at::TensorOptions().dtype(at::kLong));
@@ -1077,6 +1134,8 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
   m.def("gemm8_stamps() -> Tensor", &gemm8_stamps);
   m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4) -> bool");
+  m.def("gemm8_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, Tensor(a!) q, Tensor(b!) k, Tensor(c!) v) -> bool");
+  m.def("gemm8_swiglu(Tensor x, Tensor w, Tensor(a!) gu, Tensor(b!) m) -> bool");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
@@ -1123,6 +1182,8 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("transpose2d", &transpose2d);
   m.impl("gemm8", &gemm8);
   m.impl("gemm8_tail", &gemm8_tail);
+  m.impl("gemm8_rope", &gemm8_rope);
+  m.impl("gemm8_swiglu", &gemm8_swiglu);
   m.impl("ce_inv_count", &ce_inv_count);
   m.impl("ce_chunk", &ce_chunk);
   m.impl("ce_chunk_f32", &ce_chunk_f32);

@@ -37,6 +37,20 @@ int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_
              int64_t ldc, int out_f32, int M, int N, int K, float beta, const float* alpha_t, float alpha_f,
              int ph, hipStream_t stream);
 int mx_gemm8_stamps(unsigned long long* host);
+// layout of csrc/kernels/gemm8.hip G8Epi (fused forward epilogues)
+struct MxG8Epi {
+  uint16_t* q;
+  uint16_t* k;
+  uint16_t* v;
+  const float* cosb;
+  const float* sinb;
+  int S, Hq, Hkv;
+  uint16_t* m;
+  int64_t ldm;
+  int F;
+};
+int mx_gemm8_epi(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int M,
+                 int N, int K, int mode, MxG8Epi ep, hipStream_t stream);
 int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc, uint16_t* C,
                   int64_t ldc, int M, int N, int K, int rows, int at, float* ws, int ph, hipStream_t stream);
 int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int16_t* lo, int64_t n,

@@ -64,20 +64,62 @@ constexpr int G8_TILE = 4 * G8_HT;  // A0 | A1 | B0 | B1
 constexpr int G8_BK = 64;
 
 // image row r' (k-contiguous) / image column (mn-contiguous) -> row / column of the 256 tile
-__device__ __forceinline__ int g8_map_a(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
 __device__ __forceinline__ int g8_map_b(int r, int h) { return (r >> 5) * 64 + h * 32 + (r & 31); }
+__device__ __forceinline__ int g8_map_a(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
+
+// ---- fused epilogues (forward projections, B = the weight [N][K], bf16 output) -----------------
+// In the epilogue, lane l of wave (wr, wc) holds, per accumulator block j = 2 jh + jl, the 4
+// consecutive VIRTUAL tile columns v = 64 wc + 32 jh + 16 jl + 4 (l >> 4) + [0, 4).  A fused epilogue
+// picks which WEIGHT ROW feeds each virtual column (the B images are DMA-loaded from those rows), so
+// the two operands of its elementwise op land in the SAME lane and register -- no LDS exchange:
+//  G8_EPI_ROPE  (qkv projection, head dim 128: a tile = 2 heads): virtual (wc, jh, jl, q) -> head
+//               column d = 32 (wc & 1) + 64 jh + 16 jl + q, so blocks jh = 0 / 1 hold the rotate-half
+//               pair (d, d + 64); outputs written HEAD-MAJOR q [B,Hq,S,D], k / v [B,Hkv,S,D] (the
+//               layout the attention kernels read; csrc/kernels/rope.hip rope_split, fused away)
+//  G8_EPI_SWIGLU (gate-up projection, W = [gate; up], F rows each): tile pn covers gate columns
+//               [128 pn, 128 pn + 128) and the same up columns: jh = 0 -> gate row 128 pn + 32 wc +
+//               16 jl + q, jh = 1 -> the up row F further; outputs gu [T, 2F] (standard layout, saved
+//               for the backward) AND m = silu(g) u [T, F] (elementwise.hip swiglu_fwd, fused away)
+// Both round the GEMM result to bf16 first and then apply the exact expression of the kernel they
+// replace: bitwise equal to GEMM -> rope_split / swiglu_fwd on the same kernel's output.
+constexpr int G8_EPI_NONE = 0, G8_EPI_ROPE = 1, G8_EPI_SWIGLU = 2;
+
+struct G8Epi {
+  uint16_t* q;        // ROPE: [B, Hq, S, 128]
+  uint16_t* k;        //       [B, Hkv, S, 128]
+  uint16_t* v;        //       [B, Hkv, S, 128]
+  const float* cosb;  //       [>= S, 64] f32 (host table, mxllm/ops/reference.py rope_tables)
+  const float* sinb;
+  int S, Hq, Hkv;
+  uint16_t* m;        // SWIGLU: [T, F] with row stride ldm
+  int64_t ldm;
+  int F;
+};
+
+// weight row feeding virtual tile column v (0..255) of output tile pn (G8_EPI_SWIGLU: absolute row)
+template <int EPI>
+__device__ __forceinline__ int g8_epi_row(int v, int pn, int F) {
+  if constexpr (EPI == G8_EPI_ROPE) {
+    return (v & ~127) + ((v >> 6) & 1) * 32 + ((v >> 5) & 1) * 64 + (v & 31);
+  } else if constexpr (EPI == G8_EPI_SWIGLU) {
+    return (((v >> 5) & 1) ? F : 0) + 128 * pn + (v >> 6) * 32 + (v & 31);
+  } else {
+    return v;
+  }
+}
 __device__ __forceinline__ int g8_t(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
 // per-lane byte offsets of this wave's two LDS-DMA pieces of half-tile image h of one operand
-template <bool KC, bool IS_A>
-__device__ __forceinline__ void g8_src_offsets(int w, int lane, int64_t ld, int h, uint32_t (&off)[2]) {
+template <bool KC, bool IS_A, int EPI = G8_EPI_NONE>
+__device__ __forceinline__ void g8_src_offsets(int w, int lane, int64_t ld, int h, uint32_t (&off)[2], int pn = 0,
+                                               int F = 0) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int pc = 2 * w + j;
     if constexpr (KC) {
       const int r = 8 * pc + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const int row = IS_A ? g8_map_a(r, h) : g8_map_b(r, h);
+      const int row = IS_A ? g8_map_a(r, h) : g8_epi_row<EPI>(g8_map_b(r, h), pn, F);
       off[j] = (uint32_t)(((int64_t)row * ld + 8 * c) * 2);
     } else {
       const int k = 4 * pc + (lane >> 4);
@@ -118,6 +160,98 @@ __device__ __forceinline__ void g8_stamp(int wg, int row, int k, unsigned long l
 __device__ __forceinline__ void g8_stamp(int, int, int, unsigned long long) {}
 #endif
 
+__device__ __forceinline__ float g8_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float g8_rbf(float x) { return bf2f(f2bf(x)); }  // round through bf16
+
+// 16-B store of blocks (jl = 0, 1) of one jh: lanes l, l + 16 swap packed pairs (permlane16_swap) so
+// every lane owns 8 consecutive columns (see the plain bf16 epilogue); `dst` = this lane's 8 columns
+__device__ __forceinline__ void g8_store8(uint16_t* dst, const f32x4& va, const f32x4& vb) {
+  const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(va[0], va[1]), pack_bf16x2(vb[0], vb[1]), false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[2], vb[3]), false, false);
+  uint4 o;
+  o.x = s0[0];
+  o.y = s1[0];
+  o.z = s0[1];
+  o.w = s1[1];
+  *reinterpret_cast<uint4*>(dst) = o;
+}
+
+template <int EPI>
+__device__ __forceinline__ void g8_epilogue_fused(f32x4 (&acc)[8][4], float alpha, int ml, int pn, int wc, int lane,
+                                                  int N, const G8Epi& ep, void* C, int64_t ldc) {
+  // this lane's 8 stored columns start at offset u8 inside a 32-column group (after the swap)
+  const int u8 = 16 * ((lane >> 4) & 1) + 8 * (lane >> 5);
+  if constexpr (EPI == G8_EPI_ROPE) {
+    const int head = pn * 2 + (wc >> 1);  // 128-column heads: two per tile
+    uint16_t* dst;
+    int Hd, hh;
+    if (head < ep.Hq) {
+      dst = ep.q, Hd = ep.Hq, hh = head;
+    } else if (head < ep.Hq + ep.Hkv) {
+      dst = ep.k, Hd = ep.Hkv, hh = head - ep.Hq;
+    } else {
+      dst = ep.v, Hd = ep.Hkv, hh = head - ep.Hq - ep.Hkv;
+    }
+    const bool rot = head < ep.Hq + ep.Hkv;
+    const int d0 = 32 * (wc & 1);  // head column of block (jh 0, jl 0, lane group 0)
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = ml + qa * 64 + 16 * i;
+        const int b = m / ep.S, sq = m - b * ep.S;
+        f32x4 x0[2], x1[2];  // [jl]: head columns d (jh 0) and d + 64 (jh 1)
+#pragma unroll
+        for (int jl = 0; jl < 2; ++jl) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            x0[jl][c] = g8_rbf(acc[4 * qa + i][jl][c] * alpha);
+            x1[jl][c] = g8_rbf(acc[4 * qa + i][2 + jl][c] * alpha);
+          }
+        }
+        if (rot) {
+#pragma unroll
+          for (int jl = 0; jl < 2; ++jl) {
+            const int f = d0 + 16 * jl + 4 * (lane >> 4);  // frequency index of x0[jl][0]
+            const f32x4 cs = *reinterpret_cast<const f32x4*>(ep.cosb + (int64_t)sq * 64 + f);
+            const f32x4 sn = *reinterpret_cast<const f32x4*>(ep.sinb + (int64_t)sq * 64 + f);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float a = x0[jl][c], bb = x1[jl][c];
+              x0[jl][c] = a * cs[c] - bb * sn[c];
+              x1[jl][c] = bb * cs[c] + a * sn[c];
+            }
+          }
+        }
+        uint16_t* row = dst + (((int64_t)b * Hd + hh) * ep.S + sq) * 128;
+        g8_store8(row + d0 + u8, x0[0], x0[1]);
+        g8_store8(row + d0 + 64 + u8, x1[0], x1[1]);
+      }
+  } else {  // G8_EPI_SWIGLU
+    const int F = N / 2;
+    const int col = 128 * pn + 32 * wc + u8;  // gate column (up: + F; m: the same column)
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = ml + qa * 64 + 16 * i;
+        f32x4 g[2], u[2], mm[2];
+#pragma unroll
+        for (int jl = 0; jl < 2; ++jl)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            g[jl][c] = g8_rbf(acc[4 * qa + i][jl][c] * alpha);
+            u[jl][c] = g8_rbf(acc[4 * qa + i][2 + jl][c] * alpha);
+            mm[jl][c] = g[jl][c] * g8_sigmoid(g[jl][c]) * u[jl][c];
+          }
+        uint16_t* gu = reinterpret_cast<uint16_t*>(C) + m * ldc;
+        g8_store8(gu + col, g[0], g[1]);
+        g8_store8(gu + F + col, u[0], u[1]);
+        g8_store8(ep.m + m * ep.ldm + col, mm[0], mm[1]);
+      }
+  }
+}
+
 // V != 0: timing-only ablation builds (bench/gemm8_probe.py --ablate; results are WRONG):
 //   V & 1: every phase issues its 16 MFMAs twice (MFMA time per barrier doubled)
 //   V & 2: no barriers in the K loop and no wave-row stagger (no LDS ordering at all)
@@ -125,11 +259,12 @@ __device__ __forceinline__ void g8_stamp(int, int, int, unsigned long long) {}
 // PH = 4: the same images and registers on a 4-phase schedule (two quadrants = 32 MFMAs per phase,
 // half the barriers; every phase retires its LDS reads before its first barrier so each image is
 // restaged one phase after its last read; two half-tiles in flight across barriers, vmcnt(4))
-template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA, int V = 0, int PH = 8>
+template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA, int V = 0, int PH = 8, int EPI = G8_EPI_NONE>
 __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
              void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
-             float alpha_f, int k0 = 0, int64_t cpart = 0) {
+             float alpha_f, int k0 = 0, int64_t cpart = 0, G8Epi ep = G8Epi{}) {
+  static_assert(EPI == G8_EPI_NONE || (B_KC && !OUT_F32 && !BETA), "fused epilogues: TN-form bf16 forward only");
   // K split in two (gridDim.y == 2, k0 = K of part 0): part 1 covers K rows / columns k0 .. K-1 of
   // both operands and writes its own output image C + cpart (mx_gemm8_tail: the last, partial wave
   // of tiles of a GEMM runs as twice as many half-K workgroups; the images are summed after)
@@ -171,9 +306,12 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 
   // ---- operand descriptors (range-checked: mn-contiguous rows past K read as zeros)
   const uint16_t* abase = A_KC ? A + (int64_t)m0 * lda : A + m0;
-  const uint16_t* bbase = B_KC ? B + (int64_t)n0 * ldb : B + n0;
+  // SWIGLU: gate and up rows are F apart -> absolute weight rows off the start of B
+  const uint16_t* bbase = B_KC ? B + (int64_t)(EPI == G8_EPI_SWIGLU ? 0 : n0) * ldb : B + n0;
   const uint32_t arec = A_KC ? (uint32_t)((255 * lda + (int64_t)nk * G8_BK) * 2) : (uint32_t)(((int64_t)K * lda - m0) * 2);
-  const uint32_t brec = B_KC ? (uint32_t)((255 * ldb + (int64_t)nk * G8_BK) * 2) : (uint32_t)(((int64_t)K * ldb - n0) * 2);
+  const uint32_t brec = EPI == G8_EPI_SWIGLU ? (uint32_t)(((int64_t)(N - 1) * ldb + (int64_t)nk * G8_BK) * 2)
+                        : B_KC ? (uint32_t)((255 * ldb + (int64_t)nk * G8_BK) * 2)
+                               : (uint32_t)(((int64_t)K * ldb - n0) * 2);
   const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)abase, 0, arec, 0x00020000);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, 0, brec, 0x00020000);
   const uint32_t astep = A_KC ? G8_BK * 2 : (uint32_t)(G8_BK * lda * 2);  // bytes per K-tile
@@ -181,8 +319,8 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   uint32_t aoff[2][2], boff[2][2];
   g8_src_offsets<A_KC, true>(w, lane, lda, 0, aoff[0]);
   g8_src_offsets<A_KC, true>(w, lane, lda, 1, aoff[1]);
-  g8_src_offsets<B_KC, false>(w, lane, ldb, 0, boff[0]);
-  g8_src_offsets<B_KC, false>(w, lane, ldb, 1, boff[1]);
+  g8_src_offsets<B_KC, false, EPI>(w, lane, ldb, 0, boff[0], pn, N / 2);
+  g8_src_offsets<B_KC, false, EPI>(w, lane, ldb, 1, boff[1], pn, N / 2);
 
   // issue half-tile image `img` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile kt into buffer kt & 1
   auto issue = [&](int kt, int img) __attribute__((always_inline)) {
@@ -433,6 +571,10 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   const float alpha = alpha_f * (alpha_t ? alpha_t[0] : 1.f);
   const int ml = m0 + wr * 128 + (lane & 15);
   const int nl = n0 + wc * 64 + 4 * (lane >> 4);
+  if constexpr (EPI != G8_EPI_NONE) {
+    g8_epilogue_fused<EPI>(acc, alpha, ml, pn, wc, lane, N, ep, C, ldc);
+    return;
+  }
 #pragma unroll
   for (int qa = 0; qa < 2; ++qa) {
     f32x4 old[4][4];
@@ -573,6 +715,36 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
     G8_OUT(false, false);
 #undef G8_OUT
 #undef G8_L
+  return (int)hipGetLastError();
+}
+
+// Forward projection with a fused epilogue (G8Epi above), A = x [M][K] and B = W [N][K] both
+// k-contiguous, 4-phase schedule.  mode 1 (ROPE): N = (Hq + 2 Hkv) * 128, M = B * S, S % 256 == 0,
+// writes q / k / v head-major (C unused).  mode 2 (SWIGLU): N = 2F, F % 128 == 0, writes gu into C
+// [M][ldc >= 2F] and m into ep.m [M][ldm >= F].  Returns -1 (nothing launched) for other shapes.
+extern "C" int mx_gemm8_epi(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
+                            int M, int N, int K, int mode, G8Epi ep, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (M & 255) || (N & 255) || K % G8_BK) return -1;
+  if (lda % 8 || ldb % 8 || lda < K || ldb < K || ((uintptr_t)A | (uintptr_t)B) & 15) return -1;
+  const int64_t aspan = 256 * lda, bspan = (int64_t)N * ldb;
+  if (aspan * 2 >= ((int64_t)1 << 31) || bspan * 2 >= ((int64_t)1 << 31)) return -1;
+  const int grid = (M >> 8) * (N >> 8);
+  if (mode == G8_EPI_ROPE) {
+    if (N != (ep.Hq + 2 * ep.Hkv) * 128 || ep.S <= 0 || ep.S % 256 || M % ep.S || !ep.q || !ep.k || !ep.v ||
+        !ep.cosb || !ep.sinb || (((uintptr_t)ep.q | (uintptr_t)ep.k | (uintptr_t)ep.v) & 15))
+      return -1;
+    gemm8_kernel<true, true, false, false, 0, 4, G8_EPI_ROPE><<<grid, 512, 0, stream>>>(
+        A, lda, B, ldb, nullptr, 0, M, N, K, nullptr, 1.f, 0, 0, ep);
+  } else if (mode == G8_EPI_SWIGLU) {
+    if ((N / 2) % 128 || !C || !ep.m || ldc < N || ldc % 8 || ep.ldm < N / 2 || ep.ldm % 8 ||
+        (((uintptr_t)C | (uintptr_t)ep.m) & 15))
+      return -1;
+    ep.F = N / 2;
+    gemm8_kernel<true, true, false, false, 0, 4, G8_EPI_SWIGLU><<<grid, 512, 0, stream>>>(
+        A, lda, B, ldb, C, ldc, M, N, K, nullptr, 1.f, 0, 0, ep);
+  } else {
+    return -1;
+  }
   return (int)hipGetLastError();
 }
 

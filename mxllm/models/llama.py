@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.utils.checkpoint as ckpt
 
 from .. import ops
+from ..ops import fused
 from ..ops import reference as ref
 from .config import LlamaConfig
 
@@ -254,8 +255,19 @@ class Llama(nn.Module):
         layer = self.layers[i]
         rec = self._recompute_m(layer, i)
         rec_x = rec and RECOMPUTE_NORM != "0"
-        qkv = ops.normed_linear(x, h, layer.attn_norm, cfg.norm_eps, layer.wqkv.weight) if rec_x else layer.wqkv(x)
-        if self.seq_parallel is not None:
+        if (self.seq_parallel is None and not layer.wqkv.lora_r
+                and fused.qkv_attention_ok(x, layer.wqkv.weight, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim)):
+            # projection + RoPE + head split in ONE GEMM epilogue (mxllm/ops/fused.py)
+            o = fused.qkv_attention(x, layer.wqkv.weight, self.rope_cos, self.rope_sin, B, S, cfg.n_heads,
+                                    cfg.n_kv_heads, cfg.head_dim, causal=True, out_pad=self._pad(layer.wo),
+                                    norm=(h, layer.attn_norm, cfg.norm_eps) if rec_x else None)
+            qkv = None
+        else:
+            qkv = (ops.normed_linear(x, h, layer.attn_norm, cfg.norm_eps, layer.wqkv.weight) if rec_x
+                   else layer.wqkv(x))
+        if qkv is None:
+            pass
+        elif self.seq_parallel is not None:
             o = self.seq_parallel(qkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads, cfg.n_kv_heads,
                                   cfg.head_dim, causal=True)
         else:
@@ -268,6 +280,10 @@ class Llama(nn.Module):
         if rec:  # m = swiglu(gu) (and the gate-up input x) recomputed in the backward
             gu = ops.normed_linear(x, h, layer.mlp_norm, cfg.norm_eps, layer.wgu.weight) if rec_x else layer.wgu(x)
             d = ops.swiglu_linear(gu, layer.wd.weight)
+        elif not layer.wgu.lora_r and fused.gate_up_swiglu_ok(x, layer.wgu.weight):
+            # gate-up projection with SwiGLU in its epilogue (mxllm/ops/fused.py)
+            m = fused.gate_up_swiglu(x, layer.wgu.weight, out_pad=self._pad(layer.wd))
+            d = layer.wd(m)
         else:
             tf, tb = self._swiglu_tails(layer, x)
             m = ops.swiglu(layer.wgu(x, dy_tail=tb is not None), out_pad=self._pad(layer.wd),

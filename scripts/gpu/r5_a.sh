@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-5 GPU pass A: peer-memory multi-rank tests, strict parity, fused epilogues, config-2 A/B.
+set -o pipefail
+O=gpurun_out/r5a
+mkdir -p $O
+T="python -u -m pytest -x -v --timeout 600 --timeout-method thread"
+timeout -k 10 300 $T tests/test_fused_epi_gpu.py tests/test_gemm8_gpu.py > $O/fused.log 2>&1 || { echo "fused tests failed"; exit 1; }
+timeout -k 10 600 $T tests/test_multirank_gpu.py tests/test_comm.py > $O/mr.log 2>&1 || { echo "multirank failed"; exit 1; }
+timeout -k 10 400 $T tests/test_strict_parity_gpu.py > $O/strict.log 2>&1 || echo "strict parity failed (continuing)"
+for f in 1 0; do
+  MXLLM_FUSED_EPI=$f timeout -k 10 240 python bench.py --model llama3.1-8b --finetune full --steps 10 --warmup 3 \
+    --no-calibrate --config2 off --json-out $O/c2_fused$f.json > $O/c2_fused$f.log 2>&1 || { echo "bench fused=$f failed"; exit 1; }
+done
+echo done

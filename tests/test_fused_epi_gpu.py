@@ -1,0 +1,108 @@
+"""gemm8 fused forward epilogues (csrc/kernels/gemm8.hip G8_EPI_ROPE / G8_EPI_SWIGLU,
+mxllm/ops/fused.py) vs fp32 PyTorch references, vs the unfused kernels they replace, and
+through autograd inside the Llama layer."""
+import math
+
+import pytest
+import torch
+
+from mxllm.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from mxllm.ops import native
+
+    return native()
+
+
+def _mat(rows, cols, dev, seed, scale=1.0, pad=0):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    buf = ((torch.rand(rows, cols + pad, device=dev, generator=g) * 2 - 1) * scale).to(torch.bfloat16)
+    return buf[:, :cols]
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm()).item()
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,K", [(1, 256, 4, 2, 512), (2, 512, 8, 2, 1024), (1, 2048, 32, 8, 4096)])
+def test_gemm8_rope_epilogue(gpu, B, S, Hq, Hkv, K):
+    D = 128
+    N = (Hq + 2 * Hkv) * D
+    x = _mat(B * S, K, gpu, 1, pad=64)  # row-strided (LoRA-style padded rows)
+    w = _mat(N, K, gpu, 2, scale=0.05)
+    cos, sin = ref.rope_tables(S + 17, D, 500000.0, {"factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                                     "original_max_position_embeddings": 8192}, gpu)
+    q = torch.empty(B, Hq, S, D, device=gpu, dtype=torch.bfloat16)
+    k = torch.empty(B, Hkv, S, D, device=gpu, dtype=torch.bfloat16)
+    v = torch.empty_like(k)
+    assert _ops().gemm8_rope(x, w, cos, sin, B, S, Hq, Hkv, q, k, v)
+    # fp32 reference: projection -> split -> rotate-half RoPE
+    y = (x.float() @ w.float().t()).view(B, S, Hq + 2 * Hkv, D)
+    qr = ref.apply_rope(y[:, :, :Hq], cos, sin).transpose(1, 2)
+    kr = ref.apply_rope(y[:, :, Hq:Hq + Hkv], cos, sin).transpose(1, 2)
+    vr = y[:, :, Hq + Hkv:].transpose(1, 2)
+    for got, want in ((q, qr), (k, kr), (v, vr)):
+        assert _rel(got, want) < 5e-3
+        assert (got.float() - want).abs().max().item() < 0.05 * want.abs().max().item()
+    # the unfused path on the same GEMM: gemm8 (4-phase) -> rope_split, near-bitwise
+    qkv = torch.empty(B * S, N, device=gpu, dtype=torch.bfloat16)
+    assert _ops().gemm8(x, True, w, True, qkv, 0.0, None, 1.0, 4)
+    q2, k2, v2 = _ops().rope_split(qkv, cos, sin, B, S, Hq, Hkv, D)
+    assert torch.equal(v, v2)  # no rotation: the identical GEMM result
+    for a, b in ((q, q2), (k, k2)):
+        d = (a.float() - b.float()).abs()
+        assert d.max().item() <= 2 ** -6 * max(1.0, b.abs().max().item())  # one bf16 ulp (fma contraction)
+
+
+@pytest.mark.parametrize("T,F,K", [(256, 128, 512), (512, 1024, 1024), (4096, 14336, 4096)])
+def test_gemm8_swiglu_epilogue(gpu, T, F, K):
+    x = _mat(T, K, gpu, 3)
+    w = _mat(2 * F, K, gpu, 4, scale=0.05)
+    gu = torch.empty(T, 2 * F, device=gpu, dtype=torch.bfloat16)
+    mbuf = torch.empty(T, F + 64, device=gpu, dtype=torch.bfloat16)
+    m = mbuf[:, :F]
+    assert _ops().gemm8_swiglu(x, w, gu, m)
+    y = x.float() @ w.float().t()
+    assert _rel(gu, y) < 5e-3
+    mr = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+    assert _rel(m, mr) < 1e-2
+    # bitwise equal to the unfused kernels on the same GEMM result
+    gu2 = torch.empty_like(gu)
+    assert _ops().gemm8(x, True, w, True, gu2, 0.0, None, 1.0, 4)
+    assert torch.equal(gu, gu2)
+    assert torch.equal(m, _ops().swiglu_fwd(gu2, 0))
+
+
+def test_fused_layer_matches_unfused_autograd(gpu, monkeypatch):
+    """A 2-layer full fine-tune model (head dim 128): loss and every parameter gradient equal
+    between the fused-epilogue forward and the unfused ops (the same GEMM kernel underneath)."""
+    from mxllm.models import Llama, get_config
+    from mxllm.ops import fused
+
+    monkeypatch.setenv("MXLLM_GEMM8", "all")  # unfused path on gemm8 too: comparable GEMM results
+    cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
+    torch.manual_seed(0)
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=gpu)
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(fused, "_ON", on)
+        calls = []
+        for name in ("qkv_attention", "gate_up_swiglu"):
+            real = getattr(fused, name)
+            monkeypatch.setattr(fused, name, lambda *a, _r=real, _n=name, **k: (calls.append(_n), _r(*a, **k))[1])
+        model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3)
+        loss = model(ids, ids)
+        loss.backward()
+        res[on] = (float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+        assert (len(calls) == 4) == on, calls
+        monkeypatch.undo()
+        monkeypatch.setenv("MXLLM_GEMM8", "all")
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert abs(l1 - l0) < 1e-3 * abs(l0)
+    for n in g0:
+        assert _rel(g1[n], g0[n]) < 2e-2, n
