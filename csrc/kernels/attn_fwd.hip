@@ -35,6 +35,13 @@ namespace mx {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
+// s_waitcnt vmcnt(N) for a compile-time N (inline asm: invisible to hipcc's waitcnt pass)
+template <int N>
+__device__ __forceinline__ void g8_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 template <int CH>
 __device__ __forceinline__ int swz(int row) {
   return (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
@@ -56,7 +63,12 @@ __device__ __forceinline__ u16x4 tr_read(const char* p) {
 // NW waves per workgroup = 32 NW query rows sharing every streamed K/V tile (2 waves per SIMD
 // either way).  4 by default; 8 halves the K/V tile traffic per FLOP but measured the same
 // (0.259 vs 0.257 ms at B2 S2048 Hq64 Hkv8 D128 causal: the stream is not the limiter)
-template <int D, bool CAUSAL, int NW, bool PROF = false>
+// R: depth of the K/V tile ring in LDS (R - 1 tiles in flight ahead of the one being consumed).
+// One tile of lookahead (R = 2) left about a quarter of every tile waiting for the next tile's DMA
+// (profiles/r4ah/README.md): the DMA round trip is longer than one tile of MFMAs.  With 8 waves per
+// workgroup (one workgroup per CU, 256 query rows sharing every tile) a 3- or 4-deep ring fits the
+// CU's 160 KB of LDS (96 / 128 KB).
+template <int D, bool CAUSAL, int NW, bool PROF = false, int R = 2>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
@@ -76,7 +88,8 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   constexpr int TILE = BN * ROWB;
   constexpr int LPT = BN * CH / (64 * NW);
   static_assert(LPT >= 1 && BN * CH % (64 * NW) == 0, "K/V tile must split evenly over the waves");
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE];  // (XOR addressing: 256-B aligned)
+  static_assert(R >= 2 && R <= 4, "ring depth 2..4");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * R * TILE];  // (XOR addressing: 256-B aligned)
 
   const int nqb = (S + BM - 1) / BM;
   const int BH = B * Hq;
@@ -167,7 +180,9 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   }
 
   const uint32_t kq_base = lds0 + r * ROWB + 16 * (hh ^ swz<CH>(r));  // K row r, k step 0 (D = 128 path)
-  if (ntiles > 0) glds(0, 0);
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t)
+    if (t < ntiles) glds(t, t);  // the ring's first R - 1 tiles
   // Retire the prologue's Q loads and tile-0 DMA with a wait the compiler's
   // waitcnt pass can see (otherwise it treats them as possibly pending at the
   // loop header and drains the in-loop prefetch under the QK MFMAs).
@@ -180,10 +195,12 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   auto tile = [&](auto cur_c, int kt) {
     constexpr int CUR = decltype(cur_c)::value;
     if constexpr (PROF) tp0 = __builtin_amdgcn_s_memtime();
-    const bool more = kt + 1 < ntiles;
+    constexpr int NXT = (CUR + R - 1) % R;  // ring slot of tile kt + R - 1 (the slot tile kt - 1 used)
+    const int kpf = kt + R - 1;             // the tile this one prefetches
+    const bool more = kpf < ntiles;
     const char* kb = smem + CUR * 2 * TILE;
     const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
-    if (more && (!spread || !active)) glds(kt + 1, CUR ^ 1);  // prefetch next tile into the other buffer
+    if (more && (!spread || !active)) glds(kpf, NXT);  // prefetch R - 1 tiles ahead
     if (active) {
       f32x16 sacc[2];
 #pragma unroll
@@ -210,7 +227,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           pin(x[1]);
           sacc[0] = mfma32(x[0], qf[st], sacc[0]);
           sacc[1] = mfma32(x[1], qf[st], sacc[1]);
-          if (spread && more && (st % (KS / LPT)) == 0) glds_piece(kt + 1, CUR ^ 1, st / (KS / LPT));
+          if (spread && more && (st % (KS / LPT)) == 0) glds_piece(kpf, NXT, st / (KS / LPT));
         }
       } else {
 #pragma unroll
@@ -220,7 +237,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           for (int s = 0; s < KS; ++s) {
             const u16x8 a = *reinterpret_cast<const u16x8*>(kb + krow * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(krow)));
             sacc[n] = mfma32(a, qf[s], sacc[n]);
-            if (spread && more && n == 0 && (s % (KS / LPT)) == 0) glds_piece(kt + 1, CUR ^ 1, s / (KS / LPT));
+            if (spread && more && n == 0 && (s % (KS / LPT)) == 0) glds_piece(kpf, NXT, s / (KS / LPT));
           }
         }
       }
@@ -308,14 +325,32 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     } else {
       mark(5);
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for tile kt+1 landed
-    __syncthreads();                     // ... and every other wave's; buffer CUR free again
+    if constexpr (R == 2) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for tile kt+1 landed
+      __syncthreads();                     // ... and every other wave's; buffer CUR free again
+    } else {
+      // tile kt + 1 landed for this wave: the DMA of the tiles issued after it (at most R - 2, 2 LPT
+      // instructions each, retiring in issue order) may stay in flight.  Raw s_barrier: the fence of
+      // __syncthreads would drain them.  LDS reads of slot CUR retired first (it is restaged next).
+      const int after = min(R - 2, ntiles - 2 - kt);
+      lds_wait();
+      if (after <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (after == 1) g8_vmcnt<2 * LPT>();
+      else g8_vmcnt<4 * LPT>();
+      __builtin_amdgcn_s_barrier();
+    }
     mark(3);
     if constexpr (PROF) ph[4] += 1;
   };
-  for (int kt = 0; kt < ntiles; kt += 2) {
+  for (int kt = 0; kt < ntiles; kt += R) {
     tile(std::integral_constant<int, 0>{}, kt);
     if (kt + 1 < ntiles) tile(std::integral_constant<int, 1>{}, kt + 1);
+    if constexpr (R > 2) {
+      if (kt + 2 < ntiles) tile(std::integral_constant<int, 2 % R>{}, kt + 2);
+    }
+    if constexpr (R > 3) {
+      if (kt + 3 < ntiles) tile(std::integral_constant<int, 3 % R>{}, kt + 3);
+    }
   }
   float l_tot;
   {
@@ -732,6 +767,11 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_FWD_WAVES");
     return (e && e[0] == '8') ? 8 : 4;
   }();
+  static const int ring = [] {  // MXLLM_ATTN_FWD_RING=3|4: 8 waves with a 3- / 4-deep K/V ring (D = 128)
+    const char* e = getenv("MXLLM_ATTN_FWD_RING");
+    const int r = e && *e ? atoi(e) : 0;
+    return (r == 3 || r == 4) ? r : 0;
+  }();
   static const int fflags = [] {  // MXLLM_ATTN_FWD_FLAGS (default 1): bit 0 = spread the K/V DMA issue
     const char* e = getenv("MXLLM_ATTN_FWD_FLAGS");   // (B2 0.192 -> 0.186 ms, B16 1.372 -> 1.357 ms)
     return e && *e ? atoi(e) : 1;
@@ -765,6 +805,15 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
             sm[0] / nt, sm[1] / nt, sm[2] / nt, sm[3] / nt, sm[5] / nt, sm[6] / nwv, sm[7] / nwv, nt / nwv);
     return (int)hipGetLastError();
   }
+#define FWDR(C, RR)                                                                                    \
+  attn_fwd_kernel<128, C, 8, false, RR><<<((S + 255) / 256) * B * Hq, 512, 0, stream>>>(                 \
+      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
+  if (D == 128 && ring) {
+    if (ring == 3) { if (causal) FWDR(true, 3); else FWDR(false, 3); }
+    else { if (causal) FWDR(true, 4); else FWDR(false, 4); }
+    return (int)hipGetLastError();
+  }
+#undef FWDR
   if (D == 128) {
     if (nw128 == 8) { if (causal) FWD(128, true, 8); else FWD(128, false, 8); }
     else { if (causal) FWD(128, true, 4); else FWD(128, false, 4); }

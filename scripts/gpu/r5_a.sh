@@ -11,4 +11,15 @@ for f in 1 0; do
   MXLLM_FUSED_EPI=$f timeout -k 10 240 python bench.py --model llama3.1-8b --finetune full --steps 10 --warmup 3 \
     --no-calibrate --config2 off --json-out $O/c2_fused$f.json > $O/c2_fused$f.log 2>&1 || { echo "bench fused=$f failed"; exit 1; }
 done
-echo done
+
+# attention forward ring depth: parity at ring 3 / 4, then timing (B2 / B16, 70B heads)
+for RG in 3 4; do
+  MXLLM_ATTN_FWD_RING=$RG timeout -k 10 300 $T tests/test_kernels_gpu.py -k "attention" tests/test_strict_parity_gpu.py -k "attention" > $O/attn_ring$RG.log 2>&1 || echo "ring $RG parity FAILED"
+done
+for i in 1 2; do
+  for RG in 0 3 4; do
+    MXLLM_ATTN_FWD_RING=$RG timeout -k 10 120 python -u bench/attn_bench.py 2 64 8 2048 128 lite > $O/ab2_r${RG}_$i.txt 2>&1 || { echo "attn bench ring $RG failed"; exit 1; }
+    MXLLM_ATTN_FWD_RING=$RG timeout -k 10 120 python -u bench/attn_bench.py 16 64 8 2048 128 lite > $O/ab16_r${RG}_$i.txt 2>&1 || { echo "attn bench16 ring $RG failed"; exit 1; }
+  done
+done
+echo done2
