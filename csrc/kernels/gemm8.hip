@@ -641,9 +641,344 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
   }
 }
 
+// lane id regenerated on demand (volatile asm: never hoisted, so it is not a register that must
+// survive the persistent kernel's tile loop)
+__device__ __forceinline__ int g8_lane() {
+  int ln;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+  return ln;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent 4-phase variant: min(tiles, CUs) workgroups, each walking output
+// tiles t = L, L + G, ... (L = the XCD-contiguous remap of its id, so the G tiles in flight at a
+// time form 8 contiguous ranges, one per XCD / L2).  Between two tiles the NEXT tile's prologue
+// DMA (K-tile 0 and K-tile 1's B images) is issued BEFORE the current tile's epilogue stores, so
+// its latency runs under the stores, and the wait for it counts the stores as still in flight
+// (loads, stores and LDS-DMA retire in issue order): the stores never block the next tile's K loop.
+// No workgroup launch / drain between tiles.  K loop, images, swizzles and schedule: the PH = 4
+// path of gemm8_kernel above.
+template <bool A_KC, bool B_KC, bool OUT_F32, bool BETA>
+__global__ void __launch_bounds__(512, 1)
+gemm8p_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+              void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
+              float alpha_f) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * G8_TILE];
+  const int nM = M >> 8, nN = N >> 8, tiles = nM * nN, G = gridDim.x;
+  int L = xcd_remap(blockIdx.x, G);
+  if (L >= tiles) return;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int nk = (K + G8_BK - 1) / G8_BK;
+  const float alpha = alpha_f * (alpha_t ? alpha_t[0] : 1.f);
+
+  auto tile_of = [&](int l, int& pm, int& pn) __attribute__((always_inline)) {
+    constexpr int GM = 8;
+    const int per = GM * nN, grp = l / per, first = grp * GM;
+    const int rows = min(GM, nM - first), in = l - grp * per;
+    pm = first + in % rows;
+    pn = in / rows;
+  };
+  int pm, pn;
+  tile_of(L, pm, pn);
+  int m0 = pm << 8, n0 = pn << 8;
+  const uint32_t arec = A_KC ? (uint32_t)((255 * lda + (int64_t)nk * G8_BK) * 2) : (uint32_t)(((int64_t)K * lda - m0) * 2);
+  const uint32_t brec = B_KC ? (uint32_t)((255 * ldb + (int64_t)nk * G8_BK) * 2) : (uint32_t)(((int64_t)K * ldb - n0) * 2);
+  // mn-contiguous operands: the record limit depends on the tile's column offset (rows past K -> 0)
+  auto rsrc_a = [&](int mm0) __attribute__((always_inline)) {
+    const uint16_t* base = A_KC ? A + (int64_t)mm0 * lda : A + mm0;
+    const uint32_t rec = A_KC ? arec : (uint32_t)(((int64_t)K * lda - mm0) * 2);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, rec, 0x00020000);
+  };
+  auto rsrc_b = [&](int nn0) __attribute__((always_inline)) {
+    const uint16_t* base = B_KC ? B + (int64_t)nn0 * ldb : B + nn0;
+    const uint32_t rec = B_KC ? brec : (uint32_t)(((int64_t)K * ldb - nn0) * 2);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, rec, 0x00020000);
+  };
+  __amdgpu_buffer_rsrc_t ars = rsrc_a(m0), brs = rsrc_b(n0);
+  const uint32_t astep = A_KC ? G8_BK * 2 : (uint32_t)(G8_BK * lda * 2);
+  const uint32_t bstep = B_KC ? G8_BK * 2 : (uint32_t)(G8_BK * ldb * 2);
+  // lane-derived addresses are recomputed per tile from an opaque copy of the lane id (hipcc cannot
+  // hoist them out of the tile loop): they are not live across the epilogue, whose fp32 / beta
+  // forms otherwise spill at the 256-VGPR budget of two waves per SIMD
+  uint32_t aoff[2][2], boff[2][2];
+  auto offsets = [&]() __attribute__((always_inline)) {
+    const int ln = g8_lane();
+    g8_src_offsets<A_KC, true>(w, ln, lda, 0, aoff[0]);
+    g8_src_offsets<A_KC, true>(w, ln, lda, 1, aoff[1]);
+    g8_src_offsets<B_KC, false>(w, ln, ldb, 0, boff[0]);
+    g8_src_offsets<B_KC, false>(w, ln, ldb, 1, boff[1]);
+  };
+  offsets();
+  auto issue = [&](int kt, int img) __attribute__((always_inline)) {
+    char* dst = smem + (kt & 1) * G8_TILE + img * G8_HT + (2 * w) * 1024;
+    if (img < 2) {
+      const uint32_t so = (uint32_t)kt * astep;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (g8lptr_t)dst, 16, aoff[img][0] + so, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (g8lptr_t)(dst + 1024), 16, aoff[img][1] + so, 0, 0, 0);
+    } else {
+      const uint32_t so = (uint32_t)kt * bstep;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (g8lptr_t)dst, 16, boff[img - 2][0] + so, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (g8lptr_t)(dst + 1024), 16, boff[img - 2][1] + so, 0, 0, 0);
+    }
+  };
+  // the prologue DMA of a tile: K-tile 0 (4 images) + K-tile 1's B images
+  auto prologue = [&]() __attribute__((always_inline)) {
+    issue(0, 2);
+    issue(0, 0);
+    issue(0, 3);
+    issue(0, 1);
+    if (nk > 1) {
+      issue(1, 2);
+      issue(1, 3);
+    }
+  };
+
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t akc[2], amn[4], bmn[2];
+  auto lds_lanes = [&]() __attribute__((always_inline)) {
+    const int ln = g8_lane();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) akc[s] = g8_kc_lane(ln, s);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) amn[i] = g8_mn_lane(ln, wr * 64 + 16 * i);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bmn[j] = g8_mn_lane(ln, wc * 32 + 16 * j);
+  };
+  u16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  f32x4 acc[8][4];
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto read_a = [&](int buf, int img) __attribute__((always_inline)) {
+    const uint32_t ib = lds0 + buf * G8_TILE + img * G8_HT;
+    if constexpr (A_KC) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t b = ib + akc[s];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i][s] = rd128_off(b, (wr * 64 + 16 * i) * 128);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t b = ib + amn[i];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u16x4 lo = trd_off(b, 8192 * s), hi = trd_off(b, 8192 * s + 1024);
+          fa[i][s] = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+    }
+  };
+  auto read_b = [&](int buf, int img, u16x8(&fb)[2][2]) __attribute__((always_inline)) {
+    const uint32_t ib = lds0 + buf * G8_TILE + (2 + img) * G8_HT;
+    if constexpr (B_KC) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t b = ib + akc[s];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j][s] = rd128_off(b, (wc * 32 + 16 * j) * 128);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t b = ib + bmn[j];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u16x4 lo = trd_off(b, 8192 * s), hi = trd_off(b, 8192 * s + 1024);
+          fb[j][s] = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+    }
+  };
+  auto pin_a = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pin(fa[i][0]);
+      pin(fa[i][1]);
+    }
+  };
+  auto pin_b = [&](u16x8(&fb)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      pin(fb[j][0]);
+      pin(fb[j][1]);
+    }
+  };
+  auto mma = [&](int qa, int qb, u16x8(&fb)[2][2]) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 * qa + i][2 * qb + j] = g8_mfma(fb[j][s], fa[i][s], acc[4 * qa + i][2 * qb + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto vm4 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); };
+  auto vm0 = []() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+#define G8P_SYNC_MMA2(QA, QB0, FB0, QB1, FB1) \
+  __builtin_amdgcn_s_barrier();               \
+  pin_a();                                    \
+  pin_b(FB0);                                 \
+  pin_b(FB1);                                 \
+  mma(QA, QB0, FB0);                          \
+  mma(QA, QB1, FB1);                          \
+  __builtin_amdgcn_s_barrier();
+
+  zero_acc();
+  prologue();
+  // stores of the previous tile issued after this tile's prologue DMA (0 for the first tile): the
+  // in-order wait for K-tile 0 leaves them (and K-tile 1's B images) in flight
+  bool stores_pending = false;
+  for (;;) {
+    if (stores_pending) {
+      if (nk > 1) {
+        if constexpr (OUT_F32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");  // 4 DMA + 32 stores
+        else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");                    // 4 DMA + 16 stores
+      } else {
+        if constexpr (OUT_F32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      }
+    } else {
+      if (nk > 1) vm4(); else vm0();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+    lds_lanes();
+    offsets();
+    for (int kt = 0;; kt += 2) {
+      read_b(0, 0, fb0);
+      read_b(0, 1, fb1);
+      read_a(0, 0);
+      if (kt + 1 < nk) {
+        issue(kt + 1, 0);
+        issue(kt + 1, 1);
+      }
+      lds_wait();
+      G8P_SYNC_MMA2(0, 0, fb0, 1, fb1)
+      read_a(0, 1);
+      if (kt + 2 < nk) {
+        issue(kt + 2, 2);
+        issue(kt + 2, 3);
+        vm4();
+      } else {
+        vm0();
+      }
+      lds_wait();
+      G8P_SYNC_MMA2(1, 1, fb1, 0, fb0)
+      if (kt + 1 >= nk) break;
+      read_b(1, 0, fb0);
+      read_b(1, 1, fb1);
+      read_a(1, 0);
+      if (kt + 2 < nk) {
+        issue(kt + 2, 0);
+        issue(kt + 2, 1);
+      }
+      lds_wait();
+      G8P_SYNC_MMA2(0, 0, fb0, 1, fb1)
+      read_a(1, 1);
+      if (kt + 3 < nk) {
+        issue(kt + 3, 2);
+        issue(kt + 3, 3);
+        vm4();
+      } else {
+        vm0();
+      }
+      lds_wait();
+      G8P_SYNC_MMA2(1, 1, fb1, 0, fb0)
+      if (kt + 2 >= nk) break;
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // match the stagger: every wave's LDS reads are done
+    // ---- next tile's prologue DMA first (LDS is free), then this tile's epilogue
+    const int cm0 = m0, cn0 = n0;
+    const int Ln = L + G;
+    const bool more = Ln < tiles;
+    if (more) {
+      tile_of(Ln, pm, pn);
+      m0 = pm << 8;
+      n0 = pn << 8;
+      ars = rsrc_a(m0);
+      brs = rsrc_b(n0);
+      offsets();
+      prologue();
+    }
+    const int ln = g8_lane();
+    const int ml = cm0 + wr * 128 + (ln & 15);
+    const int nl = cn0 + wc * 64 + 4 * (ln >> 4);
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa) {
+      f32x4 old[4][4];
+      if constexpr (BETA) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t m = ml + qa * 64 + 16 * i;
+            const int n = nl + 32 * (j >> 1) + 16 * (j & 1);
+            if constexpr (OUT_F32) {
+              old[i][j] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(C) + m * ldc + n);
+            } else {
+              const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(C) + m * ldc + n);
+              old[i][j] = f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                                __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+            }
+          }
+      }
+      if constexpr (OUT_F32) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t m = ml + qa * 64 + 16 * i;
+            const int n = nl + 32 * (j >> 1) + 16 * (j & 1);
+            f32x4 v = acc[4 * qa + i][j] * alpha;
+            if constexpr (BETA) v += old[i][j];
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + m * ldc + n) = v;
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jp = 0; jp < 2; ++jp) {
+            f32x4 va = acc[4 * qa + i][2 * jp] * alpha, vb = acc[4 * qa + i][2 * jp + 1] * alpha;
+            if constexpr (BETA) {
+              va += old[i][2 * jp];
+              vb += old[i][2 * jp + 1];
+            }
+            const int64_t m = ml + qa * 64 + 16 * i;
+            const int n = cn0 + wc * 64 + 32 * jp + 16 * ((ln >> 4) & 1) + 8 * (ln >> 5);
+            g8_store8(reinterpret_cast<uint16_t*>(C) + m * ldc + n, va, vb);
+          }
+      }
+    }
+    if (!more) break;
+    zero_acc();
+    L = Ln;
+    stores_pending = !BETA;  // with BETA the epilogue's loads already drained the DMA (in-order waits)
+  }
+#undef G8P_SYNC_MMA2
+}
+
 }  // namespace mx
 
 using namespace mx;
+
+// compute units of the current device (the persistent grid: one workgroup per CU)
+static int g8_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t p;
+    n = hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+  }
+  return n;
+}
 
 // C[M, N] = alpha * op(A) op(B) + beta * C.  a_kc: A stored [M][K] (else [K][M]); b_kc: B stored [N][K]
 // (else [K][N]); row strides in elements.  Takes M, N multiples of 256; K a multiple of 64 when an
@@ -705,6 +1040,25 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
     }
   }
 #endif
+  const char* pe = getenv("MXLLM_GEMM8_PERSIST");  // 1 = persistent 4-phase kernel (read per call: A/B)
+  const int persist = pe && *pe ? atoi(pe) : 0;
+  if (persist && ph4 && grid > g8_cus()) {
+    const int pg = g8_cus();
+#define G8_P(AK, BK_, F, BT) \
+  gemm8p_kernel<AK, BK_, F, BT><<<pg, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, alpha_f)
+#define G8_PO(AK, BK_)                                                       \
+  do {                                                                       \
+    if (out_f32) { if (acc) G8_P(AK, BK_, true, true); else G8_P(AK, BK_, true, false); }     \
+    else { if (acc) G8_P(AK, BK_, false, true); else G8_P(AK, BK_, false, false); }           \
+  } while (0)
+    if (a_kc && b_kc) G8_PO(true, true);
+    else if (a_kc) G8_PO(true, false);
+    else if (b_kc) G8_PO(false, true);
+    else G8_PO(false, false);
+#undef G8_PO
+#undef G8_P
+    return (int)hipGetLastError();
+  }
   if (a_kc && b_kc)
     G8_OUT(true, true);
   else if (a_kc)

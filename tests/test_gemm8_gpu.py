@@ -152,3 +152,28 @@ def test_gemm_dispatch_uses_tail_entry(gpu, monkeypatch):
     y = gemm.mm("tn", x, w)
     assert calls == ["gemm8_tail"]
     _check(y, x.float() @ w.float().t(), 5e-3)
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("f32,beta", [(False, 0.0), (True, 0.0), (True, 1.0), (False, 1.0)])
+def test_gemm8_persistent_bitwise(gpu, a_kc, b_kc, f32, beta, monkeypatch):
+    """Persistent tile-looping kernel (MXLLM_GEMM8_PERSIST=1): more tiles than
+    CUs (each workgroup walks several, next tile's DMA issued under the previous epilogue), odd
+    K-tile counts -- bitwise equal to the one-tile-per-workgroup kernel (same K order per tile)
+    and to the fp32 reference."""
+    M, N, K = 4096, 4352, 704 if (a_kc or b_kc) else 700  # 16 x 17 = 272 tiles; 11 K-tiles
+    a = _mat(M, K, gpu, pad=8, seed=21) if a_kc else _mat(K, M, gpu, pad=8, seed=21)
+    b = _mat(N, K, gpu, pad=8, seed=22) if b_kc else _mat(K, N, gpu, pad=8, seed=22)
+    A = a.float() if a_kc else a.float().t()
+    B = b.float().t() if b_kc else b.float()
+    dt = torch.float32 if f32 else torch.bfloat16
+    c0 = _mat(M, N, gpu, seed=23).to(dt)
+    outs = {}
+    for p in ("0", "1"):
+        monkeypatch.setenv("MXLLM_GEMM8_PERSIST", p)
+        out = c0.clone()
+        assert _ops().gemm8(a, a_kc, b, b_kc, out, beta, None, 1.0, 4)
+        outs[p] = out
+    assert torch.equal(outs["0"], outs["1"])
+    ref = A @ B + (c0.float() if beta else 0.0)
+    _check(outs["1"], ref, 1e-5 if f32 else 5e-3)
