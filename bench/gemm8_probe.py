@@ -68,9 +68,24 @@ def _ph4(fn):
     return f
 
 
+def _persist(fn):
+    """the same call on the persistent 4-phase kernel (MXLLM_GEMM8_PERSIST=1, read per launch)"""
+    def f():
+        os.environ["MXLLM_GEMM8_PH"] = "4"
+        os.environ["MXLLM_GEMM8_PERSIST"] = "1"
+        try:
+            fn()
+        finally:
+            os.environ.pop("MXLLM_GEMM8_PH", None)
+            os.environ.pop("MXLLM_GEMM8_PERSIST", None)
+    return f
+
+
 def run_case(name, flops, variants, rounds, calls):
     if os.environ.get("_G8_PH4_ALL") == "1" and "gemm8" in variants and "gemm8_ph4" not in variants:
         variants = dict(variants, gemm8_ph4=_ph4(variants["gemm8"]))
+    if os.environ.get("_G8_PERSIST_ALL") == "1" and "gemm8" in variants and "gemm8_p" not in variants:
+        variants = dict(variants, gemm8_p=_persist(variants["gemm8"]))
     res = {k: [] for k in variants}
     for _ in range(rounds):
         for k, fn in variants.items():
@@ -103,6 +118,7 @@ def main():
     ap.add_argument("--layout-exp-only", action="store_true")
     ap.add_argument("--ablate", action="store_true", help="timing-only ablation builds of the NN kernel")
     ap.add_argument("--ph4", action="store_true", help="also time every gemm8 call on the 4-phase schedule")
+    ap.add_argument("--persist", action="store_true", help="also time every gemm8 call on the persistent kernel")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     if not a.no_table:
@@ -125,6 +141,8 @@ def main():
     del wa, wb, wo
     if a.ph4:
         os.environ["_G8_PH4_ALL"] = "1"
+    if a.persist:
+        os.environ["_G8_PERSIST_ALL"] = "1"
     forms = a.forms.split(",")
     models = [] if a.aug_only else (["70b", "8b"] if a.model == "both" else [a.model])
     a.aug = a.aug or a.aug_only
@@ -139,6 +157,8 @@ def main():
         ph, g, tail = 8, res["gemm8"]["ms"], 0
         if "gemm8_ph4" in res and res["gemm8_ph4"]["ms"] < g:
             ph, g = 4, res["gemm8_ph4"]["ms"]
+        if "gemm8_p" in res and res["gemm8_p"]["ms"] < g:
+            ph, g = 5, res["gemm8_p"]["ms"]  # ph 5 = the persistent 4-phase kernel (csrc/kernels/gemm8.hip)
         if "gemm8_tail" in res and res["gemm8_tail"]["ms"] < g:
             ph, g, tail = 4, res["gemm8_tail"]["ms"], gemm.tail_split(M, N, K)
         d = res[DEFAULT[form]]["ms"]

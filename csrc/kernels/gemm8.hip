@@ -1001,7 +1001,7 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
   const int grid = (M >> 8) * (N >> 8);
   const bool acc = beta != 0.f;
   const char* phs = getenv("MXLLM_GEMM8_PH");  // read per call: overrides `ph` (same-process A/B)
-  const bool ph4 = phs && *phs ? atoi(phs) == 4 : ph == 4;
+  const bool ph4 = phs && *phs ? atoi(phs) == 4 : (ph == 4 || ph == 5);  // 5 = 4-phase, persistent
 #define G8_L(AK, BK_, F, BT)                                                                                        \
   do {                                                                                                              \
     if (ph4)                                                                                                        \
@@ -1041,7 +1041,7 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
   }
 #endif
   const char* pe = getenv("MXLLM_GEMM8_PERSIST");  // 1 = persistent 4-phase kernel (read per call: A/B)
-  const int persist = pe && *pe ? atoi(pe) : 0;
+  const int persist = pe && *pe ? atoi(pe) : (ph == 5);
   if (persist && ph4 && grid > g8_cus()) {
     const int pg = g8_cus();
 #define G8_P(AK, BK_, F, BT) \
