@@ -612,6 +612,9 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
         dp = mfma32b(x[2], x[3], dp);
         if (spread && (st & 1) == 0 && more) glds_piece(nx_hj, nx_it, buf ^ 1, st >> 1);
         if (spread && st == KS - 1 && more) glds_piece(nx_hj, nx_it, buf ^ 1, 4);
+        // pin the DMA issue order: the counted end-of-tile wait assumes every DMA piece
+        // precedes the 4 dS^T stores; no instruction is scheduled across this point
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     mark(1);
@@ -686,6 +689,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
       // dS stores here, not among the S/dP steps: next to the in-flight LDS-DMA they stalled
       // issue (B16 5.13 -> 6.09 ms); (prio & 64: at the loop top instead, A/B)
       if (spread && (i & 1) == 0 && (prio & 64) == 0) flush_ds_piece(i >> 1);
+      __builtin_amdgcn_sched_barrier(0);  // the dS^T stores stay after the DMA and in this order
     }
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq)
@@ -697,7 +701,12 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     // dS^T stores (issued after the DMA; loads, stores and LDS-DMA retire in issue order) in flight
     // across the barrier instead of waiting for their completion
     static_assert(2 * DB == 8, "4 dS store pieces per tile (D = 128)");
-    if ((prio & 256) && ds_young) {
+#ifdef MXLLM_ATTN_BWD_NO_COUNTED_WAIT
+    constexpr bool kCounted = false;  // build fallback: mxllm/_build.py found the ISA invariant broken
+#else
+    constexpr bool kCounted = true;
+#endif
+    if (kCounted && (prio & 256) && ds_young) {
       // raw barrier: __syncthreads()'s fence would wait for the stores (vmcnt(0)) after all; the
       // LDS reads of this tile are retired (lgkmcnt(0)), the DMA by the counted wait
       __builtin_amdgcn_s_waitcnt(0x0074);  // vmcnt(4) lgkmcnt(0)

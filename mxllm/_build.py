@@ -75,6 +75,56 @@ def _check_loadable(path: str) -> None:
         raise RuntimeError(f"built library does not load: {r.stderr.strip()[-600:]}")
 
 
+def _attn_bwd_counted_wait_ok(asm: str) -> tuple[bool, str]:
+    """ISA invariant of the attention backward's counted end-of-tile wait: every
+    ``s_waitcnt vmcnt(4) lgkmcnt(0)`` in front of an ``s_barrier`` must have at least 4 vector-memory
+    instructions (the dS^T stores) between it and the last LDS-DMA issue before it -- then, with
+    in-order retirement, vmcnt(4) implies the DMA landed.  Returns (ok, detail)."""
+    import re
+
+    found = 0
+    for fn in re.findall(r"^(_ZN2mx16attn_bwd8_kernel\w+):", asm, re.M):
+        i = asm.index(fn + ":")
+        j = asm.index(".Lfunc_end", i)
+        lines = [x.strip() for x in asm[i:j].splitlines()]
+        for k, line in enumerate(lines):
+            if not line.startswith("s_waitcnt vmcnt(4) lgkmcnt(0)") or k + 1 >= len(lines) or lines[k + 1] != "s_barrier":
+                continue
+            found += 1
+            n, kk = 0, k - 1
+            while kk >= 0 and not (("buffer_load" in lines[kk] and " lds" in lines[kk]) or "global_load_lds" in lines[kk]):
+                if re.match(r"(global|buffer|scratch|flat)_(store|load|atomic)", lines[kk]):
+                    n += 1
+                kk -= 1
+            if n < 4:
+                return False, f"{fn}: {n} vector-memory ops between the last LDS-DMA and the counted wait"
+    return True, f"{found} counted waits checked"
+
+
+# post-compile ISA checks: file -> (check(asm) -> (ok, detail), fallback compiler flag)
+ISA_CHECKS = {"attn_bwd.hip": (_attn_bwd_counted_wait_ok, "-DMXLLM_ATTN_BWD_NO_COUNTED_WAIT")}
+
+
+def _compile_checked(src: str, obj: str, cmd: list[str], flags: list[str]) -> str:
+    """Compile; for a file with an ISA check, also emit its device assembly and verify it -- on a
+    failed check recompile with the check's fallback flag (the safe, slower schedule)."""
+    out = _run(cmd)
+    chk = ISA_CHECKS.get(os.path.basename(src))
+    if chk is None:
+        return out
+    fn, fallback = chk
+    asm_path = obj + ".s"
+    _run([os.path.join(ROCM, "bin", "hipcc")] + flags + ["-S", "--offload-device-only", src, "-o", asm_path])
+    with open(asm_path) as f:
+        ok, detail = fn(f.read())
+    os.remove(asm_path)
+    if ok:
+        return out + f"\n[isa check {os.path.basename(src)}] ok: {detail}"
+    print(f"[mxllm build] WARNING: ISA check of {os.path.basename(src)} failed ({detail}); "
+          f"rebuilding with {fallback}", file=sys.stderr, flush=True)
+    return _run([os.path.join(ROCM, "bin", "hipcc")] + flags + [fallback, "-c", src, "-o", obj])
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     inc, tlib, abi = _torch_paths()
     os.makedirs(OUT_DIR, exist_ok=True)
@@ -99,22 +149,26 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
         key = _hash([src] + hdrs, " ".join(flags))
         obj = os.path.join(OUT_DIR, os.path.basename(src) + f".{key}.o")
         cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + ["-c", src, "-o", obj]
-        jobs_list.append((src, obj, cmd))
+        jobs_list.append((src, obj, cmd, flags))
     for src in cpp_srcs:
         key = _hash([src] + hdrs, " ".join(cxx_flags))
         obj = os.path.join(OUT_DIR, os.path.basename(src) + f".{key}.o")
         cmd = ["g++"] + cxx_flags + ["-c", src, "-o", obj]
-        jobs_list.append((src, obj, cmd))
+        jobs_list.append((src, obj, cmd, None))
 
-    todo = [(s, o, c) for (s, o, c) in jobs_list if force or not os.path.exists(o)]
+    todo = [j for j in jobs_list if force or not os.path.exists(j[1])]
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            futs = {ex.submit(_run, c): s for (s, o, c) in todo}
+            futs = {ex.submit(_compile_checked if fl is not None else (lambda s_, o_, c_, f_: _run(c_)), s, o, c, fl): s
+                    for (s, o, c, fl) in todo}
             for f in cf.as_completed(futs):
-                f.result()
+                out = f.result()
                 if verbose:
                     print(f"[mxllm build] compiled {os.path.relpath(futs[f], ROOT)}", flush=True)
-    objs = [o for (_, o, _) in jobs_list]
+                    for line in out.splitlines():
+                        if line.startswith("[isa check"):
+                            print("[mxllm build] " + line[1:].replace("]", ":", 1), flush=True)
+    objs = [j[1] for j in jobs_list]
     link_key = _hash([], "|".join(objs))
     stamp = LIB_PATH + ".stamp"
     if force or not os.path.exists(LIB_PATH) or not os.path.exists(stamp) or open(stamp).read() != link_key:

@@ -159,7 +159,7 @@ def test_config4_failed_child_is_retried_deeper(monkeypatch):
         return {"error": "child job exit code 1"} if len(calls) <= fails[0] else {"ms_per_step": 1.0}
 
     monkeypatch.setattr(bench, "run_config4", fake)
-    a = argparse.Namespace(config4_act_ckpt_layers=None)
+    a = argparse.Namespace(config4_act_ckpt_layers=None, config4_timeout=360.0, time_budget_s=1e9, child_min_s=90.0)
     r = bench.run_config4_planned(a, 8, 308.0)
     assert calls == [0, 40] and r["ms_per_step"] == 1.0
     assert r["hbm_plan"]["checkpointed_layers"] == 40 and r["hbm_plan"]["first_attempt"]["checkpointed_layers"] == 0
@@ -173,6 +173,11 @@ def test_config4_failed_child_is_retried_deeper(monkeypatch):
     a.config4_act_ckpt_layers = 56
     r = bench.run_config4_planned(a, 8, 308.0)
     assert calls == [56] and "error" in r
+    # no budget left for a retry: the failed first attempt is reported, the retry skipped
+    calls.clear()
+    a.config4_act_ckpt_layers, a.time_budget_s = None, 0.0
+    r = bench.run_config4_planned(a, 8, 308.0)
+    assert calls == [0] and "error" in r and "time budget" in r["retry_skipped"]
 
 
 def test_world8_hung_config4_child_keeps_headline_inside_budget():
