@@ -775,6 +775,331 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
   }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 15] (immediate per case; inline asm is
+// invisible to hipcc's waitcnt pass)
+__device__ __forceinline__ void vm_wait_le(int n) {
+  switch (n) {
+#define MX_VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    MX_VMC(1) MX_VMC(2) MX_VMC(3) MX_VMC(4) MX_VMC(5) MX_VMC(6) MX_VMC(7) MX_VMC(8)
+    MX_VMC(9) MX_VMC(10) MX_VMC(11) MX_VMC(12) MX_VMC(13) MX_VMC(14) MX_VMC(15)
+#undef MX_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// Staggered split-mode key-block kernel (MXLLM_ATTN_BWD8=2).  Same work split
+// as attn_bwd8_kernel (8 waves = 4 key groups x 2 q halves, 128 keys of one q head per workgroup),
+// but the two q halves run HALF A TILE apart: each tile is two phases -- A: S = Q K^T, dP = dO V^T
+// and the softmax, B: dV^T += dO^T P, dK^T += Q^T dS -- separated by a barrier, and waves 4-7 start
+// one barrier late.  One half's softmax VALU then runs under the other half's MFMAs (in
+// attn_bwd8_kernel both halves hit the softmax at the same time behind one barrier per tile, and the
+// faster half waited ~1,260 cycles per tile: profiles/r4ad/README.md).  The offset needs the Q / dO
+// tiles of THREE iterations in LDS (a 3-slot ring, 96 KB + the 64 KB K / V images = the CU's whole
+// 160 KB), so lse / delta no longer go through LDS: each wave loads its 32 rows' values one
+// iteration ahead into one VGPR (lanes 0-31 lse, 32-63 delta) and broadcasts them with shuffles.
+// Issue / wait schedule (barrier numbers of the leading half: tile L = barriers 2L .. 2L+2):
+//   lead (waves 0-3) issues iteration L+2's DMA and L+1's lse/delta at the start of its phase B(L),
+//   lag (waves 4-7) at the start of its phase A(L) -- both right after slot (L+2) % 3 was last read
+//   (barrier 2L+1) -- and each waits for iteration L+1's DMA only at the barrier before which it
+//   must have landed (2L+2 for the lead's B(L), 2L+2 for the lag's A(L)), with counted vmcnt waits
+//   that leave the newer loads / DMA / dS^T stores in flight (retirement is in issue order; the
+//   issue order is pinned with sched_barrier).  1.5 tiles of DMA lookahead instead of 1.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(512, 1)
+attn_bwd8s_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                  const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                  uint16_t* __restrict__ dST, float* __restrict__ dKp, float* __restrict__ dVp, int B, int Hq,
+                  int Hkv, int S, int Sk, int off, float sl, float scale, int S_pad, int hpw) {
+  constexpr int D = 128, BN = 128, BQ = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int KIMG = BN * ROWB;  // K (or V) image [128][D]: 32 KB
+  constexpr int QT = BQ * ROWB;    // Q / dO tile [64][D]: 16 KB
+  constexpr int SLOT = 2 * QT;     // ring slot: Q tile | dO tile
+  constexpr int NSLOT = 3;
+  constexpr int LDSB = 2 * KIMG + NSLOT * SLOT;
+  static_assert(LDSB <= 160 * 1024, "the CU's LDS");
+  static_assert(LDSB >= 4 * 2 * DB * 16 * 64 * 4, "dK/dV pair reduction reuses the tile LDS");
+  constexpr int SEGS = QT / 1024;
+  static_assert(SEGS / 8 == 2, "two pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[LDSB];
+  char* kimg = smem;
+  char* vimg = smem + KIMG;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+
+  const int nkb = (Sk + BN - 1) / BN;
+  const int HP = Hq / hpw;
+  const int BHP = B * HP;
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BHP, (Hq / Hkv) / hpw);
+  const int kb = bid / BHP;
+  const int bhp = bid % BHP;
+  if (kb >= nkb) return;
+  const int b = bhp / HP, hp = bhp % HP, h0 = hp * hpw, hk = h0 / (Hq / Hkv);
+  const uint16_t* Kp = K + (size_t)(b * Hkv + hk) * Sk * D;
+  const uint16_t* Vp = V + (size_t)(b * Hkv + hk) * Sk * D;
+  const size_t dstride = (size_t)Hq * D;
+  auto Qp = [&](int h) { return Q + (size_t)(b * Hq + h) * S * D; };
+  auto dOp = [&](int h) { return dO + (size_t)b * S * dstride + (size_t)h * D; };
+  auto dstp = [&](int h) { return dST + (size_t)(b * Hq + h) * (nkb * BN) * S_pad; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = w & 3, m = w >> 2;  // m = 0: the leading half, 1: the lagging half
+  const int r = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int k0 = kb * BN;
+  const int key = k0 + 32 * kg + r;
+
+  {  // K / V images of the key block (rows past Sk read as zeros: masked)
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)Kp, 0, Sk * ROWB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)Vp, 0, Sk * ROWB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < KIMG / 1024 / 8; ++i) {
+      const int seg = w * (KIMG / 1024 / 8) + i;
+      const int row = seg * (1024 / ROWB) + lane / (ROWB / 16), slot = lane % (ROWB / 16);
+      const int vo = (k0 + row) * ROWB + 16 * (slot ^ swzb<CH>(row));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kimg + seg * 1024), 16, vo, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vimg + seg * 1024), 16, vo, 0, 0, 0);
+    }
+  }
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { dk[d][j] = 0.f; dv[d][j] = 0.f; }
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, (k0 - off) / BQ * BQ);
+  const int nqt = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
+  const int nit = nqt * hpw;  // flattened (head, q tile) iterations
+
+  const int orec = (int)(((size_t)(S - 1) * dstride + D) * 2);
+  const int pseg = w * (SEGS / 8);
+  typedef int i32x2_t __attribute__((ext_vector_type(2)));
+  i32x2_t qoff = {0, 0}, ooff = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int prow = (pseg + i) * (1024 / ROWB) + lane / (ROWB / 16), pslot = lane % (ROWB / 16);
+    const int pch = pslot ^ swzb<CH>(prow);
+    qoff[i] = prow * ROWB + pch * 16;
+    ooff[i] = (int)(prow * dstride * 2) + pch * 16;
+  }
+  // iteration L -> (head offset hj, q tile it)
+  auto iter = [&](int L, int& hj, int& it) {
+    hj = L / nqt;
+    it = L - hj * nqt;
+  };
+  // this wave's 4 DMA pieces (2 Q, 2 dO) of iteration L into ring slot L % 3
+  auto dma_to = [&](int L, int slot) {
+    int hj, it;
+    iter(L, hj, it);
+    const int h = h0 + hj, q0 = qstart + it * BQ;
+    char* qt = smem + 2 * KIMG + slot * SLOT;
+    char* dot = qt + QT;
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc((void*)Qp(h), 0, S * ROWB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc((void*)dOp(h), 0, orec, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lptr_t)(qt + (pseg + i) * 1024), 16, qoff[i] + q0 * ROWB, 0, 0,
+                                               0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (lptr_t)(dot + (pseg + i) * 1024), 16,
+                                               ooff[i] + (int)(q0 * dstride * 2), 0, 0, 0);
+    }
+  };
+  // lse (lanes 0-31) / delta (lanes 32-63) of this wave's 32 rows of iteration L: ONE load
+  auto ldload = [&](int L) -> float {
+    int hj, it;
+    iter(L, hj, it);
+    const int h = h0 + hj;
+    const int q = min(qstart + it * BQ + 32 * m + r, S - 1);
+    const float* base = (hh ? DELTA : LSE) + (size_t)(b * Hq + h) * S;
+    return base[q];
+  };
+
+
+  const uint32_t tile_base = lds_addr(smem + 2 * KIMG);
+  static_assert(ROWB == 256 && (SLOT % 256) == 0 && (KIMG % 256) == 0, "XOR addressing assumes 256-B rows");
+  uint32_t trA, trB;
+  {
+    const int rowA = 32 * m + 4 * hh + tq, rowB = rowA + 8;
+    const int chunk = (16 * (g & 1) + 4 * tp) >> 3;
+    trA = rowA * ROWB + 16 * (chunk ^ swzb<CH>(rowA)) + 8 * (tp & 1);
+    trB = rowB * ROWB + 16 * (chunk ^ swzb<CH>(rowB)) + 8 * (tp & 1);
+  }
+  const int swz = swzb<CH>(r);
+  const uint32_t qrowb = (32 * m + r) * ROWB + 16 * (hh ^ swz);
+  const uint32_t krowb = lds_addr(kimg) + (32 * kg + r) * ROWB + 16 * (hh ^ swz);
+
+  // prologue: K / V images, iterations 0 and 1, lse / delta of iteration 0; all landed
+  float ldc = 0.f, ldn = 0.f;
+  if (nit > 0) {
+    ldc = ldload(0);
+    dma_to(0, 0);
+  }
+  if (nit > 1) dma_to(1, 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  if (m == 1) __builtin_amdgcn_s_barrier();  // the lagging half starts one barrier late
+
+  // ops this wave issues per iteration: the next lse/delta (1) and the DMA two iterations ahead (4)
+  // -- UNCONDITIONALLY (past the last iteration: the last iteration's data again, into the slot
+  // nobody reads any more), so every iteration issues the same ops and hipcc's own waits for the
+  // lse/delta register stay counted -- and the previous iteration's dS^T stores (4, from L = 1 on)
+  auto issue_ahead = [&](int L) {
+    ldn = ldload(min(L + 1, nit - 1));
+    __builtin_amdgcn_sched_barrier(0);
+    dma_to(min(L + 2, nit - 1), (L + 2) % NSLOT);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int hj = 0, it = 0;
+  for (int L = 0; L < nit; ++L) {
+    const int q0 = qstart + it * BQ;
+    const uint32_t sbase = tile_base + (uint32_t)(L % NSLOT) * SLOT;
+    // ================= phase A: S, dP, softmax
+    if (m == 1) issue_ahead(L);
+    const bool need_mask = (q0 + BQ > S) || (k0 + BN > Sk) || (CAUSAL && (k0 + 32 * kg + 31 > q0 + 32 * m + off));
+    f32x16 sa, dp;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { sa[j] = 0.f; dp[j] = 0.f; }
+    {
+      const uint32_t qb = sbase + qrowb, kb2 = krowb;
+      u16x8 f[2][4];
+      auto ld = [&](int st, u16x8 (&x)[4]) {
+        const uint32_t qa = qb ^ (uint32_t)(32 * st), ka = kb2 ^ (uint32_t)(32 * st);
+        x[0] = rd128_off(qa, 0);
+        x[1] = rd128_off(ka, 0);
+        x[2] = rd128_off(qa, QT);
+        x[3] = rd128_off(ka, KIMG);
+      };
+      ld(0, f[0]);
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        if (st + 1 < KS) ld(st + 1, f[(st + 1) & 1]);
+        lds_wait_le(st + 1 < KS ? 4 : 0);
+        u16x8(&x)[4] = f[st & 1];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) pin(x[y]);
+        sa = mfma32b(x[0], x[1], sa);
+        dp = mfma32b(x[2], x[3], dp);
+      }
+    }
+    // rows of sa/dp: q = q0 + 32m + (j&3) + 8(j>>2) + 4hh ; lse / delta of row 32m + rr in lane rr / 32 + rr
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * gq + jj;
+        const int rr = 8 * gq + 4 * hh + jj;
+        const float lv = __shfl(ldc, rr, 64);
+        const float dl = __shfl(ldc, 32 + rr, 64);
+        float p;
+        if (need_mask) {
+          const int q = q0 + 32 * m + jj + 8 * gq + 4 * hh;
+          const bool dead = (key >= Sk) | (q >= S) | (CAUSAL & (key > q + off));
+          p = dead ? 0.f : __builtin_amdgcn_exp2f(sa[j] * sl - lv);
+        } else {
+          p = __builtin_amdgcn_exp2f(sa[j] * sl - lv);
+        }
+        sa[j] = p;
+        dp[j] = p * (dp[j] - dl);
+      }
+    u16x8 pb[2], sb[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pb[s2][j] = f2bf(sa[8 * s2 + j]);
+        sb[s2][j] = f2bf(dp[8 * s2 + j]);
+      }
+    if (m == 1 && L >= 1) {
+      // lag, end of A(L): iteration L+1's DMA (issued in A(L-1)) lands before the barrier that
+      // opens it for the leading half; newer ops (B(L-1)'s 4 stores, this A's 5 issues) may pend
+      vm_wait_le(4 + 1 + 4);
+    }
+    lds_wait();
+    __builtin_amdgcn_s_barrier();
+    // ================= phase B: dV^T += dO^T P, dK^T += Q^T dS
+    if (m == 0) issue_ahead(L);
+    const uint32_t ta = sbase + trA, tb = sbase + trB;
+    u16x4 tr[2][4];
+    auto issue_tr = [&](int i, u16x4 (&t)[4]) {
+      const int s2 = i / DB, db = i % DB;
+      const uint32_t a = ta ^ (uint32_t)(64 * db), bb = tb ^ (uint32_t)(64 * db);
+      t[0] = trd_off(a, s2 * 16 * ROWB + QT);
+      t[1] = trd_off(bb, s2 * 16 * ROWB + QT);
+      t[2] = trd_off(a, s2 * 16 * ROWB);
+      t[3] = trd_off(bb, s2 * 16 * ROWB);
+    };
+    issue_tr(0, tr[0]);
+#pragma unroll
+    for (int i = 0; i < 2 * DB; ++i) {
+      if (i + 1 < 2 * DB) issue_tr(i + 1, tr[(i + 1) & 1]);
+      lds_wait_le(i + 1 < 2 * DB ? 4 : 0);
+      u16x4(&t)[4] = tr[i & 1];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) pin(t[x]);
+      const int s2 = i / DB, db = i % DB;
+      dv[db] = mfma32b(u16x8{t[0][0], t[0][1], t[0][2], t[0][3], t[1][0], t[1][1], t[1][2], t[1][3]}, pb[s2], dv[db]);
+      dk[db] = mfma32b(u16x8{t[2][0], t[2][1], t[2][2], t[2][3], t[3][0], t[3][1], t[3][2], t[3][3]}, sb[s2], dk[db]);
+    }
+    {  // this iteration's dS^T (4 stores; not kept live across the loop: the register budget)
+      uint16_t* rowp = dstp(h0 + hj) + ((size_t)(q0 / BQ) * (nkb * BN) + key) * BQ + 32 * m;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+        *reinterpret_cast<u16x4*>(rowp + 8 * gq + 4 * hh) =
+            u16x4{f2bf(dp[4 * gq]), f2bf(dp[4 * gq + 1]), f2bf(dp[4 * gq + 2]), f2bf(dp[4 * gq + 3])};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (m == 0 && L >= 1) {
+      // lead, end of B(L): iteration L+1's DMA (issued in B(L-1)) lands before this barrier;
+      // newer ops (B(L-1)'s 4 stores, this B's 5 issues and 4 stores) may pend
+      vm_wait_le(4 + 1 + 4 + 4);
+    }
+    lds_wait();
+    __builtin_amdgcn_s_barrier();
+    ldc = ldn;
+    iter(L + 1, hj, it);
+  }
+  if (m == 0) __builtin_amdgcn_s_barrier();  // match the lagging half's extra barrier
+  // the unconditional look-ahead DMA of the last iterations may still be writing ring slots the
+  // reduction below reuses
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // sum the two halves' partials: m = 1 waves park theirs in LDS ([kg][value][lane], conflict-free)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem) + (size_t)kg * (2 * DB * 16) * 64 + lane;
+  if (m == 1) {
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        red[((db * 16) + j) * 64] = dk[db][j];
+        red[((DB * 16) + db * 16 + j) * 64] = dv[db][j];
+      }
+  }
+  __syncthreads();
+  if (m == 0 && key < Sk) {
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        dk[db][j] += red[((db * 16) + j) * 64];
+        dv[db][j] += red[((DB * 16) + db * 16 + j) * 64];
+      }
+    float* dkq = dKp + ((size_t)bhp * Sk + key) * D;
+    float* dvq = dVp + ((size_t)bhp * Sk + key) * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d = db * 32 + 8 * gq + 4 * hh;
+        *reinterpret_cast<f32x4*>(dkq + d) =
+            f32x4{dk[db][4 * gq] * scale, dk[db][4 * gq + 1] * scale, dk[db][4 * gq + 2] * scale,
+                  dk[db][4 * gq + 3] * scale};
+        *reinterpret_cast<f32x4*>(dvq + d) = f32x4{dv[db][4 * gq], dv[db][4 * gq + 1], dv[db][4 * gq + 2],
+                                                  dv[db][4 * gq + 3]};
+      }
+  }
+}
+
 // Deterministic dQ: dq[b,h,q,:] = sum over the key blocks that visited q (ascending kb)
 // of the partials written by attn_bwd_kernel<.., DQM=2>.  One thread per 4 floats.
 template <int D, bool CAUSAL>
@@ -1018,6 +1343,10 @@ static bool attn_bwd8_on() {
   }();
   return on;
 }
+static bool attn_bwd8_stagger() {  // MXLLM_ATTN_BWD8=2: the staggered half-tile schedule (read per call: A/B)
+  const char* e = getenv("MXLLM_ATTN_BWD8");
+  return e && e[0] == '2';
+}
 static int attn_bwd8_hpw(int B, int Hq, int Hkv, int S, int Sk, int D, int dq_mode) {
   (void)S;
   if (dq_mode != 3 || D != 128 || !attn_bwd8_on() || Hkv <= 0 || Hq % Hkv) return 1;
@@ -1109,6 +1438,14 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
       fprintf(stderr, "[attn_bwd8 prof] waves %d-%d cycles/tile: issue %.0f  S,dP %.0f  softmax %.0f  dV,dK %.0f  barrier %.0f\n",
               4 * half, 4 * half + 3, sum[half][0] / tiles[half], sum[half][1] / tiles[half], sum[half][2] / tiles[half],
               sum[half][3] / tiles[half], sum[half][4] / tiles[half]);
+  } else if (dq_mode == 3 && D == 128 && bwd8 && attn_bwd8_stagger()) {
+    uint16_t* dst = reinterpret_cast<uint16_t*>(work);
+    if (causal)
+      attn_bwd8s_kernel<true><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
+                                                         off, sl, scale, S_pad, hpw);
+    else
+      attn_bwd8s_kernel<false><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
+                                                          off, sl, scale, S_pad, hpw);
   } else if (dq_mode == 3 && D == 128 && bwd8) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     if (causal)

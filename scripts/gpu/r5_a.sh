@@ -16,6 +16,16 @@ done
 for RG in 3 4; do
   MXLLM_ATTN_FWD_RING=$RG timeout -k 10 300 $T tests/test_kernels_gpu.py -k "attention" tests/test_strict_parity_gpu.py -k "attention" > $O/attn_ring$RG.log 2>&1 || echo "ring $RG parity FAILED"
 done
+# staggered attention backward (MXLLM_ATTN_BWD8=2): parity first, then timing beside the default
+MXLLM_ATTN_BWD8=2 timeout -k 10 300 $T tests/test_kernels_gpu.py -k "attention" tests/test_strict_parity_gpu.py -k "attention" > $O/attn_bwd_stag.log 2>&1 && STAG_OK=1 || { echo "bwd stagger parity FAILED"; STAG_OK=0; }
+if [ "$STAG_OK" = 1 ]; then
+  for i in 1 2; do
+    for BW in 1 2; do
+      MXLLM_ATTN_BWD8=$BW timeout -k 10 120 python -u bench/attn_bench.py 2 64 8 2048 128 lite > $O/bwd_b2_bw${BW}_$i.txt 2>&1 || { echo "bwd bench failed"; exit 1; }
+      MXLLM_ATTN_BWD8=$BW timeout -k 10 120 python -u bench/attn_bench.py 16 64 8 2048 128 lite > $O/bwd_b16_bw${BW}_$i.txt 2>&1 || { echo "bwd bench16 failed"; exit 1; }
+    done
+  done
+fi
 for i in 1 2; do
   for RG in 0 3 4; do
     MXLLM_ATTN_FWD_RING=$RG timeout -k 10 120 python -u bench/attn_bench.py 2 64 8 2048 128 lite > $O/ab2_r${RG}_$i.txt 2>&1 || { echo "attn bench ring $RG failed"; exit 1; }
