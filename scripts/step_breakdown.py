@@ -8,8 +8,21 @@ import csv
 import sys
 
 
+def _rows(path: str) -> list[dict]:
+    """Kernel rows from a rocprofv3 CSV kernel trace, or from its SQLite output (``*.db``, the
+    default ``rocpd`` format): Kernel_Name / Start_Timestamp / End_Timestamp."""
+    if not path.endswith(".db"):
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+
+    con = sqlite3.connect(path)
+    q = ("select s.display_name, d.start, d.end from rocpd_kernel_dispatch d "
+         "join rocpd_info_kernel_symbol s on d.kernel_id = s.id")
+    return [{"Kernel_Name": n, "Start_Timestamp": a, "End_Timestamp": b} for n, a, b in con.execute(q)]
+
+
 def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
+    rows = _rows(sys.argv[1])
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # one grad-norm kernel per optimizer step (AdamW may be issued as several chunk launches)
