@@ -68,7 +68,12 @@ __device__ __forceinline__ u16x4 tr_read(const char* p) {
 // (profiles/r4ah/README.md): the DMA round trip is longer than one tile of MFMAs.  With 8 waves per
 // workgroup (one workgroup per CU, 256 query rows sharing every tile) a 3- or 4-deep ring fits the
 // CU's 160 KB of LDS (96 / 128 KB).
-template <int D, bool CAUSAL, int NW, bool PROF = false, int R = 2>
+// SR (split ring, 4 waves, D = 128): K in a 3-slot ring and V in a 2-slot ring = 80 KB, so two
+// workgroups still share a CU, and TWO barriers per tile: M (after the softmax, before PV: this
+// tile's V landed) and E (after PV: every wave is done with the V slot the next tile restages).
+// Tile kt issues K(kt + 2) and V(kt + 1) during its QK^T steps, so a K tile has two tiles of MFMAs
+// to land and a V tile one and a half, where the symmetric 2-slot ring gives both one.
+template <int D, bool CAUSAL, int NW, bool PROF = false, int R = 2, bool SR = false>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                 uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
@@ -89,7 +94,14 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   constexpr int LPT = BN * CH / (64 * NW);
   static_assert(LPT >= 1 && BN * CH % (64 * NW) == 0, "K/V tile must split evenly over the waves");
   static_assert(R >= 2 && R <= 4, "ring depth 2..4");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * R * TILE];  // (XOR addressing: 256-B aligned)
+  static_assert(!SR || (NW == 4 && R == 2 && D == 128), "split ring: the 4-wave D = 128 kernel");
+  // (XOR addressing: 256-B aligned)
+  __shared__ __attribute__((aligned(1024))) char smem[SR ? 5 * TILE : 2 * R * TILE];
+  // byte offsets of K ring slot c (from smem) and of V ring slot c (from smem + VBASE): the LDS read
+  // bases carry the region start, so every slot offset stays a ds_read immediate (< 64 KiB)
+  constexpr int VBASE = SR ? 3 * TILE : TILE;
+  constexpr auto KOF = [](int c) constexpr { return SR ? c * TILE : c * 2 * TILE; };
+  constexpr auto VOF = [](int c) constexpr { return SR ? c * TILE : c * 2 * TILE; };
 
   const int nqb = (S + BM - 1) / BM;
   const int BH = B * Hq;
@@ -147,6 +159,21 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kb + seg * 1024), 16, off, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vb + seg * 1024), 16, off, 0, 0, 0);
   };
+  // split ring: piece i of K tile kt into K slot ks / of V tile kt into V slot vs (SR only: slots TILE apart).
+  // The source offset goes through a local: `voff[i] + ...` written straight into the builtin's argument
+  // list makes hipcc's host pass drop the kernel's launch stub (undefined __device_stub__ at load)
+  auto glds_k = [&](int kt, int ks, int i) {
+    char* kb = smem + ks * TILE;
+    const int seg = w * LPT + i;
+    const int off = voff[i] + kt * TILE;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kb + seg * 1024), 16, off, 0, 0, 0);
+  };
+  auto glds_v = [&](int kt, int vs, int i) {
+    char* vb = smem + VBASE + vs * TILE;
+    const int seg = w * LPT + i;
+    const int off = voff[i] + kt * TILE;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vb + seg * 1024), 16, off, 0, 0, 0);
+  };
   auto glds = [&](int kt, int buf) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) glds_piece(kt, buf, i);
@@ -175,14 +202,25 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   for (int db = 0; db < DB; ++db) {
     const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
     const int rA = 4 * hh + tq, rB = 8 + 4 * hh + tq;
-    va_base[db][0] = lds0 + TILE + rA * ROWB + 16 * (chunk ^ swz<CH>(rA)) + 8 * (tp & 1);
-    va_base[db][1] = lds0 + TILE + rB * ROWB + 16 * (chunk ^ swz<CH>(rB)) + 8 * (tp & 1);
+    va_base[db][0] = lds0 + VBASE + rA * ROWB + 16 * (chunk ^ swz<CH>(rA)) + 8 * (tp & 1);
+    va_base[db][1] = lds0 + VBASE + rB * ROWB + 16 * (chunk ^ swz<CH>(rB)) + 8 * (tp & 1);
   }
 
   const uint32_t kq_base = lds0 + r * ROWB + 16 * (hh ^ swz<CH>(r));  // K row r, k step 0 (D = 128 path)
+  if constexpr (SR) {  // K(0), V(0), K(1)
 #pragma unroll
-  for (int t = 0; t < R - 1; ++t)
-    if (t < ntiles) glds(t, t);  // the ring's first R - 1 tiles
+    for (int i = 0; i < LPT; ++i) {
+      if (ntiles > 0) {
+        glds_k(0, 0, i);
+        glds_v(0, 0, i);
+      }
+      if (ntiles > 1) glds_k(1, 1, i);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < R - 1; ++t)
+      if (t < ntiles) glds(t, t);  // the ring's first R - 1 tiles
+  }
   // Retire the prologue's Q loads and tile-0 DMA with a wait the compiler's
   // waitcnt pass can see (otherwise it treats them as possibly pending at the
   // loop header and drains the in-loop prefetch under the QK MFMAs).
@@ -190,19 +228,34 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   __syncthreads();
   const int wq_hi = q0 + 32 * w + 31;
 
-  // One 64-key tile out of ring buffer CUR (compile-time).
+  // One 64-key tile out of ring buffer CUR (compile-time; SR: K slot CUR % 3, V slot CUR % 2).
   if constexpr (PROF) t_loop = __builtin_amdgcn_s_memtime();
   auto tile = [&](auto cur_c, int kt) {
     constexpr int CUR = decltype(cur_c)::value;
     if constexpr (PROF) tp0 = __builtin_amdgcn_s_memtime();
+    constexpr int CK = SR ? CUR % 3 : CUR, CV = SR ? CUR % 2 : CUR;  // K / V slots read by this tile
     constexpr int NXT = (CUR + R - 1) % R;  // ring slot of tile kt + R - 1 (the slot tile kt - 1 used)
-    const int kpf = kt + R - 1;             // the tile this one prefetches
+    constexpr int NK = (CUR + 2) % 3, NV = (CUR + 1) % 2;  // SR: slots of K(kt + 2) / V(kt + 1)
+    const int kpf = kt + R - 1;             // the tile this one prefetches (SR: V(kt + 1))
     const bool more = kpf < ntiles;
-    const char* kb = smem + CUR * 2 * TILE;
+    const bool morek = SR && kt + 2 < ntiles;  // SR: K(kt + 2)
+    const char* kb = smem + KOF(CK);
     const bool active = !CAUSAL || (kt * BN <= wq_hi + causal_off);
-    if (more && (!spread || !active)) glds(kpf, NXT);  // prefetch R - 1 tiles ahead
+    // DMA piece i of this tile's prefetch: SR K(kt + 2) then V(kt + 1), else K and V of tile kpf
+    auto pf_piece = [&](int i) {
+      if constexpr (SR) {
+        if (morek) glds_k(kt + 2, NK, i);
+        glds_v(kt + 1, NV, i);
+      } else {
+        glds_piece(kpf, NXT, i);
+      }
+    };
+    if (more && (!spread || !active)) {  // prefetch R - 1 tiles ahead (SR: 2 for K, 1 for V)
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) pf_piece(i);
+    }
+    f32x16 sacc[2];
     if (active) {
-      f32x16 sacc[2];
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -214,8 +267,8 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
         u16x8 kf2[2][2];
         auto ld = [&](int st, u16x8 (&x)[2]) {
           const uint32_t a = kq_base ^ (uint32_t)(32 * st);
-          x[0] = rd128_off(a, CUR * 2 * TILE);
-          x[1] = rd128_off(a, CUR * 2 * TILE + 32 * ROWB);
+          x[0] = rd128_off(a, KOF(CK));
+          x[1] = rd128_off(a, KOF(CK) + 32 * ROWB);
         };
         ld(0, kf2[0]);
 #pragma unroll
@@ -227,7 +280,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           pin(x[1]);
           sacc[0] = mfma32(x[0], qf[st], sacc[0]);
           sacc[1] = mfma32(x[1], qf[st], sacc[1]);
-          if (spread && more && (st % (KS / LPT)) == 0) glds_piece(kpf, NXT, st / (KS / LPT));
+          if (spread && more && (st % (KS / LPT)) == 0) pf_piece(st / (KS / LPT));
         }
       } else {
 #pragma unroll
@@ -237,7 +290,7 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           for (int s = 0; s < KS; ++s) {
             const u16x8 a = *reinterpret_cast<const u16x8*>(kb + krow * ROWB + 16 * ((2 * s + hh) ^ swz<CH>(krow)));
             sacc[n] = mfma32(a, qf[s], sacc[n]);
-            if (spread && more && n == 0 && (s % (KS / LPT)) == 0) glds_piece(kpf, NXT, s / (KS / LPT));
+            if (spread && more && n == 0 && (s % (KS / LPT)) == 0) pf_piece(s / (KS / LPT));
           }
         }
       }
@@ -296,6 +349,21 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
       l_i += (lp[0] + lp[1]) + (lp[2] + lp[3]);
       if constexpr (PROF) asm volatile("" ::"v"(l_i));
       mark(1);
+    } else {
+      mark(5);
+    }
+    if constexpr (SR) {
+      // M: V(kt) -- issued by the previous tile, before this tile's prefetch -- landed for this wave
+      // (vector-memory ops retire in issue order: this tile's pieces may stay in flight), then for
+      // every wave.  K(kt + 1), issued with it, is covered too.  Raw barrier: no fence drain.
+      const int younger = (more ? LPT : 0) + (morek ? LPT : 0);
+      if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (younger == LPT) g8_vmcnt<LPT>();
+      else g8_vmcnt<2 * LPT>();
+      __builtin_amdgcn_s_barrier();
+      mark(3);
+    }
+    if (active) {
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -308,8 +376,8 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           u16x4 fv[DB][2];
 #pragma unroll
           for (int db = 0; db < DB; ++db) {
-            fv[db][0] = trd_off(va_base[db][0], CUR * 2 * TILE + (32 * n + 16 * s2) * ROWB);
-            fv[db][1] = trd_off(va_base[db][1], CUR * 2 * TILE + (32 * n + 16 * s2) * ROWB);
+            fv[db][0] = trd_off(va_base[db][0], VOF(CV) + (32 * n + 16 * s2) * ROWB);
+            fv[db][1] = trd_off(va_base[db][1], VOF(CV) + (32 * n + 16 * s2) * ROWB);
           }
 #pragma unroll
           for (int db = 0; db < DB; ++db) {
@@ -322,10 +390,12 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
           }
         }
       mark(2);
-    } else {
-      mark(5);
     }
-    if constexpr (R == 2) {
+    if constexpr (SR) {
+      // E: every wave is done reading V slot CV (restaged by the next tile) and K slot CK
+      lds_wait();
+      __builtin_amdgcn_s_barrier();
+    } else if constexpr (R == 2) {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA for tile kt+1 landed
       __syncthreads();                     // ... and every other wave's; buffer CUR free again
     } else {
@@ -342,9 +412,15 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
     mark(3);
     if constexpr (PROF) ph[4] += 1;
   };
-  for (int kt = 0; kt < ntiles; kt += R) {
+  for (int kt = 0; kt < ntiles; kt += (SR ? 6 : R)) {
     tile(std::integral_constant<int, 0>{}, kt);
     if (kt + 1 < ntiles) tile(std::integral_constant<int, 1>{}, kt + 1);
+    if constexpr (SR) {  // 6 = lcm of the K and V ring depths: static slots
+      if (kt + 2 < ntiles) tile(std::integral_constant<int, 2>{}, kt + 2);
+      if (kt + 3 < ntiles) tile(std::integral_constant<int, 3>{}, kt + 3);
+      if (kt + 4 < ntiles) tile(std::integral_constant<int, 4>{}, kt + 4);
+      if (kt + 5 < ntiles) tile(std::integral_constant<int, 5>{}, kt + 5);
+    }
     if constexpr (R > 2) {
       if (kt + 2 < ntiles) tile(std::integral_constant<int, 2 % R>{}, kt + 2);
     }
@@ -767,8 +843,11 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     const char* e = getenv("MXLLM_ATTN_FWD_WAVES");
     return (e && e[0] == '8') ? 8 : 4;
   }();
-  static const int ring = [] {  // MXLLM_ATTN_FWD_RING=3|4: 8 waves with a 3- / 4-deep K/V ring (D = 128)
+  // MXLLM_ATTN_FWD_RING=3|4: 8 waves with a 3- / 4-deep K/V ring; =k3: 4 waves, split ring (K 3, V 2
+  // slots, two barriers per tile) -- D = 128
+  static const int ring = [] {
     const char* e = getenv("MXLLM_ATTN_FWD_RING");
+    if (e && e[0] == 'k' && e[1] == '3') return -3;
     const int r = e && *e ? atoi(e) : 0;
     return (r == 3 || r == 4) ? r : 0;
   }();
@@ -789,8 +868,12 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     uint32_t* pbuf = nullptr;
     if (hipMalloc(&pbuf, n * 4) != hipSuccess) return -1;
     (void)hipMemsetAsync(pbuf, 0, n * 4, stream);
-    attn_fwd_kernel<128, true, 4, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo,
-                                                                  fflags, pbuf);
+    if (ring == -3)
+      attn_fwd_kernel<128, true, 4, true, 2, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off,
+                                                                            sl, ldo, fflags, pbuf);
+    else
+      attn_fwd_kernel<128, true, 4, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo,
+                                                                    fflags, pbuf);
     std::vector<uint32_t> h(n);
     (void)hipMemcpyAsync(h.data(), pbuf, n * 4, hipMemcpyDeviceToHost, stream);
     (void)hipStreamSynchronize(stream);
@@ -808,7 +891,17 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
 #define FWDR(C, RR)                                                                                    \
   attn_fwd_kernel<128, C, 8, false, RR><<<((S + 255) / 256) * B * Hq, 512, 0, stream>>>(                 \
       q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
-  if (D == 128 && ring) {
+  if (D == 128 && ring == -3) {
+    const unsigned grid = ((S + 127) / 128) * B * Hq;
+    if (causal)
+      attn_fwd_kernel<128, true, 4, false, 2, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off,
+                                                                             sl, ldo, fflags);
+    else
+      attn_fwd_kernel<128, false, 4, false, 2, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk,
+                                                                              off, sl, ldo, fflags);
+    return (int)hipGetLastError();
+  }
+  if (D == 128 && ring > 0) {
     if (ring == 3) { if (causal) FWDR(true, 3); else FWDR(false, 3); }
     else { if (causal) FWDR(true, 4); else FWDR(false, 4); }
     return (int)hipGetLastError();
