@@ -177,15 +177,17 @@ def test_attention_every_kv_tile_is_visited(gpu, S, tile):
         _assert_rows(f"tile-coverage S={S} {name}", a.contiguous(), b.contiguous(), c.contiguous(), cf.contiguous(),
                      eps_q=1.0 if name in ("dQ", "dK") else 0.99)
     # the dominant key's dV row really is the head's largest (the test has teeth), and ours matches
-    # the fp32 reference on exactly those rows to 1 % (a skipped or doubled tile: O(1))
+    # the fp32 reference on exactly those rows to 1 % (a skipped or doubled tile: O(1)).  Not dK:
+    # with P ~ 1 on the dominant key, its dS = P (dP - delta) is a cancellation of two ~10-sized
+    # terms, so that row's dK is tiny and ill-conditioned (fp32 summation order alone moved it by
+    # 34-94 % relative, gpurun_out r5f) -- the per-row absolute bound above covers it
     dv_ref = fp[3][0]  # [H, S, D]
     for h in range(H):
         key = h * tile + (7 * h + 5) % tile
         assert int(dv_ref[h].norm(dim=-1).argmax()) == key
-        for name, ours_t, ref_t in (("dK", mine[2][0, h, key], fk[0, h, key]), ("dV", mine[3][0, h, key],
-                                                                                 dv_ref[h, key])):
-            rel = float((ours_t.float() - ref_t.float()).norm() / ref_t.float().norm().clamp_min(1e-12))
-            assert rel < 1e-2, (f"tile-coverage S={S} head {h} dominant key {key} {name}: rel err {rel:.3g}")
+        ours_t, ref_t = mine[3][0, h, key].float(), dv_ref[h, key].float()
+        rel = float((ours_t - ref_t).norm() / ref_t.norm().clamp_min(1e-12))
+        assert rel < 1e-2, f"tile-coverage S={S} head {h} dominant key {key} dV: rel err {rel:.3g}"
 
 
 def _mat(rows, cols, dev, seed):
