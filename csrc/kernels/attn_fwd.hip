@@ -463,6 +463,292 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// D = 128 forward with a barrier-enforced ping-pong of two wave groups (opt-in MXLLM_ATTN_FWD=pp).
+// Per 64-key tile a wave's work is a serial chain -- QK^T MFMAs, the softmax VALU (32 exp2 per
+// lane: ~830 cycles, as much as the tile's 1,024 MFMA cycles), the PV MFMAs -- and the two waves
+// that share a SIMD in the 4-wave kernel come from different workgroups, so nothing keeps one's
+// softmax under the other's MFMAs (phase profile: ~3,700 cycles per tile against a 2,048-cycle
+// MFMA floor for the pair, profiles/r5f).  Here one 8-wave workgroup (256 query rows, 32 per wave)
+// owns the CU; waves w and w + 4 share a SIMD, and group B (waves 4-7) runs one phase behind
+// group A.  Phases alternate, separated by workgroup barriers:
+//   MFMA phase of tile t:  O += V(t-1) P(t-1)  then  S(t) = K(t) Q^T   (32 MFMAs, setprio 1)
+//   VALU phase of tile t:  mask, row max, deferred rescale, P(t) = exp2(...), l, bf16 pack of P(t)
+// so in every phase one wave of each SIMD issues MFMAs while the other runs its softmax.  K/V
+// tiles sit in a 4-slot ring (128 KB); every wave issues its pieces of tile t + 2 during its MFMA
+// phase of tile t, into the slot tile t - 2 used (last read by group B two phases earlier), and
+// before the barrier that opens group A's QK^T of tile t' every wave has its pieces of t' landed
+// (counted vmcnt: only tile t' + 1's may still fly).  Same arithmetic as attn_fwd_kernel.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(512, 1)
+attn_fwd_pp_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                   uint16_t* __restrict__ O, float* __restrict__ LSE, int B, int Hq, int Hkv, int S, int Sk,
+                   int causal_off, float sl, int ldo) {
+  constexpr int D = 128, NW = 8, BM = 32 * NW, BN = 64, CH = D / 8, ROWB = D * 2, KS = D / 16, DB = D / 32;
+  constexpr int TILE = BN * ROWB;           // 16 KiB
+  constexpr int LPT = BN * CH / (64 * NW);  // DMA pieces per wave per K (and per V) tile
+  constexpr int R = 4;                      // ring slots
+  static_assert(LPT == 2, "8 waves x 2 pieces = one 16 KiB tile");
+  __shared__ __attribute__((aligned(1024))) char smem[R * 2 * TILE];
+
+  const int nqb = (S + BM - 1) / BM;
+  const int BH = B * Hq;
+  const int bid = xcd_balance(blockIdx.x, gridDim.x, BH, Hq / Hkv);
+  const int qb = nqb - 1 - bid / BH;
+  const int bh = bid % BH;
+  const int b = bh / Hq, h = bh % Hq;
+  const int hk = h / (Hq / Hkv);
+  const uint16_t* Qp = Q + ((size_t)(b * Hq + h) * S) * D;
+  const uint16_t* Kp = K + ((size_t)(b * Hkv + hk) * Sk) * D;
+  const uint16_t* Vp = V + ((size_t)(b * Hkv + hk) * Sk) * D;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2;  // 0: group A, 1: group B (one phase behind)
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = qb * BM;
+  const int qrow = q0 + 32 * w + r;
+  const int qld = min(qrow, S - 1);
+
+  u16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const u16x8*>(Qp + (size_t)qld * D + 16 * s + 8 * hh);
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM + causal_off);
+  const int ntiles = kend > 0 ? (kend + BN - 1) / BN : 0;
+
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)Kp, 0, Sk * ROWB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)Vp, 0, Sk * ROWB, 0x00020000);
+  int voff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int seg = w * LPT + i;
+    const int byte = seg * 1024 + lane * 16;
+    const int row = byte / ROWB, slot = (byte % ROWB) / 16;
+    voff[i] = row * ROWB + 16 * (slot ^ swz<CH>(row));
+  }
+  // piece i (K and V) of tile kt into ring slot kt % R (source offsets through locals: see glds_k)
+  auto dma_piece = [&](int kt, int i) {
+    char* kb = smem + (kt & (R - 1)) * 2 * TILE;
+    char* vb = kb + TILE;
+    const int seg = w * LPT + i;
+    const int off = voff[i] + kt * TILE;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (lptr_t)(kb + seg * 1024), 16, off, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lptr_t)(vb + seg * 1024), 16, off, 0, 0, 0);
+  };
+
+  f32x16 o[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[d][j] = 0.f;
+  float m_i = -1e30f, l_i = 0.f;
+
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t va_base[DB][2];
+#pragma unroll
+  for (int db = 0; db < DB; ++db) {
+    const int chunk = (db * 32 + 16 * (g & 1) + 4 * tp) >> 3;
+    const int rA = 4 * hh + tq, rB = 8 + 4 * hh + tq;
+    va_base[db][0] = lds0 + TILE + rA * ROWB + 16 * (chunk ^ swz<CH>(rA)) + 8 * (tp & 1);
+    va_base[db][1] = lds0 + TILE + rB * ROWB + 16 * (chunk ^ swz<CH>(rB)) + 8 * (tp & 1);
+  }
+  const uint32_t kq_base = lds0 + r * ROWB + 16 * (hh ^ swz<CH>(r));
+  const int wq_hi = q0 + 32 * w + 31;
+  auto active = [&](int kt) { return !CAUSAL || (kt * BN <= wq_hi + causal_off); };
+
+  if (ntiles > 0) {
+    dma_piece(0, 0);
+    dma_piece(0, 1);
+  }
+  if (ntiles > 1) {
+    dma_piece(1, 0);
+    dma_piece(1, 1);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): Q, tiles 0 and 1 (visible to hipcc's waitcnt pass)
+  __syncthreads();
+
+  f32x16 sacc[2];
+  u16x8 pb[2][2];  // P(t) in bf16: the B operand of the PV MFMAs, [32-key block n][16-key step s2]
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sacc[n][j] = 0.f;
+
+  // MFMA phase of tile t: PV(t - 1), prefetch of tile t + 2, QK^T(t)
+  auto mfma_phase = [&](int t) {
+    const bool pv = t >= 1 && active(t - 1);
+    const bool qk = t < ntiles && active(t);
+    const bool pf = t + 2 < ntiles;
+    __builtin_amdgcn_s_setprio(1);
+    if (pv) {
+      const uint32_t vo = (uint32_t)(((t - 1) & (R - 1)) * 2 * TILE);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          u16x4 fv[DB][2];
+#pragma unroll
+          for (int db = 0; db < DB; ++db) {
+            fv[db][0] = trd_off(va_base[db][0] + vo, (32 * n + 16 * s2) * ROWB);
+            fv[db][1] = trd_off(va_base[db][1] + vo, (32 * n + 16 * s2) * ROWB);
+          }
+#pragma unroll
+          for (int db = 0; db < DB; ++db) {
+            lds_wait_le(2 * (DB - 1 - db));
+            pin(fv[db][0]);
+            pin(fv[db][1]);
+            const u16x4 va = fv[db][0], vc = fv[db][1];
+            const u16x8 a = u16x8{va[0], va[1], va[2], va[3], vc[0], vc[1], vc[2], vc[3]};
+            o[db] = mfma32(a, pb[n][s2], o[db]);
+          }
+        }
+    }
+    if (pf && !qk) {
+      dma_piece(t + 2, 0);
+      dma_piece(t + 2, 1);
+    }
+    if (qk) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sacc[n][j] = 0.f;
+      const uint32_t kb = kq_base + (uint32_t)((t & (R - 1)) * 2 * TILE);
+      u16x8 kf2[2][2];
+      auto ld = [&](int st, u16x8 (&x)[2]) {
+        const uint32_t a = kb ^ (uint32_t)(32 * st);  // slot offsets are multiples of 32 KiB: bits 5-7 free
+        x[0] = rd128_off(a, 0);
+        x[1] = rd128_off(a, 32 * ROWB);
+      };
+      ld(0, kf2[0]);
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        if (st + 1 < KS) ld(st + 1, kf2[(st + 1) & 1]);
+        lds_wait_le(st + 1 < KS ? 2 : 0);
+        u16x8(&x)[2] = kf2[st & 1];
+        pin(x[0]);
+        pin(x[1]);
+        sacc[0] = mfma32(x[0], qf[st], sacc[0]);
+        sacc[1] = mfma32(x[1], qf[st], sacc[1]);
+        if (pf && st < LPT) dma_piece(t + 2, st);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // VALU phase of tile t (active): the softmax of S(t) -> P(t) in bf16, l, deferred O rescale
+  auto valu_phase = [&](int t) {
+    const int kt = t;
+    const bool need_mask = (kt * BN + BN > Sk) || (CAUSAL && (kt * BN + BN - 1 > q0 + 32 * w + causal_off));
+    float mp[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    if (need_mask) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int key = kt * BN + n * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          const bool dead = (key >= Sk) | (CAUSAL & (key > qrow + causal_off));
+          const float x = dead ? -INFINITY : sacc[n][j];
+          sacc[n][j] = x;
+          mp[j & 3] = fmaxf(mp[j & 3], x);
+        }
+    } else {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) mp[j & 3] = fmaxf(mp[j & 3], sacc[n][j]);
+    }
+    float mx = fmaxf(fmaxf(mp[0], mp[1]), fmaxf(mp[2], mp[3]));
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    constexpr float kThr = 8.f;
+    const float mt = mx * sl;
+    if (__any(mt > m_i + kThr)) {
+      const float mnew = fmaxf(m_i, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m_i - mnew);
+      l_i *= alpha;
+      m_i = mnew;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) o[d] *= alpha;
+    }
+    const float nm = -m_i;
+    float lp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][j], sl, nm));
+        sacc[n][j] = p;
+        lp[j & 3] += p;
+      }
+    l_i += (lp[0] + lp[1]) + (lp[2] + lp[3]);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[n][s2][j] = f2bf(sacc[n][8 * s2 + j]);
+  };
+
+  // phases 2t and 2t + 1: group A runs MFMA(t) then VALU(t), group B VALU(t - 1) then MFMA(t);
+  // every phase ends at a workgroup barrier (the same count for every wave: 2 ntiles + 2)
+  auto phase_end = [&](bool opens_qk, int tn) {
+    // before group A's QK^T of tile tn: every wave's pieces of tn have landed (this wave issued at
+    // most tile tn + 1's 2 LPT pieces after them; tiles 0 / 1: the prologue's wait)
+    if (opens_qk && tn >= 2 && tn < ntiles) {
+      if (tn + 1 < ntiles) g8_vmcnt<2 * LPT>();
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_wait();                    // this phase's LDS reads retired: their slot may be restaged next
+    __builtin_amdgcn_s_barrier();  // raw: __syncthreads()'s fence would drain the in-flight DMA
+  };
+  // One loop per group (s_barrier matches arrivals, not code addresses): in a shared loop body the
+  // join after every phase keeps S of one group and P of the other live at once (256 VGPRs + spills
+  // of the Q fragments; 186 and none this way)
+  if (ntiles > 0) {
+    if (grp == 0) {
+      for (int t = 0; t <= ntiles; ++t) {
+        mfma_phase(t);
+        phase_end(false, 0);
+        if (t < ntiles && active(t)) valu_phase(t);
+        phase_end(true, t + 1);
+      }
+    } else {
+      for (int t = 0; t <= ntiles; ++t) {
+        if (t >= 1 && active(t - 1)) valu_phase(t - 1);
+        phase_end(false, 0);
+        mfma_phase(t);
+        phase_end(true, t + 1);
+      }
+    }
+  }
+
+  float l_tot;
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_i), __float_as_uint(l_i), false, false);
+    l_tot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qrow < S) {
+    uint16_t* op = O + ((size_t)b * S + qrow) * (size_t)ldo + (size_t)h * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d = db * 32 + 8 * gq + 4 * hh;
+        u16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(o[db][4 * gq + j] * inv);
+        *reinterpret_cast<u16x4*>(op + d) = v4;
+      }
+    if (hh == 0) LSE[(size_t)(b * Hq + h) * S + qrow] = m_i + __log2f(l_tot);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // D = 128 forward, software-pipelined (opt-in: MXLLM_ATTN_FWD=p; measured SLOWER than the kernel
 // above -- 0.300 vs 0.265 ms at B2 S2048 Hq64 Hkv8, see profiles/r1d_experiments.md -- and kept for
 // the record and further work).  One wave per SIMD owning the whole register file and 64 query rows (two 32-row blocks
@@ -831,8 +1117,18 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   const int off = Sk - S;
   static const bool pipe = [] {  // MXLLM_ATTN_FWD=p: the software-pipelined 64-row-per-wave kernel (A/B)
     const char* e = getenv("MXLLM_ATTN_FWD");
-    return e && e[0] == 'p';
+    return e && e[0] == 'p' && e[1] != 'p';
   }();
+  static const bool pingpong = [] {  // MXLLM_ATTN_FWD=pp: the 8-wave two-group ping-pong kernel
+    const char* e = getenv("MXLLM_ATTN_FWD");
+    return e && e[0] == 'p' && e[1] == 'p';
+  }();
+  if (D == 128 && pingpong) {
+    const unsigned grid = ((S + 255) / 256) * B * Hq;
+    if (causal) attn_fwd_pp_kernel<true><<<grid, 512, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
+    else attn_fwd_pp_kernel<false><<<grid, 512, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
+    return (int)hipGetLastError();
+  }
   if (D == 128 && pipe) {
     const unsigned grid = ((S + 255) / 256) * B * Hq;
     if (causal) attn_fwd_p_kernel<true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
