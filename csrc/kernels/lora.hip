@@ -383,6 +383,7 @@ struct XtgArgs {
   float alpha;
   int accumulate;
   int fused_red;  // 1: last-arriving workgroup reduces; 0: lora_xtg_reduce_kernel does
+  int narrow3;    // 1: narrow-G problems stream through three stages per wave (0: two, A/B)
 };
 
 // 16-B chunk swizzle of a 128-B LDS row: conflict-free ds_read_b64_tr_b16 of
@@ -500,11 +501,75 @@ __global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float
       }
     }
   };
-  if (b0 < b1) issue(b0, 0);
-  if (b0 + 1 < b1) issue(b0 + 1, 1);
-  for (int b = b0; b < b1; b += 2) {
-    block(std::integral_constant<int, 0>{}, b);
-    if (b + 1 < b1) block(std::integral_constant<int, 1>{}, b + 1);
+  if (wide || !a.narrow3) {
+    if (b0 < b1) issue(b0, 0);
+    if (b0 + 1 < b1) issue(b0 + 1, 1);
+    for (int b = b0; b < b1; b += 2) {
+      block(std::integral_constant<int, 0>{}, b);
+      if (b + 1 < b1) block(std::integral_constant<int, 1>{}, b + 1);
+    }
+  } else {
+    // narrow G (one 16-column block, 2 KiB per 64-row block): a stage is X 8 KiB + G 2 KiB, so the
+    // wave's 32 KiB hold THREE stages -- two blocks in flight behind the one being read instead of
+    // one (~80 KiB of DMA in flight per CU, the HBM-latency cover of MI355X_MICROARCH §Indexed
+    // rows; with two stages these streams ran at ~3.6 TB/s, profiles/r4_final6)
+    constexpr int STN = XB + 2048;
+    auto issue3 = [&](int b, int st) {
+      const int64_t t0 = (int64_t)b * 64;
+      char* xs = wreg + st * STN;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        __builtin_amdgcn_global_load_lds((lgptr_t)(xsrc + (t0 + 8 * q) * P.ldx), (llptr_t)(xs + q * 1024), 16, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_global_load_lds((lgptr_t)(gsrc + (t0 + 32 * q) * P.ldg), (llptr_t)(xs + XB + q * 1024), 16,
+                                         0, 0);
+    };
+    auto block3 = [&](auto SC, int b) {
+      constexpr int st = decltype(SC)::value;
+      // this block's 10 DMA instructions landed; the (up to two) later blocks' may still fly
+      if (b + 2 < b1) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (b + 1 < b1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      u16x4 xr[2][2][4], gr[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[ks][h][i] = trd_off(xb[i], st * STN + (32 * ks + 16 * h) * 128);
+          gr[ks][h] = trd_off(gnb, st * STN + (32 * ks + 16 * h) * 32);
+        }
+      lds_wait();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pin(xr[ks][h][i]);
+          pin(gr[ks][h]);
+        }
+      if (b + 3 < b1) issue3(b + 3, st);  // refill this stage (its reads have retired)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const u16x8 bf = u16x8{gr[ks][0][0], gr[ks][0][1], gr[ks][0][2], gr[ks][0][3],
+                               gr[ks][1][0], gr[ks][1][1], gr[ks][1][2], gr[ks][1][3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const u16x8 af = u16x8{xr[ks][0][i][0], xr[ks][0][i][1], xr[ks][0][i][2], xr[ks][0][i][3],
+                                 xr[ks][1][i][0], xr[ks][1][i][1], xr[ks][1][i][2], xr[ks][1][i][3]};
+          acc[i][0] = lmfma(af, bf, acc[i][0]);
+        }
+      }
+    };
+    if (b0 < b1) issue3(b0, 0);
+    if (b0 + 1 < b1) issue3(b0 + 1, 1);
+    if (b0 + 2 < b1) issue3(b0 + 2, 2);
+    for (int b = b0; b < b1; b += 3) {
+      block3(std::integral_constant<int, 0>{}, b);
+      if (b + 1 < b1) block3(std::integral_constant<int, 1>{}, b + 1);
+      if (b + 2 < b1) block3(std::integral_constant<int, 2>{}, b + 2);
+    }
   }
   // 4 waves -> one 64 x 16 JB tile in LDS (each wave's own region; its DMA has drained)
   float* rw = reinterpret_cast<float*>(wreg);
@@ -996,6 +1061,7 @@ extern "C" int mx_lora_xtg(const int64_t* desc, int np, int T, float alpha, int 
   a.np = np, a.T = T, a.S = lora_splits(ntiles, T / 64, 8), a.ntiles = ntiles, a.alpha = alpha;
   a.accumulate = accumulate;
   a.fused_red = lora_env("MXLLM_LORA_FUSED_RED", 0);
+  a.narrow3 = lora_env("MXLLM_LORA_XTG_STAGES", 3) == 3;
   lora_xtg_kernel<<<dim3(ntiles, a.S), 256, 0, stream>>>(a, ws);
   if (a.S > 1 && !a.fused_red) lora_xtg_reduce_kernel<<<ntiles, 256, 0, stream>>>(a, ws);
   return (int)hipGetLastError();
