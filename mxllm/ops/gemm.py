@@ -76,6 +76,26 @@ def tail_split(M: int, N: int, K: int) -> int:
     return 0
 
 
+_MULTI: bool | None = None
+
+
+def _multi_rank() -> bool:
+    """True in a process group of more than one rank.  The persistent gemm8 (table ``ph`` 5) gives
+    each of its one-per-CU workgroups a FIXED share of the tiles; a collective kernel that holds CUs
+    for its whole duration (RCCL's channels, the peer collectives) then delays the workgroups that
+    cannot start, and with them the whole GEMM -- under ZeRO-3's reduce-scatters overlapped with the
+    dW GEMMs that costs far more than the persistence wins (0.7 % of the world-1 config-4 proxy,
+    profiles/r5e).  The one-tile-per-workgroup launch lets the hardware rebalance around them."""
+    global _MULTI
+    if _MULTI is None:
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()):
+            return False  # not cached: the group may come up later in this process
+        _MULTI = dist.get_world_size() > 1
+    return _MULTI
+
+
 def _policy() -> str:
     return os.environ.get("MXLLM_GEMM8", "table")
 
@@ -93,6 +113,8 @@ def schedule(form: str, M: int, N: int, K: int, out_dtype: torch.dtype) -> int:
     if pol == "0" or not takes(form, M, N, K):
         return 0
     ph = _table().get((form, M, N, K, "f32" if out_dtype == torch.float32 else "bf16"), 0)
+    if ph == 5 and _multi_rank():
+        ph = 4  # persistent kernel: world 1 only (see _multi_rank)
     if ph:
         return ph
     return DEFAULT_PH if (pol == "all" or deterministic()) else 0
