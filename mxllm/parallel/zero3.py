@@ -135,6 +135,17 @@ def init_full_state(cfg, seed, device) -> dict:
     return out
 
 
+class _EmuWork:
+    """Work handle of an async emulated collective: ``wait()`` makes the caller's stream wait."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+
 class Comm:
     """The two collectives ZeRO-3 issues, over real ranks or emulated.
 
@@ -153,6 +164,32 @@ class Comm:
 
             self.ag = comm_mod.create(ag_pg, device)
             self.rs = self.ag if rs_pg is ag_pg else comm_mod.create(rs_pg, device)
+        # emulated world N: the local stand-ins (a broadcast copy for the all-gather, an N-way sum
+        # for the reduce-scatter) run on the caller's stream by default -- every byte of them on
+        # the critical path, a conservative proxy.  MXLLM_Z3_EMUL_ASYNC=1 issues the async ones
+        # the way the real communicators do (their own two streams, the caller's stream waiting
+        # on an event at wait(), tensors kept alive by record_stream), so the proxy models the
+        # overlap -- and the CU contention of a collective kernel running beside the compute.
+        self._emu_streams = None
+        if (self.emulate and device is not None and torch.device(device).type == "cuda"
+                and os.environ.get("MXLLM_Z3_EMUL_ASYNC", "0") == "1"):
+            self._emu_streams = {"ag": torch.cuda.Stream(device), "rs": torch.cuda.Stream(device)}
+
+    def _emu(self, kind: str, fn, tensors, async_op: bool):
+        """Run an emulated collective's local stand-in ``fn``: inline, or (async emulation) on the
+        ``kind`` stream with RCCL's stream semantics."""
+        if not (async_op and self._emu_streams):
+            fn()
+            return None
+        s = self._emu_streams[kind]
+        s.wait_stream(torch.cuda.current_stream(s.device))
+        with torch.cuda.stream(s):
+            fn()
+        for t in tensors:
+            t.record_stream(s)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        return _EmuWork(ev)
 
     @property
     def real(self) -> bool:
@@ -165,17 +202,16 @@ class Comm:
     def all_gather(self, full: torch.Tensor, shard: torch.Tensor, async_op: bool):
         if self.real:
             return self.ag.all_gather(full, shard, async_op=async_op)
-        full.view(self.world, -1).copy_(shard.unsqueeze(0).expand(self.world, -1))
-        return None
+        return self._emu("ag", lambda: full.view(self.world, -1).copy_(shard.unsqueeze(0).expand(self.world, -1)),
+                         (full, shard), async_op)
 
     def reduce_scatter(self, out: torch.Tensor, full: torch.Tensor, async_op: bool):
         if self.real:
             return self.rs.reduce_scatter(out, full, async_op=async_op)
         if self.world == 1:
             out.copy_(full)
-        else:
-            torch.sum(full.view(self.world, -1), dim=0, out=out)
-        return None
+            return None
+        return self._emu("rs", lambda: torch.sum(full.view(self.world, -1), dim=0, out=out), (out, full), async_op)
 
     def all_reduce(self, t: torch.Tensor, async_op: bool = False):
         if self.real:
