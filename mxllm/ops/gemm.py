@@ -76,9 +76,6 @@ def tail_split(M: int, N: int, K: int) -> int:
     return 0
 
 
-_MULTI: bool | None = None
-
-
 def _multi_rank() -> bool:
     """True in a process group of more than one rank.  The persistent gemm8 (table ``ph`` 5) gives
     each of its one-per-CU workgroups a FIXED share of the tiles; a collective kernel that holds CUs
@@ -86,14 +83,11 @@ def _multi_rank() -> bool:
     cannot start, and with them the whole GEMM -- under ZeRO-3's reduce-scatters overlapped with the
     dW GEMMs that costs far more than the persistence wins (0.7 % of the world-1 config-4 proxy,
     profiles/r5e).  The one-tile-per-workgroup launch lets the hardware rebalance around them."""
-    global _MULTI
-    if _MULTI is None:
-        import torch.distributed as dist
+    import torch.distributed as dist
 
-        if not (dist.is_available() and dist.is_initialized()):
-            return False  # not cached: the group may come up later in this process
-        _MULTI = dist.get_world_size() > 1
-    return _MULTI
+    # asked only for ph-5 shapes (a few fp32 dW GEMMs per layer): not cached, so a process that
+    # brings a group up or down later is still answered right
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 def _policy() -> str:
