@@ -1,0 +1,26 @@
+#!/bin/bash
+# round 5 final evidence pass: GPU suite, smoke(), default bench line x2, kernel-trace breakdowns
+OUT=gpurun_out/${FINAL_OUT:-r5_final2}; mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/tests.txt 2>&1
+rc=$?; tail -3 $OUT/tests.txt; [ $rc -eq 0 ] || { echo "gpu suite rc=$rc"; exit 1; }
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "smoke rc=$?"; tail -5 $OUT/smoke.txt; exit 1; }
+tail -2 $OUT/smoke.txt
+for i in 1 2; do
+  timeout -k 10 400 python bench.py > $OUT/bench_$i.json 2> $OUT/bench_$i.err || { echo "bench rc=$?"; exit 1; }
+  echo "bench $i: $(python -c "import json;j=json.load(open('$OUT/bench_$i.json'));print(j['value'],j['ms_per_step'],j['config2_8b_full']['value'],j['config2_8b_full']['ms_per_step'],j['config2_8b_full_mb4']['value'],j['calibration'])")"
+done
+# config-4 proxy at the planner's depth on a 309 GB card (0 checkpointed layers, activations recomputed)
+C4="--model llama3.1-70b --finetune full --parallel zero3 --act-ckpt --act-ckpt-layers 0 --micro-batch 4 --emulate-world 8 --steps 3 --warmup 2 --no-calibrate"
+timeout -k 10 400 python -u bench.py $C4 --json-out $OUT/c4_ck0.json > $OUT/c4_ck0.log 2>&1 || { echo "c4 rc=$?"; exit 1; }
+echo "c4 ck0: $(python -c "import json;j=json.load(open('$OUT/c4_ck0.json'));print(j['ms_per_step'],j['value'],j['peak_hbm_reserved_gb'])")"
+ROOT=$(pwd)
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_head -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --config2 off --no-calibrate > $ROOT/$OUT/prof_head.log 2>&1 || { echo "prof head rc=$?"; exit 1; }
+python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_head/run_kernel_trace.csv 40 > $ROOT/$OUT/step_breakdown_70b_lora.txt
+head -16 $ROOT/$OUT/step_breakdown_70b_lora.txt
+rm -f $ROOT/$OUT/prof_head/run_kernel_trace.csv
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_c4 -o run -- python3 $ROOT/bench.py $C4 > $ROOT/$OUT/prof_c4.log 2>&1 || { echo "prof c4 rc=$?"; exit 1; }
+python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_c4/run_kernel_trace.csv 40 embedding_fwd > $ROOT/$OUT/step_breakdown_c4_ck0.txt
+head -12 $ROOT/$OUT/step_breakdown_c4_ck0.txt
+rm -f $ROOT/$OUT/prof_c4/run_kernel_trace.csv
