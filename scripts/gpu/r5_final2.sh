@@ -3,7 +3,8 @@
 OUT=gpurun_out/${FINAL_OUT:-r5_final2}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/tests.txt 2>&1
-rc=$?; tail -3 $OUT/tests.txt; [ $rc -eq 0 ] || { echo "gpu suite rc=$rc"; exit 1; }
+rc=$?; tail -3 $OUT/tests.txt; [ $rc -eq 0 ] || echo "gpu suite rc=$rc (continuing: bench evidence still wanted)"
+[ $rc -le 1 ] || { echo "suite ended abnormally (rc=$rc): stop"; exit 1; }  # 1 = tests failed; anything else: no more GPU work
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "smoke rc=$?"; tail -5 $OUT/smoke.txt; exit 1; }
 tail -2 $OUT/smoke.txt
 for i in 1 2; do
