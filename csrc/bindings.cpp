@@ -614,7 +614,7 @@ at::Tensor rope_merge_bwd(const at::Tensor& dq, const at::Tensor& dkp, const at:
   auto dqkv = empty_rows(B * S, NHD, out_pad, dq.options().dtype(at::kBFloat16));
   MX_OK(mx_rope_merge_bwd(dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), cos.data_ptr<float>(),
                           sin.data_ptr<float>(), bfm(dqkv), (int)B, (int)S, (int)Hq, (int)Hkv, (int)kvin, (int)D,
-                          NHD + out_pad, cur_stream()));
+                          NHD + out_pad, cur_stream(), 0));
   return dqkv;
 }
 
@@ -650,7 +650,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
                                                              double scale, int64_t dq_mode,
                                                              const c10::optional<at::Tensor>& dq_out = c10::nullopt,
                                                              const c10::optional<at::Tensor>& dk_out = c10::nullopt,
-                                                             const c10::optional<at::Tensor>& dv_out = c10::nullopt) {
+                                                             const c10::optional<at::Tensor>& dv_out = c10::nullopt,
+                                                             uint16_t* dqkv = nullptr, int64_t ldq = 0,
+                                                             const float* cosb = nullptr, const float* sinb = nullptr) {
   check_bf16(dout, "dout");
   check_f32(lse, "lse");
   const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
@@ -691,17 +693,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd_impl(const at::Tensor& d
   if (causal >= 0 && dq_mode != 1) {
     at::Tensor work = dq_mode == 2 ? at::empty({nkb, B, Hq, S_pad, D}, q.options().dtype(at::kFloat))
                                    : at::empty({B * Hq, nkb * 128, S_pad}, q.options());
-    auto dq = outs ? *dq_out : at::empty({B, Hq, S, D}, q.options().dtype(at::kFloat));
+    // dqkv: the dQ kernel writes d(q) into it; no fp32 dQ at all
+    auto dq = outs ? *dq_out
+                   : at::empty({dqkv ? 0 : B, Hq, S, D}, q.options().dtype(at::kFloat));
     MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                       dq.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
                       (int)S, (int)Sk, (int)D, causal, (float)scale, (int)dq_mode, work.data_ptr(), ldo,
-                      cur_stream()));
+                      cur_stream(), dqkv, ldq, cosb, sinb));
     return {dq, dkp, dvp};
   }
   auto dq_pad = at::zeros({B, Hq, S_pad, D}, q.options().dtype(at::kFloat));
   MX_OK(mx_attn_bwd(bf(q), bf(k), bf(v), bf(o), bf(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
                     dq_pad.data_ptr<float>(), dkp.data_ptr<float>(), dvp.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv,
-                    (int)S, (int)Sk, (int)D, causal, (float)scale, 1, nullptr, ldo, cur_stream()));
+                    (int)S, (int)Sk, (int)D, causal, (float)scale, 1, nullptr, ldo, cur_stream(), nullptr, 0, nullptr,
+                    nullptr));
   auto dq = S_pad == S ? dq_pad : dq_pad.narrow(2, 0, S).contiguous();
   return {dq, dkp, dvp};
 }
@@ -713,6 +718,33 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> attn_bwd(const at::Tensor& dout, 
                                                         const c10::optional<at::Tensor>& dk_out,
                                                         const c10::optional<at::Tensor>& dv_out) {
   return attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, dq_mode, dq_out, dk_out, dv_out);
+}
+
+// The attention backward straight into d(qkv) [B*S, (Hq+2Hkv)*D (+out_pad)] bf16 (D = 128, split mode):
+// the dQ kernel writes the q columns with the inverse RoPE applied, rope_merge_bwd only the k / v
+// columns from the dK / dV partials -- the fp32 dQ never reaches HBM (mxllm/ops/attention.py).
+at::Tensor attn_bwd_rope(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                         const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, const at::Tensor& cos,
+                         const at::Tensor& sin, int64_t out_pad) {
+  const int64_t B = q.size(0), Hq = q.size(1), S = q.size(2), D = q.size(3);
+  const int64_t Hkv = k.size(1), Sk = k.size(2);
+  MX_CHECK(D == 128 && Sk == S, "attn_bwd_rope: D = 128 self-attention");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  MX_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.numel() >= S * (D / 2) && sin.numel() >= S * (D / 2),
+           "cos / sin: [>= S, D/2] contiguous f32");
+  MX_CHECK(out_pad >= 0 && out_pad % 8 == 0, "out_pad must be a non-negative multiple of 8");
+  DevGuard g(q.device());
+  const int64_t NHD = (Hq + 2 * Hkv) * D;
+  auto dqkv = empty_rows(B * S, NHD, out_pad, q.options());
+  auto res = attn_bwd_impl(dout, q, k, v, o, lse, causal ? 1 : 0, scale, 3, c10::nullopt, c10::nullopt, c10::nullopt,
+                           bfm(dqkv), NHD + out_pad, cos.data_ptr<float>(), sin.data_ptr<float>());
+  const at::Tensor& dkp = std::get<1>(res);
+  const at::Tensor& dvp = std::get<2>(res);
+  MX_OK(mx_rope_merge_bwd(nullptr, dkp.data_ptr<float>(), dvp.data_ptr<float>(), cos.data_ptr<float>(),
+                          sin.data_ptr<float>(), bfm(dqkv), (int)B, (int)S, (int)Hq, (int)Hkv, (int)dkp.size(1), (int)D,
+                          NHD + out_pad, cur_stream(), (int)Hq));
+  return dqkv;
 }
 
 // timing-only ablation variants (mode: -1 = causal without dQ atomics)
@@ -1172,6 +1204,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("lora_grads(Tensor x, Tensor dy, Tensor g, Tensor st, Tensor(a!) ga, Tensor(b!) gb, int[] splits, int r, bool accumulate) -> ()");
   m.def("attn_bwd_ablate(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, int mode, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, int dq_mode=3, Tensor? dq_out=None, Tensor? dk_out=None, Tensor? dv_out=None) -> (Tensor, Tensor, Tensor)");
+  m.def("attn_bwd_rope(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor cos, Tensor sin, int out_pad=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
@@ -1203,6 +1236,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("rope_merge_bwd", &rope_merge_bwd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("attn_bwd_rope", &attn_bwd_rope);
   m.impl("attn_bwd_ablate", &attn_bwd_ablate);
   m.impl("rope_append", &rope_append);
   m.impl("decode_attn_partials", &decode_attn_partials);

@@ -72,14 +72,15 @@ int mx_rope_split(const uint16_t* qkv, const float* cosb, const float* sinb, con
                   uint16_t* k, uint16_t* v, int B, int S, int Hq, int Hkv, int D, hipStream_t stream);
 int mx_rope_merge_bwd(const float* dq, const float* dkp, const float* dvp, const float* cosb, const float* sinb,
                       uint16_t* dqkv, int B, int S, int Hq, int Hkv, int kv_heads_in, int D, int64_t ldq,
-                      hipStream_t stream);
+                      hipStream_t stream, int head0);
 // attn_fwd.hip / attn_bwd.hip
 int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B, int Hq,
                 int Hkv, int S, int Sk, int D, int causal, float scale, int ldo, hipStream_t stream);
 int mx_attn_bwd_partial_heads(int B, int Hq, int Hkv, int S, int Sk, int D, int dq_mode);
 int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o, const uint16_t* dout,
                 const float* lse, float* delta, float* dq, float* dkp, float* dvp, int B, int Hq, int Hkv, int S,
-                int Sk, int D, int causal, float scale, int dq_mode, void* work, int64_t ldo, hipStream_t stream);
+                int Sk, int D, int causal, float scale, int dq_mode, void* work, int64_t ldo, hipStream_t stream,
+                uint16_t* dqkv, int64_t ldq, const float* cosb, const float* sinb);
 }
 
 extern "C" {

@@ -1134,7 +1134,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_reduce(const float* __restric
 template <int D, bool CAUSAL, int QB>
 __global__ void __launch_bounds__(256 * QB, 1)
 attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict__ K, float* __restrict__ dQ,
-                   int B, int Hq, int Hkv, int S, int Sk, int off, int S_pad, int Sk_pad, float scale) {
+                   int B, int Hq, int Hkv, int S, int Sk, int off, int S_pad, int Sk_pad, float scale,
+                   uint16_t* __restrict__ dqkv = nullptr, int64_t ldq = 0, const float* __restrict__ cosb = nullptr,
+                   const float* __restrict__ sinb = nullptr) {
   constexpr int BK = 64, BQ = 64, CH = D / 8, ROWB = D * 2, DB = D / 32;
   constexpr int DSROWB = BQ * 2;     // dS^T image row: 64 q = 128 B
   constexpr int KT = BK * ROWB;      // K tile [64][D]
@@ -1305,6 +1307,55 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
       }
     }
   }
+  // dqkv (D = 128): the q columns of the token-major d(qkv) directly -- scaled, the inverse RoPE
+  // applied in fp32 and rounded to bf16 once, the arithmetic of rope_merge_bwd_kernel -- instead of
+  // an fp32 dQ that kernel re-reads (70B training shape: 134 MB written + 134 MB read per layer
+  // become 67 MB written).  The rotate-half partner of column d is d +- 64, held by wave wl ^ 2 of
+  // the sub-block: the tile goes through LDS ([sub][64 rows][128] fp32, the freed stage buffers).
+  if constexpr (D == 128 && QB == 4) {
+    if (dqkv != nullptr) {
+      static_assert(QB * BQ * D * 4 <= NSTAGE * BUF, "dQ exchange tile fits the stage buffers");
+      lds_wait();
+      __syncthreads();  // every wave past its last stage reads (the last stage waited vmcnt(0))
+      float* xs = reinterpret_cast<float*>(smem) + (size_t)sub * BQ * D;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int tile = wl + 4 * t;
+        if (tile < 2 * DB) {
+          const int m = tile / DB, db = tile % DB;
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            xs[(32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh) * D + db * 32 + r] = acc[t][j] * scale;
+        }
+      }
+      __syncthreads();
+      constexpr int HALF = D / 2;
+      for (int u = wl * 64 + lane; u < BQ * (HALF / 8); u += 256) {
+        const int row = u / (HALF / 8), c = (u % (HALF / 8)) * 8;
+        const int q = qsub0 + row;
+        if (q >= S) continue;
+        const float* x = xs + row * D;
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(x + c), u1 = *reinterpret_cast<const f32x4*>(x + c + 4);
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(x + HALF + c);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(x + HALF + c + 4);
+        const float a1[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+        const float a2[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+        const float* cp = cosb + (int64_t)q * HALF + c;
+        const float* sp = sinb + (int64_t)q * HALF + c;
+        u16x8 y1, y2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float cj = cp[j], sj = sp[j];
+          y1[j] = f2bf(a1[j] * cj + a2[j] * sj);
+          y2[j] = f2bf(a2[j] * cj - a1[j] * sj);
+        }
+        uint16_t* dst = dqkv + ((int64_t)b * S + q) * ldq + (int64_t)h * D;
+        *reinterpret_cast<u16x8*>(dst + c) = y1;
+        *reinterpret_cast<u16x8*>(dst + HALF + c) = y2;
+      }
+      return;
+    }
+  }
   // C layout: row = qsub0 + 32m + (j&3) + 8(j>>2) + 4hh, col = db*32 + r
   float* dqp = dQ + (size_t)bh * S * D;
 #pragma unroll
@@ -1368,10 +1419,13 @@ extern "C" int mx_attn_bwd_partial_heads(int B, int Hq, int Hkv, int S, int Sk, 
 extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
                            const uint16_t* dout, const float* lse, float* delta, float* dq, float* dkp, float* dvp,
                            int B, int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, int dq_mode,
-                           void* work, int64_t ldo, hipStream_t stream) {
+                           void* work, int64_t ldo, hipStream_t stream, uint16_t* dqkv, int64_t ldq,
+                           const float* cosb, const float* sinb) {
   if (B <= 0 || S <= 0 || Sk <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return -1;
   if (dq_mode < 1 || dq_mode > 3 || (dq_mode > 1 && !work)) return -1;
+  // dqkv: the split dQ kernel writes d(q) with the inverse RoPE into it (D = 128, split mode only)
+  if (dqkv && (dq_mode != 3 || D != 128 || !cosb || !sinb || ldq % 8 || causal < 0)) return -1;
   const int64_t rows = (int64_t)B * S * Hq;
   const int64_t dthreads = rows * (D / 8);
   const unsigned dgrid = (unsigned)((dthreads + 255) / 256);
@@ -1496,10 +1550,10 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     constexpr int QB = DD == 128 ? 4 : (DD == 64 ? 2 : 1);                                                        \
     if (causal)                                                                                                   \
       attn_bwd_dq_kernel<DD, true, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,  \
-                                                                       nkb * 128, scale);                         \
+                                                                       nkb * 128, scale, dqkv, ldq, cosb, sinb);  \
     else                                                                                                          \
       attn_bwd_dq_kernel<DD, false, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, \
-                                                                        nkb * 128, scale);                        \
+                                                                        nkb * 128, scale, dqkv, ldq, cosb, sinb); \
   } while (0)
     if (D == 128) DQK(128);
     else if (D == 64) DQK(64);

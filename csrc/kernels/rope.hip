@@ -70,16 +70,17 @@ __global__ void __launch_bounds__(256) rope_merge_bwd_kernel(const float* __rest
                                                              const float* __restrict__ cosb,
                                                              const float* __restrict__ sinb,
                                                              uint16_t* __restrict__ dqkv, int B, int S, int Hq,
-                                                             int Hkv, int kv_heads_in, int64_t ldq) {
+                                                             int Hkv, int kv_heads_in, int64_t ldq, int head0) {
   constexpr int HALF = D / 2, CPH = HALF / 8;
   const int NH = Hq + 2 * Hkv;
+  const int NHW = NH - head0;         // heads this call writes: head0 .. NH-1 (head0 = Hq: the dQ kernel did q)
   const int rep = kv_heads_in / Hkv;  // partials per kv head (Hq for per-q-head partials, Hkv if pre-summed)
-  const int64_t n = (int64_t)B * S * NH * CPH;
+  const int64_t n = (int64_t)B * S * NHW * CPH;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int cc = (int)(i % CPH);
     const int64_t th = i / CPH;
-    const int head = (int)(th % NH);
-    const int64_t t = th / NH;
+    const int head = head0 + (int)(th % NHW);
+    const int64_t t = th / NHW;
     const int b = (int)(t / S), s = (int)(t % S);
     const int c = cc * 8;
     float a1[8], a2[8];
@@ -158,13 +159,14 @@ extern "C" int mx_rope_split(const uint16_t* qkv, const float* cosb, const float
 // be the left part of the LoRA-augmented backward GEMM operand (mxllm/ops/linear.py)
 extern "C" int mx_rope_merge_bwd(const float* dq, const float* dkp, const float* dvp, const float* cosb,
                                  const float* sinb, uint16_t* dqkv, int B, int S, int Hq, int Hkv, int kv_heads_in,
-                                 int D, int64_t ldq, hipStream_t stream) {
-  const int64_t items = (int64_t)B * S * (Hq + 2 * Hkv) * (D / 16);
+                                 int D, int64_t ldq, hipStream_t stream, int head0) {
+  if (head0 != 0 && head0 != Hq) return -1;  // all heads, or the k / v heads only (dq == nullptr allowed)
+  const int64_t items = (int64_t)B * S * (Hq + 2 * Hkv - head0) * (D / 16);
   if (items <= 0) return 0;
   if (kv_heads_in % Hkv || ldq < (int64_t)(Hq + 2 * Hkv) * D || ldq % 8) return -1;
 #define MERGE(DD)                                                                                       \
   rope_merge_bwd_kernel<DD><<<grid_for(items), 256, 0, stream>>>(dq, dkp, dvp, cosb, sinb, dqkv, B, S, Hq, Hkv, \
-                                                                 kv_heads_in, ldq)
+                                                                 kv_heads_in, ldq, head0)
   if (D == 128) MERGE(128);
   else if (D == 64) MERGE(64);
   else if (D == 32) MERGE(32);

@@ -11,7 +11,8 @@ GPU path (csrc/kernels/rope.hip, attn_fwd.hip, attn_bwd.hip):
             --attn_fwd (MFMA 32x32x16 bf16)--> o [B,S,Hq*D] token-major, lse [B,Hq,S]
   backward: attn_bwd -> dq f32 [B,Hq,S,D] (dS^T through HBM + a dQ kernel by
             default; f32-atomic and partial-sum modes selectable), dk/dv partials
-            [B,Hq,S,D] f32 --rope_merge_bwd--> d(qkv) bf16 [T,(Hq+2Hkv)D]
+            [B,Hq,S,D] f32 --rope_merge_bwd--> d(qkv) bf16 [T,(Hq+2Hkv)D]; at D = 128 the
+            dQ kernel writes d(q) of d(qkv) itself (attn_bwd_rope, backward_dqkv)
 """
 from __future__ import annotations
 
@@ -43,13 +44,33 @@ class _AttnBlockFn(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse, cos, sin = ctx.saved_tensors
         B, S, Hq, Hkv, D, causal, grad_pad = ctx.dims
-        ops = native()
-        dq, dkp, dvp = attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D), dq_mode())
-        dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D, grad_pad)
+        dqkv = backward_dqkv(do, q, k, v, o, lse, cos, sin, causal, grad_pad)
         return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
 _DS_BUDGET = float(os.environ.get("MXLLM_ATTN_DS_BUDGET_GB", "4")) * 2**30
+
+
+def _ds_bytes_per_head(S: int, Sk: int) -> int:
+    return (Sk + 127) // 128 * 128 * ((S + 63) // 64 * 64) * 2
+
+
+def backward_dqkv(do, q, k, v, o, lse, cos, sin, causal: bool, grad_pad: int = 0) -> torch.Tensor:
+    """d(qkv) [B*S, (Hq+2Hkv)*D (+grad_pad)] bf16 of the RoPE'd attention block.  The split backward at
+    D = 128 writes it directly (``attn_bwd_rope``: the dQ kernel applies the inverse RoPE to d(q) and
+    rounds once, rope_merge_bwd fills only the k / v columns; no fp32 dQ through HBM -- 70B training
+    shape: -201 MB of traffic per layer); otherwise fp32 dQ + dK / dV partials then rope_merge_bwd.
+    ``MXLLM_ATTN_DQ_ROPE=0`` forces the two-step path (A/B)."""
+    ops = native()
+    B, Hq, S, D = q.shape
+    Hkv, Sk = k.shape[1], k.shape[2]
+    scale = 1.0 / math.sqrt(D)
+    mode = dq_mode()
+    if (mode == 3 and D == 128 and Sk == S and B * Hq * _ds_bytes_per_head(S, Sk) <= _DS_BUDGET
+            and os.environ.get("MXLLM_ATTN_DQ_ROPE", "1") != "0"):
+        return ops.attn_bwd_rope(do.contiguous(), q, k, v, o, lse, causal, scale, cos, sin, grad_pad)
+    dq, dkp, dvp = attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, mode)
+    return ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D, grad_pad)
 
 
 def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float, mode: int):
@@ -63,7 +84,7 @@ def attn_bwd(do, q, k, v, o, lse, causal: bool, scale: float, mode: int):
     ops = native()
     B, Hq, S, D = q.shape
     Hkv, Sk = k.shape[1], k.shape[2]
-    per_head = (Sk + 127) // 128 * 128 * ((S + 63) // 64 * 64) * 2
+    per_head = _ds_bytes_per_head(S, Sk)
     if mode != 3 or B * Hq * per_head <= _DS_BUDGET:
         return ops.attn_bwd(do, q, k, v, o, lse, causal, scale, mode)
     G = Hq // Hkv

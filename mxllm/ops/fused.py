@@ -74,15 +74,12 @@ class _QKVAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
-        from .attention import attn_bwd, dq_mode
+        from .attention import backward_dqkv
 
         xs, w, q, k, v, o, lse, cos, sin, nw = ctx.saved_tensors
         B, S, Hq, Hkv, D, causal, xshape, keep_x, eps = ctx.dims
-        ops = native()
-        dq, dkp, dvp = attn_bwd(do.contiguous(), q, k, v, o, lse, causal, 1.0 / math.sqrt(D), dq_mode())
+        dqkv = backward_dqkv(do, q, k, v, o, lse, cos, sin, causal, 0)
         del q, k, v, o, lse
-        dqkv = ops.rope_merge_bwd(dq, dkp, dvp, cos, sin, B, S, Hq, Hkv, D, 0)
-        del dq, dkp, dvp
         dx = gemm.mm("nn", dqkv, w).view(xshape) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
