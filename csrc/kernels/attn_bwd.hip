@@ -1346,8 +1346,8 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float cj = cp[j], sj = sp[j];
-          y1[j] = f2bf(a1[j] * cj + a2[j] * sj);
-          y2[j] = f2bf(a2[j] * cj - a1[j] * sj);
+          y1[j] = f2bf(__builtin_fmaf(a1[j], cj, a2[j] * sj));  // same contraction as rope_merge_bwd_kernel
+          y2[j] = f2bf(__builtin_fmaf(a2[j], cj, -(a1[j] * sj)));
         }
         uint16_t* dst = dqkv + ((int64_t)b * S + q) * ldq + (int64_t)h * D;
         *reinterpret_cast<u16x8*>(dst + c) = y1;

@@ -121,8 +121,8 @@ __global__ void __launch_bounds__(256) rope_merge_bwd_kernel(const float* __rest
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float cj = cp[j], sj = sp[j];
-        y1[j] = f2bf(a1[j] * cj + a2[j] * sj);
-        y2[j] = f2bf(a2[j] * cj - a1[j] * sj);
+        y1[j] = f2bf(__builtin_fmaf(a1[j], cj, a2[j] * sj));  // explicit contraction: the dQ kernel's
+        y2[j] = f2bf(__builtin_fmaf(a2[j], cj, -(a1[j] * sj)));  // epilogue and this give the same bits
       }
     }
     *reinterpret_cast<u16x8*>(dst + c) = y1;
