@@ -25,3 +25,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/
 python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_c4/run_kernel_trace.csv 40 embedding_fwd > $ROOT/$OUT/step_breakdown_c4_ck0.txt
 head -12 $ROOT/$OUT/step_breakdown_c4_ck0.txt
 rm -f $ROOT/$OUT/prof_c4/run_kernel_trace.csv
+C2="--model llama3.1-8b --finetune full --steps 4 --warmup 2 --no-calibrate --config2 off"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_c2 -o run -- python3 $ROOT/bench.py $C2 > $ROOT/$OUT/prof_c2.log 2>&1 || { echo "prof c2 rc=$?"; exit 1; }
+python $ROOT/scripts/step_breakdown.py $ROOT/$OUT/prof_c2/run_kernel_trace.csv 40 > $ROOT/$OUT/step_breakdown_c2_8b_full.txt
+head -12 $ROOT/$OUT/step_breakdown_c2_8b_full.txt
+rm -f $ROOT/$OUT/prof_c2/run_kernel_trace.csv
+echo done
