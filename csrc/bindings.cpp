@@ -277,6 +277,41 @@ bool gemm8_swiglu(const at::Tensor& x, const at::Tensor& w, at::Tensor& gu, at::
   return true;
 }
 
+// The down projection's dX GEMM with the SwiGLU backward in its epilogue (gemm8 G8_EPI_SWIGLU_BWD):
+// dy [T, H] and w = W_down [H, F] -> dgu [T, 2F] from the forward's gu [T, 2F] (dm never reaches
+// HBM), and with m given also m = silu(g) u [T, F] (the recompute path's dW input).  Returns false
+// (nothing launched) for shapes the kernel does not take.
+bool gemm8_swiglu_bwd(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& gu, at::Tensor& dgu,
+                      const c10::optional<at::Tensor>& m) {
+  MX_CHECK(dy.is_cuda() && w.is_cuda() && gu.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
+               w.scalar_type() == at::kBFloat16 && gu.scalar_type() == at::kBFloat16 &&
+               dgu.scalar_type() == at::kBFloat16,
+           "gemm8_swiglu_bwd: bf16 GPU tensors");
+  MX_CHECK(dy.dim() == 2 && w.dim() == 2 && gu.dim() == 2 && dgu.dim() == 2 && dy.size(1) == w.size(0) &&
+               gu.size(0) == dy.size(0) && gu.size(1) == 2 * w.size(1) && dgu.sizes() == gu.sizes(),
+           "gemm8_swiglu_bwd: shapes");
+  if (m) {
+    MX_CHECK(m->scalar_type() == at::kBFloat16 && m->dim() == 2 && m->size(0) == dy.size(0) &&
+                 m->size(1) == w.size(1),
+             "gemm8_swiglu_bwd: m [T, F] bf16");
+    if (m->stride(1) != 1) return false;
+  }
+  if (dy.stride(1) != 1 || w.stride(1) != 1 || gu.stride(1) != 1 || dgu.stride(1) != 1) return false;
+  DevGuard g(dy.device());
+  MxG8Epi ep{};
+  ep.gu = bf(gu);
+  ep.ldg = gu.stride(0);
+  if (m) {
+    ep.m = reinterpret_cast<uint16_t*>(m->data_ptr());
+    ep.ldm = m->stride(0);
+  }
+  const int rc = mx_gemm8_epi(bf(dy), dy.stride(0), bf(w), w.stride(0), bfm(dgu), dgu.stride(0), (int)dy.size(0),
+                              (int)w.size(1), (int)dy.size(1), 3, ep, cur_stream());
+  if (rc == -1) return false;
+  MX_OK(rc);
+  return true;
+}
+
 // the gemm8 diagnostic build's cycle stamps (MXLLM_GEMM8_STAMPS): int64 [1024, 2, 80] on the host
 at::Tensor gemm8_stamps() {
   auto out = at::empty({1024, 2, 80}, at::TensorOptions().dtype(at::kLong));
@@ -1168,6 +1203,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4) -> bool");
   m.def("gemm8_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, Tensor(a!) q, Tensor(b!) k, Tensor(c!) v) -> bool");
   m.def("gemm8_swiglu(Tensor x, Tensor w, Tensor(a!) gu, Tensor(b!) m) -> bool");
+  m.def("gemm8_swiglu_bwd(Tensor dy, Tensor w, Tensor gu, Tensor(a!) dgu, Tensor(b!)? m=None) -> bool");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
   m.def("swiglu_bwd(Tensor dm, Tensor gu, int out_pad=0) -> Tensor");
@@ -1217,6 +1253,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("gemm8_tail", &gemm8_tail);
   m.impl("gemm8_rope", &gemm8_rope);
   m.impl("gemm8_swiglu", &gemm8_swiglu);
+  m.impl("gemm8_swiglu_bwd", &gemm8_swiglu_bwd);
   m.impl("ce_inv_count", &ce_inv_count);
   m.impl("ce_chunk", &ce_chunk);
   m.impl("ce_chunk_f32", &ce_chunk_f32);

@@ -48,6 +48,8 @@ struct MxG8Epi {
   uint16_t* m;
   int64_t ldm;
   int F;
+  const uint16_t* gu;
+  int64_t ldg;
 };
 int mx_gemm8_epi(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int M,
                  int N, int K, int mode, MxG8Epi ep, hipStream_t stream);

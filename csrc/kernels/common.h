@@ -31,6 +31,18 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// SwiGLU gradient, s = sigmoid(g) by the hardware reciprocal:
+//   dg = dm u s (1 + g (1 - s)),  du = dm g s.
+// The one multiply-add is an explicit FMA and the rest are product chains, so
+// -ffp-contract=fast has nothing left to contract.  Every kernel that produces
+// dgu (elementwise.hip swiglu_bwd, lora.hip swiglu_lora, the gemm8 SwiGLU-backward
+// epilogue) therefore gives the same bits.
+__device__ __forceinline__ void swiglu_grad(float dm, float g, float u, float& dg, float& du) {
+  const float s = __builtin_amdgcn_rcpf(1.f + __expf(-g));
+  dg = dm * u * s * __builtin_fmaf(g, 1.f - s, 1.f);
+  du = dm * g * s;
+}
+
 // two f32 -> packed bf16x2 in one u32 (lo in bits 0..15)
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);

@@ -57,10 +57,11 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
-      const float s = sigmoid_f(gf);
-      og[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
-      ou[j] = f2bf(df * gf * s);
-      if constexpr (WM) om[j] = f2bf(gf * s * uf);
+      float dg, du;
+      swiglu_grad(df, gf, uf, dg, du);
+      og[j] = f2bf(dg);
+      ou[j] = f2bf(du);
+      if constexpr (WM) om[j] = f2bf(gf * sigmoid_f(gf) * uf);
     }
     uint16_t* orow = dgu + t * ldg;
     *reinterpret_cast<u16x8*>(orow + c) = og;

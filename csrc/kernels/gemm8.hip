@@ -80,9 +80,13 @@ __device__ __forceinline__ int g8_map_a(int r, int h) { return (r >> 6) * 128 + 
 //               [128 pn, 128 pn + 128) and the same up columns: jh = 0 -> gate row 128 pn + 32 wc +
 //               16 jl + q, jh = 1 -> the up row F further; outputs gu [T, 2F] (standard layout, saved
 //               for the backward) AND m = silu(g) u [T, F] (elementwise.hip swiglu_fwd, fused away)
-// Both round the GEMM result to bf16 first and then apply the exact expression of the kernel they
-// replace: bitwise equal to GEMM -> rope_split / swiglu_fwd on the same kernel's output.
-constexpr int G8_EPI_NONE = 0, G8_EPI_ROPE = 1, G8_EPI_SWIGLU = 2;
+//  G8_EPI_SWIGLU_BWD (NN form: the down projection's dX GEMM dm = dy W_down, F = N columns): the
+//               lane's 8 dm columns (after the bf16 swap) meet the saved gu [T, 2F] at the same
+//               columns -> writes dgu [T, 2F] (and, with ep.m set, the recomputed m = silu(g) u) in
+//               place of dm (elementwise.hip swiglu_bwd / swiglu_bwd_m, fused away)
+// All round the GEMM result to bf16 first and then apply the exact expression of the kernel they
+// replace: bitwise equal to GEMM -> rope_split / swiglu_fwd / swiglu_bwd on the same kernel's output.
+constexpr int G8_EPI_NONE = 0, G8_EPI_ROPE = 1, G8_EPI_SWIGLU = 2, G8_EPI_SWIGLU_BWD = 3;
 
 struct G8Epi {
   uint16_t* q;        // ROPE: [B, Hq, S, 128]
@@ -91,9 +95,11 @@ struct G8Epi {
   const float* cosb;  //       [>= S, 64] f32 (host table, mxllm/ops/reference.py rope_tables)
   const float* sinb;
   int S, Hq, Hkv;
-  uint16_t* m;        // SWIGLU: [T, F] with row stride ldm
+  uint16_t* m;        // SWIGLU: [T, F] with row stride ldm (SWIGLU_BWD: optional recomputed m)
   int64_t ldm;
   int F;
+  const uint16_t* gu; // SWIGLU_BWD: the forward's [T, 2F] with row stride ldg
+  int64_t ldg;
 };
 
 // weight row feeding virtual tile column v (0..255) of output tile pn (G8_EPI_SWIGLU: absolute row)
@@ -227,6 +233,53 @@ __device__ __forceinline__ void g8_epilogue_fused(f32x4 (&acc)[8][4], float alph
         g8_store8(row + d0 + u8, x0[0], x0[1]);
         g8_store8(row + d0 + 64 + u8, x1[0], x1[1]);
       }
+  } else if constexpr (EPI == G8_EPI_SWIGLU_BWD) {
+    const int F = N;
+    const int cb = 256 * pn + 64 * wc + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5);  // + 32 jp
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = ml + qa * 64 + 16 * i;
+        const uint16_t* gr = ep.gu + m * ep.ldg;
+        u16x8 g8[2], u8v[2], d8[2];
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          g8[jp] = *reinterpret_cast<const u16x8*>(gr + cb + 32 * jp);
+          u8v[jp] = *reinterpret_cast<const u16x8*>(gr + F + cb + 32 * jp);
+        }
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {  // dm rounded to bf16 and swapped exactly as the plain store
+          const f32x4 va = acc[4 * qa + i][2 * jp] * alpha, vb = acc[4 * qa + i][2 * jp + 1] * alpha;
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(va[0], va[1]), pack_bf16x2(vb[0], vb[1]),
+                                                          false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[2], vb[3]),
+                                                          false, false);
+          uint4 o;
+          o.x = s0[0];
+          o.y = s1[0];
+          o.z = s0[1];
+          o.w = s1[1];
+          d8[jp] = __builtin_bit_cast(u16x8, o);
+        }
+        uint16_t* dr = reinterpret_cast<uint16_t*>(C) + m * ldc;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          u16x8 og, ou, om;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gf = bf2f(g8[jp][j]), uf = bf2f(u8v[jp][j]);
+            float dg, du;
+            swiglu_grad(bf2f(d8[jp][j]), gf, uf, dg, du);
+            og[j] = f2bf(dg);
+            ou[j] = f2bf(du);
+            om[j] = f2bf(gf * __builtin_amdgcn_rcpf(1.f + __expf(-gf)) * uf);
+          }
+          *reinterpret_cast<u16x8*>(dr + cb + 32 * jp) = og;
+          *reinterpret_cast<u16x8*>(dr + F + cb + 32 * jp) = ou;
+          if (ep.m) *reinterpret_cast<u16x8*>(ep.m + m * ep.ldm + cb + 32 * jp) = om;
+        }
+      }
   } else {  // G8_EPI_SWIGLU
     const int F = N / 2;
     const int col = 128 * pn + 32 * wc + u8;  // gate column (up: + F; m: the same column)
@@ -264,7 +317,8 @@ __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
              void* __restrict__ C, int64_t ldc, int M, int N, int K, const float* __restrict__ alpha_t,
              float alpha_f, int k0 = 0, int64_t cpart = 0, G8Epi ep = G8Epi{}) {
-  static_assert(EPI == G8_EPI_NONE || (B_KC && !OUT_F32 && !BETA), "fused epilogues: TN-form bf16 forward only");
+  static_assert(EPI == G8_EPI_NONE || (!OUT_F32 && !BETA && (EPI == G8_EPI_SWIGLU_BWD ? A_KC && !B_KC : B_KC)),
+                "fused epilogues: bf16, beta 0; TN-form forwards, NN-form SwiGLU backward");
   // K split in two (gridDim.y == 2, k0 = K of part 0): part 1 covers K rows / columns k0 .. K-1 of
   // both operands and writes its own output image C + cpart (mx_gemm8_tail: the last, partial wave
   // of tiles of a GEMM runs as twice as many half-K workgroups; the images are summed after)
@@ -1075,9 +1129,24 @@ extern "C" int mx_gemm8(const uint16_t* A, int64_t lda, int a_kc, const uint16_t
 // Forward projection with a fused epilogue (G8Epi above), A = x [M][K] and B = W [N][K] both
 // k-contiguous, 4-phase schedule.  mode 1 (ROPE): N = (Hq + 2 Hkv) * 128, M = B * S, S % 256 == 0,
 // writes q / k / v head-major (C unused).  mode 2 (SWIGLU): N = 2F, F % 128 == 0, writes gu into C
-// [M][ldc >= 2F] and m into ep.m [M][ldm >= F].  Returns -1 (nothing launched) for other shapes.
+// [M][ldc >= 2F] and m into ep.m [M][ldm >= F].  mode 3 (SWIGLU_BWD, NN form: A = dy [M][K], B =
+// W_down [K][N]): dm -> dgu into C [M][ldc >= 2N] from ep.gu, and m into ep.m when set.  Returns -1
+// (nothing launched) for other shapes.
 extern "C" int mx_gemm8_epi(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
                             int M, int N, int K, int mode, G8Epi ep, hipStream_t stream) {
+  if (mode == G8_EPI_SWIGLU_BWD) {
+    // NN: A = dy [M][K] k-contiguous, B = W_down [K][N] n-contiguous; C = dgu [M][ldc >= 2N]
+    if (M <= 0 || N <= 0 || K <= 0 || (M & 255) || (N & 255) || K % G8_BK) return -1;
+    if (lda % 8 || ldb % 8 || lda < K || ldb < N || ldc < 2 * (int64_t)N || ldc % 8 || !C || !ep.gu ||
+        ep.ldg < 2 * (int64_t)N || ep.ldg % 8 || (ep.m && (ep.ldm < N || ep.ldm % 8)) ||
+        (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)ep.gu | (uintptr_t)ep.m) & 15))
+      return -1;
+    if (256 * lda * 2 >= ((int64_t)1 << 31) || (int64_t)K * ldb * 2 >= ((int64_t)1 << 31)) return -1;
+    ep.F = N;
+    gemm8_kernel<true, false, false, false, 0, 4, G8_EPI_SWIGLU_BWD><<<(M >> 8) * (N >> 8), 512, 0, stream>>>(
+        A, lda, B, ldb, C, ldc, M, N, K, nullptr, 1.f, 0, 0, ep);
+    return (int)hipGetLastError();
+  }
   if (M <= 0 || N <= 0 || K <= 0 || (M & 255) || (N & 255) || K % G8_BK) return -1;
   if (lda % 8 || ldb % 8 || lda < K || ldb < K || ((uintptr_t)A | (uintptr_t)B) & 15) return -1;
   const int64_t aspan = 256 * lda, bspan = (int64_t)N * ldb;

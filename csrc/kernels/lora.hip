@@ -744,9 +744,10 @@ __global__ void __launch_bounds__(256) swiglu_lora_kernel(const uint16_t* __rest
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float gf = bf2f(g[i][j]), uf = bf2f(u[i][j]), df = bf2f(d[i][j]);
-          const float s = sl_sigmoid(gf);
-          o0[j] = f2bf(df * uf * s * (1.f + gf * (1.f - s)));
-          o1[j] = f2bf(df * gf * s);
+          float dg, du;
+          swiglu_grad(df, gf, uf, dg, du);
+          o0[j] = f2bf(dg);
+          o1[j] = f2bf(du);
         }
         *reinterpret_cast<u16x8*>(orow + i * ostep + c) = o0;
         *reinterpret_cast<u16x8*>(orow + i * ostep + F + c) = o1;

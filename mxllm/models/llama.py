@@ -280,6 +280,10 @@ class Llama(nn.Module):
         if rec:  # m = swiglu(gu) (and the gate-up input x) recomputed in the backward
             gu = ops.normed_linear(x, h, layer.mlp_norm, cfg.norm_eps, layer.wgu.weight) if rec_x else layer.wgu(x)
             d = ops.swiglu_linear(gu, layer.wd.weight)
+        elif (not layer.wgu.lora_r and not layer.wd.lora_r
+              and fused.gate_up_swiglu_down_ok(x, layer.wgu.weight, layer.wd.weight)):
+            # gate-up + SwiGLU + down: the backward's dm GEMM writes dgu (mxllm/ops/fused.py)
+            d = fused.gate_up_swiglu_down(x, layer.wgu.weight, layer.wd.weight)
         elif not layer.wgu.lora_r and fused.gate_up_swiglu_ok(x, layer.wgu.weight):
             # gate-up projection with SwiGLU in its epilogue (mxllm/ops/fused.py)
             m = fused.gate_up_swiglu(x, layer.wgu.weight, out_pad=self._pad(layer.wd))

@@ -12,6 +12,10 @@ touches HBM:
     attention; backward = attention backward -> inverse-RoPE merge -> dX / dW GEMMs.
   * ``gate_up_swiglu`` x -> (gu, m = silu(g) u) from ONE GEMM; gu is kept for the backward
     (SwiGLU backward -> dX / dW GEMMs).
+  * ``gate_up_swiglu_down`` the same plus the down projection, so that its backward can run the
+    down projection's dX GEMM with the SwiGLU backward in the epilogue (``G8_EPI_SWIGLU_BWD``):
+    dgu straight from dy, W_down and the saved gu; the [T, F] dm never touches HBM and the
+    separate swiglu_bwd pass (reads dm + gu, writes dgu) is gone.
 
 The weight gradients go the ``_LinearFn`` way (written by the dW GEMM straight into the
 owner's buffer).  Bitwise, each epilogue equals the GEMM followed by the kernel it replaces
@@ -30,6 +34,8 @@ from ._ext import native, use_native
 from .linear import param_weight_grad
 
 _ON = os.environ.get("MXLLM_FUSED_EPI", "1") != "0"
+# the down projection's dX GEMM writes dgu through the SwiGLU backward epilogue (A/B: 0 = dm + swiglu_bwd)
+_BWD_ON = os.environ.get("MXLLM_FUSED_SWIGLU_BWD", "1") != "0"
 
 
 def _x2(x: torch.Tensor) -> torch.Tensor:
@@ -142,3 +148,70 @@ def gate_up_swiglu(x: torch.Tensor, w: torch.Tensor, out_pad: int = 0, norm: tup
     ``out_pad``: the result is the left part of a [T, F + out_pad] buffer."""
     h, nw, eps = norm if norm is not None else (None, None, 0.0)
     return _GateUpSwiGLUFn.apply(x, w, out_pad, h, nw, eps)
+
+
+def swiglu_bwd_gemm(dy: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor, want_m: bool = False):
+    """(dgu, m or None) = SwiGLU backward of dm = dy W_down from the saved gu, through the gemm8
+    epilogue when it takes the shape, else the NN GEMM + swiglu_bwd(_m) pass (same bits where the
+    GEMM dispatch picks gemm8 for dm: the epilogue's main loop is the plain kernel's)."""
+    if _BWD_ON and use_native(dy) and not gemm.deterministic():
+        dgu = torch.empty_like(gu)
+        m = torch.empty(gu.shape[0], gu.shape[1] // 2, dtype=gu.dtype, device=gu.device) if want_m else None
+        if native().gemm8_swiglu_bwd(dy, wd, gu, dgu, m):
+            return dgu, m
+    dm = gemm.mm("nn", dy, wd).contiguous()
+    if want_m:
+        return native().swiglu_bwd_m(dm, gu.contiguous())
+    return native().swiglu_bwd(dm, gu, 0), None
+
+
+def gate_up_swiglu_down_ok(x: torch.Tensor, wgu: torch.Tensor, wd: torch.Tensor) -> bool:
+    return (_BWD_ON and gate_up_swiglu_ok(x, wgu) and wd.dim() == 2 and wd.dtype == torch.bfloat16
+            and 2 * wd.shape[1] == wgu.shape[0] and wd.shape[1] % 256 == 0 and wd.shape[0] % 64 == 0
+            and wd.stride(1) == 1)
+
+
+class _GateUpSwiGLUDownFn(torch.autograd.Function):
+    """y = swiglu(x Wgu^T) Wd^T: the gate-up GEMM with the SwiGLU epilogue, then the down GEMM;
+    backward: dgu from the down projection's dX GEMM epilogue, dWd from the saved m, then the
+    gate-up dX / dW GEMMs.  Weight gradients go the ``_LinearFn`` way."""
+
+    @staticmethod
+    def forward(ctx, x, wgu, wd, h, nw, eps):
+        x2 = _x2(x)
+        T, F2 = x2.shape[0], wgu.shape[0]
+        gu = torch.empty(T, F2, dtype=x.dtype, device=x.device)
+        m = torch.empty(T, F2 // 2, dtype=x.dtype, device=x.device)
+        if not native().gemm8_swiglu(x2, wgu, gu, m):
+            raise RuntimeError("gemm8_swiglu declined a shape gate_up_swiglu_down_ok accepted")
+        y = gemm.mm("tn", m, wd)
+        keep_x = h is None
+        ctx.save_for_backward(x2 if keep_x else h, wgu, wd, gu, m, nw)
+        ctx.wgp = wgu if wgu.is_leaf else None
+        ctx.wdp = wd if wd.is_leaf else None
+        ctx.dims = (x.shape, keep_x, eps)
+        return y.view(*x.shape[:-1], wd.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, wgu, wd, gu, m, nw = ctx.saved_tensors
+        xshape, keep_x, eps = ctx.dims
+        dy2 = dy.reshape(-1, wd.shape[0])
+        dgu, _ = swiglu_bwd_gemm(dy2, wd, gu)
+        del gu
+        dwd = param_weight_grad(ctx.wdp, dy2, m) if ctx.needs_input_grad[2] else None
+        del m
+        dx = gemm.mm("nn", dgu, wgu).view(xshape) if ctx.needs_input_grad[0] else None
+        dwgu = None
+        if ctx.needs_input_grad[1]:
+            x2 = xs if keep_x else _norm_input(xs, nw, eps)
+            dwgu = param_weight_grad(ctx.wgp, dgu, x2)
+        return dx, dwgu, dwd, None, None, None
+
+
+def gate_up_swiglu_down(x: torch.Tensor, wgu: torch.Tensor, wd: torch.Tensor,
+                        norm: tuple | None = None) -> torch.Tensor:
+    """The MLP body swiglu(x Wgu^T) Wd^T (callers check ``gate_up_swiglu_down_ok``); ``norm`` as in
+    ``gate_up_swiglu``."""
+    h, nw, eps = norm if norm is not None else (None, None, 0.0)
+    return _GateUpSwiGLUDownFn.apply(x, wgu, wd, h, nw, eps)

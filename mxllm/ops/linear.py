@@ -369,10 +369,11 @@ class _SwiGLULinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, w.shape[0])
         dgu = dw = None
         if use_native(g2):
-            # dm first: one pass over (dm, gu) then writes dgu AND the recomputed m for dW
-            dm = gemm.mm("nn", dy2, w)
-            dgu, m = native().swiglu_bwd_m(dm.contiguous(), g2.contiguous())
-            del dm
+            # dgu AND the recomputed m for dW from one pass over gu: the dX GEMM's SwiGLU-backward
+            # epilogue (mxllm/ops/fused.py), else dm first and one swiglu_bwd_m pass over (dm, gu)
+            from .fused import swiglu_bwd_gemm
+
+            dgu, m = swiglu_bwd_gemm(dy2, w, g2, want_m=True)
             if ctx.needs_input_grad[1]:
                 dw = param_weight_grad(ctx.wp, dy2, m)
             del m

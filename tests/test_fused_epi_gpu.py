@@ -1,6 +1,6 @@
-"""gemm8 fused forward epilogues (csrc/kernels/gemm8.hip G8_EPI_ROPE / G8_EPI_SWIGLU,
-mxllm/ops/fused.py) vs fp32 PyTorch references, vs the unfused kernels they replace, and
-through autograd inside the Llama layer."""
+"""gemm8 fused epilogues (csrc/kernels/gemm8.hip G8_EPI_ROPE / G8_EPI_SWIGLU forward,
+G8_EPI_SWIGLU_BWD backward; mxllm/ops/fused.py) vs fp32 PyTorch references, vs the unfused
+kernels they replace, and through autograd inside the Llama layer."""
 import math
 
 import pytest
@@ -78,6 +78,40 @@ def test_gemm8_swiglu_epilogue(gpu, T, F, K):
     assert torch.equal(m, _ops().swiglu_fwd(gu2, 0))
 
 
+@pytest.mark.parametrize("T,F,H,pad", [(256, 256, 512, 0), (512, 1024, 1024, 64), (4096, 14336, 4096, 0)])
+def test_gemm8_swiglu_bwd_epilogue(gpu, T, F, H, pad):
+    """dgu (and the recomputed m) from the down projection's dX GEMM epilogue: against fp32
+    autograd, and bitwise against the unfused gemm8 NN GEMM -> swiglu_bwd / swiglu_bwd_m."""
+    dy = _mat(T, H, gpu, 5)
+    wd = _mat(H, F, gpu, 6, scale=0.05, pad=pad)  # W_down [H, F] (row-strided when pad)
+    gu = _mat(T, 2 * F, gpu, 7, scale=2.0, pad=pad)
+    dgu = torch.empty(T, 2 * F, device=gpu, dtype=torch.bfloat16)
+    m = torch.empty(T, F, device=gpu, dtype=torch.bfloat16)
+    assert _ops().gemm8_swiglu_bwd(dy, wd, gu, dgu, m)
+    guf = gu.float().requires_grad_(True)
+    mr = torch.nn.functional.silu(guf[:, :F]) * guf[:, F:]
+    mr.backward(dy.float() @ wd.float())
+    assert _rel(dgu, guf.grad) < 1e-2
+    assert _rel(m, mr.detach()) < 1e-2
+    # the unfused path on the same GEMM kernel: bitwise
+    dm = torch.empty(T, F, device=gpu, dtype=torch.bfloat16)
+    assert _ops().gemm8(dy, True, wd, False, dm, 0.0, None, 1.0, 4)
+    assert torch.equal(dgu, _ops().swiglu_bwd(dm, gu.contiguous(), 0))
+    dgu2, m2 = _ops().swiglu_bwd_m(dm, gu.contiguous())
+    assert torch.equal(dgu, dgu2) and torch.equal(m, m2)
+    # without m: the same dgu
+    dgu3 = torch.zeros_like(dgu)
+    assert _ops().gemm8_swiglu_bwd(dy, wd, gu, dgu3)
+    assert torch.equal(dgu3, dgu)
+
+
+def test_gemm8_swiglu_bwd_declines_odd_shapes(gpu):
+    dy = _mat(200, 512, gpu, 1)  # T % 256 != 0
+    wd = _mat(512, 256, gpu, 2)
+    gu = _mat(200, 512, gpu, 3)
+    assert not _ops().gemm8_swiglu_bwd(dy, wd, gu, torch.empty_like(gu))
+
+
 def test_fused_layer_matches_unfused_autograd(gpu, monkeypatch):
     """A 2-layer full fine-tune model (head dim 128): loss and every parameter gradient equal
     between the fused-epilogue forward and the unfused ops (the same GEMM kernel underneath)."""
@@ -92,7 +126,7 @@ def test_fused_layer_matches_unfused_autograd(gpu, monkeypatch):
     for on in (True, False):
         monkeypatch.setattr(fused, "_ON", on)
         calls = []
-        for name in ("qkv_attention", "gate_up_swiglu"):
+        for name in ("qkv_attention", "gate_up_swiglu_down"):
             real = getattr(fused, name)
             monkeypatch.setattr(fused, name, lambda *a, _r=real, _n=name, **k: (calls.append(_n), _r(*a, **k))[1])
         model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3)
@@ -106,3 +140,29 @@ def test_fused_layer_matches_unfused_autograd(gpu, monkeypatch):
     assert abs(l1 - l0) < 1e-3 * abs(l0)
     for n in g0:
         assert _rel(g1[n], g0[n]) < 2e-2, n
+
+
+def test_fused_mlp_backward_matches_two_step(gpu, monkeypatch):
+    """The gate-up + SwiGLU + down MLP with the SwiGLU backward in the dm GEMM's epilogue gives
+    bitwise the loss and gradients of the two-step backward (dm GEMM -> swiglu_bwd) on gemm8."""
+    from mxllm.models import Llama, get_config
+    from mxllm.ops import fused
+
+    monkeypatch.setenv("MXLLM_GEMM8", "all")
+    cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(fused, "_BWD_ON", on)
+        calls = []
+        real = fused.swiglu_bwd_gemm
+        monkeypatch.setattr(fused, "swiglu_bwd_gemm", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+        model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3)
+        loss = model(ids, ids)
+        loss.backward()
+        res[on] = (float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+        assert (len(calls) == 2) == on, calls
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert l1 == l0
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
