@@ -45,6 +45,8 @@ def main():
         res["bwd_partials_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, True, sc, 2))
         res["bwd_noatomic_ms"] = timeit(lambda: ops.attn_bwd_ablate(do, q, k, v, o, lse, -1, sc))
         res["bwd_noatomic_TF"] = 2.5 * fl / res["bwd_noatomic_ms"] / 1e9
+    cs = torch.rand(S, D // 2, device=dev)
+    res["bwd_rope_ms"] = timeit(lambda: ops.attn_bwd_rope(do, q, k, v, o, lse, True, sc, cs, cs, 0))  # into d(qkv)
     res["fwd_TF"] = fl / res["fwd_ms"] / 1e9
     res["bwd_TF"] = 2.5 * fl / res["bwd_ms"] / 1e9
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)

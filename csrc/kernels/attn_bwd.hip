@@ -1312,7 +1312,7 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ dST, const uint16_t* __restrict_
   // an fp32 dQ that kernel re-reads (70B training shape: 134 MB written + 134 MB read per layer
   // become 67 MB written).  The rotate-half partner of column d is d +- 64, held by wave wl ^ 2 of
   // the sub-block: the tile goes through LDS ([sub][64 rows][128] fp32, the freed stage buffers).
-  if constexpr (D == 128 && QB == 4) {
+  if constexpr (D == 128) {
     if (dqkv != nullptr) {
       static_assert(QB * BQ * D * 4 <= NSTAGE * BUF, "dQ exchange tile fits the stage buffers");
       lds_wait();
@@ -1542,7 +1542,12 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
 #undef RED
   } else if (dq_mode == 3) {
     // 128 q rows per workgroup (every K tile feeds two 64-row sub-blocks); D=32 keeps 64
-    const int qbs = D == 128 ? 4 : (D == 64 ? 2 : 1);
+    // MXLLM_ATTN_DQ_QB=2 (experiment): D = 128 with 128 q rows per workgroup and a 4-deep ring
+    static const int qb128 = [] {
+      const char* e = getenv("MXLLM_ATTN_DQ_QB");
+      return e && e[0] == '2' ? 2 : 4;
+    }();
+    const int qbs = D == 128 ? qb128 : (D == 64 ? 2 : 1);
     const int qgrid = ((S + 64 * qbs - 1) / (64 * qbs)) * B * Hq;
     const uint16_t* dst = reinterpret_cast<const uint16_t*>(work);
 #define DQK(DD)                                                                                                   \
@@ -1555,7 +1560,14 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
       attn_bwd_dq_kernel<DD, false, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, \
                                                                         nkb * 128, scale, dqkv, ldq, cosb, sinb); \
   } while (0)
-    if (D == 128) DQK(128);
+    if (D == 128 && qbs == 2) {
+      if (causal)
+        attn_bwd_dq_kernel<128, true, 2><<<qgrid, 512, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, nkb * 128,
+                                                                   scale, dqkv, ldq, cosb, sinb);
+      else
+        attn_bwd_dq_kernel<128, false, 2><<<qgrid, 512, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,
+                                                                    nkb * 128, scale, dqkv, ldq, cosb, sinb);
+    } else if (D == 128) DQK(128);
     else if (D == 64) DQK(64);
     else DQK(32);
 #undef DQK
