@@ -237,17 +237,22 @@ __device__ __forceinline__ void g8_epilogue_fused(f32x4 (&acc)[8][4], float alph
     const int F = N;
     const int cb = 256 * pn + 64 * wc + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5);  // + 32 jp
 #pragma unroll
-    for (int qa = 0; qa < 2; ++qa)
+    for (int qa = 0; qa < 2; ++qa) {
+      // all 16 gu loads of this half first (64 VGPRs): one memory round trip per half, not per row
+      u16x8 g8[4][2], u8v[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint16_t* gr = ep.gu + (int64_t)(ml + qa * 64 + 16 * i) * ep.ldg;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          g8[i][jp] = *reinterpret_cast<const u16x8*>(gr + cb + 32 * jp);
+          u8v[i][jp] = *reinterpret_cast<const u16x8*>(gr + F + cb + 32 * jp);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t m = ml + qa * 64 + 16 * i;
-        const uint16_t* gr = ep.gu + m * ep.ldg;
-        u16x8 g8[2], u8v[2], d8[2];
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          g8[jp] = *reinterpret_cast<const u16x8*>(gr + cb + 32 * jp);
-          u8v[jp] = *reinterpret_cast<const u16x8*>(gr + F + cb + 32 * jp);
-        }
+        u16x8 d8[2];
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {  // dm rounded to bf16 and swapped exactly as the plain store
           const f32x4 va = acc[4 * qa + i][2 * jp] * alpha, vb = acc[4 * qa + i][2 * jp + 1] * alpha;
@@ -265,21 +270,28 @@ __device__ __forceinline__ void g8_epilogue_fused(f32x4 (&acc)[8][4], float alph
         uint16_t* dr = reinterpret_cast<uint16_t*>(C) + m * ldc;
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
-          u16x8 og, ou, om;
+          u16x8 og, ou;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float gf = bf2f(g8[jp][j]), uf = bf2f(u8v[jp][j]);
             float dg, du;
-            swiglu_grad(bf2f(d8[jp][j]), gf, uf, dg, du);
+            swiglu_grad(bf2f(d8[jp][j]), bf2f(g8[i][jp][j]), bf2f(u8v[i][jp][j]), dg, du);
             og[j] = f2bf(dg);
             ou[j] = f2bf(du);
-            om[j] = f2bf(gf * __builtin_amdgcn_rcpf(1.f + __expf(-gf)) * uf);
           }
           *reinterpret_cast<u16x8*>(dr + cb + 32 * jp) = og;
           *reinterpret_cast<u16x8*>(dr + F + cb + 32 * jp) = ou;
-          if (ep.m) *reinterpret_cast<u16x8*>(ep.m + m * ep.ldm + cb + 32 * jp) = om;
+          if (ep.m) {
+            u16x8 om;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float gf = bf2f(g8[i][jp][j]);
+              om[j] = f2bf(gf * __builtin_amdgcn_rcpf(1.f + __expf(-gf)) * bf2f(u8v[i][jp][j]));
+            }
+            *reinterpret_cast<u16x8*>(ep.m + m * ep.ldm + cb + 32 * jp) = om;
+          }
         }
       }
+    }
   } else {  // G8_EPI_SWIGLU
     const int F = N / 2;
     const int col = 128 * pn + 32 * wc + u8;  // gate column (up: + F; m: the same column)
