@@ -99,6 +99,10 @@ def parse(argv=None):
     ap.add_argument("--config3", choices=["auto", "on", "off"], default="auto",
                     help="also measure BASELINE config 3 (Llama-3.1-8B FULL fine-tune, DDP over all N GPUs) "
                          "in-process after the headline; auto = when the headline runs on 8 GPUs")
+    ap.add_argument("--config3-zero1", choices=["auto", "on", "off"], default="auto",
+                    help="with config 3: ALSO measure it with the optimizer sharded (ZeRO-1: reduce-scatter, "
+                         "AdamW on 1/N of the state, all-gather), after config 4 and only if the time budget "
+                         "is left; auto = on GPUs")
     ap.add_argument("--config3-timeout", type=float, default=300.0,
                     help="hard limit for the config-3 child job; the headline line is printed either way")
     ap.add_argument("--config2-mb4", choices=["auto", "on", "off"], default="auto",
@@ -255,6 +259,9 @@ def main(argv=None):
         children.append(("config3", f"config3_8b_full_dp{env.world_size}"))
     if c4:
         children.append(("config4", "config4_full_zero3"))
+    if c3 and env.world_size > 1 and (a.config3_zero1 == "on" or (a.config3_zero1 == "auto" and cuda)):
+        # the same DDP fine-tune with the optimizer sharded: last, so it never costs config 4 its budget
+        children.append(("config3z", f"config3_8b_full_dp{env.world_size}_zero1"))
     try:
         if cuda and a.calibrate:
             # box speed next to the number: fixed GEMM + copy after the timed steps
@@ -301,7 +308,7 @@ def main(argv=None):
                 if kind == "config4":
                     out[key] = run_config4_planned(a, env.world_size, free_gb)
                 else:
-                    out[key] = run_config3(a, env.world_size)
+                    out[key] = run_config3(a, env.world_size, "zero1" if kind == "config3z" else "ddp")
             except Exception as e:  # noqa: BLE001  the headline (and later phases) survive any phase error
                 out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
         out["child_phases"]["elapsed_s"] = round(time.time() - _T0, 1)
@@ -483,16 +490,20 @@ def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "") 
     return res
 
 
-def run_config3(a, world: int) -> dict:
-    """BASELINE config 3: Llama-3.1-8B FULL fine-tune, plain DDP over ``world`` GPUs, as a
-    fresh child job after the headline."""
-    argv = ["--model", a.full_model, "--finetune", "full", "--parallel", "ddp", "--micro-batch",
+def run_config3(a, world: int, parallel: str = "ddp") -> dict:
+    """BASELINE config 3: Llama-3.1-8B FULL fine-tune, DDP over ``world`` GPUs, as a fresh child
+    job after the headline.  ``parallel`` = "zero1": the same data-parallel step with the
+    optimizer sharded (mxllm/parallel/zero1.py: the buckets are reduce-scattered, each rank runs
+    AdamW over its 1/N of the fp32 state, the bf16 parameters are all-gathered back under the
+    next forward) -- the same link bytes as the all-reduce, 1/N of the ~38 ms AdamW per rank."""
+    argv = ["--model", a.full_model, "--finetune", "full", "--parallel", parallel, "--micro-batch",
             str(a.micro_batch), "--seq-len", str(a.seq_len), "--steps", str(a.full_steps), "--warmup",
             str(a.full_warmup)]
-    res = _run_child(a, world, argv, a.config3_timeout, tag="config3")
+    res = _run_child(a, world, argv, a.config3_timeout, tag="config3" if parallel == "ddp" else "config3z")
     name = PRETTY.get(a.full_model, a.full_model)
-    res["metric"] = f"fine-tune tokens/sec (whole node) {name} FULL-parameter DDP"
-    res["label"] = (f"BASELINE config 3: {name} full-parameter fine-tune, DDP over {world} GPUs, "
+    how = "DDP" if parallel == "ddp" else "DDP with a ZeRO-1 sharded optimizer"
+    res["metric"] = f"fine-tune tokens/sec (whole node) {name} FULL-parameter {how}"
+    res["label"] = (f"BASELINE config 3: {name} full-parameter fine-tune, {how} over {world} GPUs, "
                     f"measured after the headline in a separate job")
     return res
 

@@ -22,7 +22,9 @@ fp32 state (8B at N=8: 12 GB instead of 96 GB per GPU).
     the model waits per layer (``Llama.param_wait`` hook) — the next forward
     starts as soon as its first layer's parameters have arrived;
   * the full flat grad buffer is cleared bucket by bucket once its
-    reduce-scatter has completed (the dW GEMMs accumulate into it, beta = 1).
+    reduce-scatter has completed (the dW GEMMs accumulate into it, beta = 1) --
+    unless the trainer's gradients are "fresh" (every gradient op overwrites its
+    slot on the step's first micro-batch: nothing to clear).
 Reference: the reference claims DDP fine-tuning (README.md:7) and has none.
 """
 from __future__ import annotations
@@ -63,6 +65,10 @@ class Zero1(DDP):
                 self.pshard[cs:cs + n].copy_(flat.params[own:own + n])
         self.master = self.pshard.float() if flat.params.dtype != torch.float32 else self.pshard
         self._ag_work: list = [None] * len(self.buckets)
+        # clear each bucket of the full gradient buffer once its reduce-scatter is done (the dW GEMMs
+        # accumulate into it); False when every gradient op overwrites its slot on the step's first
+        # micro-batch (the trainer's "fresh" gradients)
+        self.clear_grads = True
         self._launched: set[int] = set()  # bucket indices reduce-scattered this step
         self._param_slot_bucket = {id(p): bi for p, bi in zip(flat.param_list, self._param_bucket)}
         log.info("ZeRO-1: %d buckets, optimizer shard %.1f M of %.1f M elements (world %d)", len(self.buckets),
@@ -82,7 +88,8 @@ class Zero1(DDP):
         else:
             out.copy_(g)
             b.work = None
-            g.zero_()
+            if self.clear_grads:
+                g.zero_()
 
     def finish(self) -> float:
         """Wait for every bucket's reduce-scatter, clear the full grad buffer
@@ -97,7 +104,8 @@ class Zero1(DDP):
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
-                self.flat.grads[b.start:b.end].zero_()  # dW GEMMs accumulate (beta 1) next step
+                if self.clear_grads:
+                    self.flat.grads[b.start:b.end].zero_()  # dW GEMMs accumulate (beta 1) next step
             b.work = None
             b.pending = b.expected
             b.seen.clear()

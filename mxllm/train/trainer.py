@@ -139,12 +139,15 @@ class Trainer:
         # "fresh" gradients: every gradient of the step is formed by an op that can
         # OVERWRITE its flat slot (dW GEMMs with beta 0, the RMSNorm / embedding
         # kernels' accum_grad), so AdamW need not zero the gradient buffer behind
-        # itself (2-4 B/param less HBM traffic per step).  GPU kernels only; not
-        # with LoRA (its kernels accumulate), ZeRO-1 (buckets are cleared after the
-        # reduce-scatter) or parameters used twice (tied embeddings: autograd sums)
+        # itself (2-4 B/param less HBM traffic per step); under ZeRO-1 the full
+        # gradient buffer is then not cleared behind each reduce-scatter either (8B:
+        # a 16 GB memset per step).  GPU kernels only; not with LoRA (its kernels
+        # accumulate) or parameters used twice (tied embeddings: autograd sums)
         self.fresh_grads = (os.environ.get("MXLLM_FRESH_GRADS", "1") != "0" and self.flat.device.type == "cuda"
-                            and self.zero1 is None and not getattr(model, "lora", False)
+                            and not getattr(model, "lora", False)
                             and not any(getattr(p, "_mx_no_direct", False) for p in self.flat.param_list))
+        if self.zero1 is not None:
+            self.zero1.clear_grads = not self.fresh_grads
         if self.fresh_grads:
             # enforce the invariant: a gradient that reaches a parameter through
             # autograd's AccumulateGrad (not an op honouring _mx_grad_fresh) would be ADDED onto

@@ -62,6 +62,23 @@ def test_config4_phase_in_same_line():
     assert j["config"]["parallelism"] == "dp2"  # the headline itself is unchanged
 
 
+def test_config3_zero1_variant_in_same_line():
+    """Config 3 runs as plain DDP and, after it, as the same step with the optimizer sharded
+    (ZeRO-1); both child results land in the one line."""
+    r = _bench("--gpus", "2", "--config3", "on", "--config3-zero1", "on", "--full-model", "tiny", "--full-steps", "1",
+               "--full-warmup", "1", "--config4", "off")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    c3, c3z = j["config3_8b_full_dp2"], j["config3_8b_full_dp2_zero1"]
+    for c in (c3, c3z):
+        assert "error" not in c and "skipped" not in c, c
+        assert c["n_gpus"] == 2 and c["value"] > 0 and "config 3" in c["label"]
+    assert "zero1" not in c3["config"]["parallelism"] and "zero1" in c3z["config"]["parallelism"]
+    assert "ZeRO-1" in c3z["label"]
+
+
 def test_zero3_emulation_is_labelled():
     r = _bench("--finetune", "full", "--parallel", "zero3", "--act-ckpt", "--emulate-world", "4")
     assert r.returncode == 0, r.stderr[-3000:]

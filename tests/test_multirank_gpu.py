@@ -178,7 +178,7 @@ def _batches(cfg, world, steps, per_rank, seq):
 
 
 def _trainer_worker(rank, world, port, q, mode, ref_world):
-    """``mode``: ddp | zero3.  ``world`` ranks train on the same global batches; at world 1
+    """``mode``: ddp | zero1 | zero3.  ``world`` ranks train on the same global batches; at world 1
     the ``ref_world`` ranks' micro-batches become gradient-accumulation micro-batches."""
     if world > 1:
         _peer_env(port)
@@ -194,10 +194,11 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
         cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
         opt = OptimConfig(lr=1e-3, grad_clip=1.0, weight_decay=0.01)
         seq = 128
-        if mode == "ddp":
+        if mode in ("ddp", "zero1"):
             model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=1234)
-            tr = Trainer(model, env, opt)
-            out["overlap"] = tr.overlap_optimizer
+            tr = Trainer(model, env, opt, shard_optimizer=mode == "zero1")
+            # ZeRO-1: sharded AdamW, then the all-gathers the next forward waits on per layer
+            out["overlap"] = tr.overlap_optimizer if mode == "ddp" else (tr.zero1 is not None) == (world > 1)
             out["comm"] = getattr(tr.ddp.comm, "kind", None)
             per_rank = 2
         else:
@@ -212,17 +213,17 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
         losses = []
         for s in range(STEPS):
             ranks = range(ref_world) if world == 1 else [rank]
-            if mode == "ddp":
+            if mode != "zero3":
                 mbs = [(data[s][r].to(dev), data[s][r].to(dev)) for r in ranks]
             else:
                 mbs = [(data[s][r][i:i + 1].to(dev), data[s][r][i:i + 1].to(dev)) for r in ranks for i in range(2)]
             losses.append(tr.train_step(mbs))
         losses = [float(x) for x in losses]
-        if mode == "ddp":
+        if mode != "zero3":
             tr.params_ready()
             out["in_sync"] = check_in_sync([tr.flat.params], raise_on_mismatch=False)
-            master = {s.name: tr.flat.master[s.offset:s.offset + s.numel].float().view(s.shape).cpu()
-                      for s in tr.flat.slots}
+            full = tr.zero1.full_master() if tr.zero1 is not None else tr.flat.master.float()
+            master = {s.name: full[s.offset:s.offset + s.numel].float().view(s.shape).cpu() for s in tr.flat.slots}
         else:
             tr.params_ready()
             out["in_sync"] = check_in_sync([tr.units[0].shard], raise_on_mismatch=False)  # replicated norms
@@ -241,7 +242,7 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode", ["ddp", "zero3"])
+@pytest.mark.parametrize("mode", ["ddp", "zero1", "zero3"])
 def test_trainers_multirank_on_shared_gpu_match_world1(gpu, mode):
     ref = None
     for world in (2, 4):
