@@ -74,7 +74,10 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
 // step (mxllm/models/llama.py, FusedLinear).  desc[i] = {src, dst, rows, cols,
 // src_ld, dst_ld, first_block, src_col_stride, dst_col_stride} (column strides != 1
 // give transposed copies, e.g. B -> the B^T image of the LoRA backward kernel); block b belongs to the descriptor with the
-// largest first_block <= b (binary search), each block copies 4096 elements.
+// largest first_block <= b (binary search), each block copies 4096 elements -- or, for a TRANSPOSING
+// descriptor (source rows contiguous, destination a column-major view: dst_ld == 1, dst_col_stride
+// != 1), one 64 x 64 tile of the source (row-major tile order) through LDS, so both the reads and
+// the writes are row-contiguous (mxllm/ops/linear.py copy2d_plan sizes the blocks the same way).
 constexpr int kCopyBlockElems = 4096;
 
 __global__ void __launch_bounds__(256) copy2d_batched_kernel(const int64_t* __restrict__ desc, int n) {
@@ -89,6 +92,21 @@ __global__ void __launch_bounds__(256) copy2d_batched_kernel(const int64_t* __re
   const uint16_t* src = reinterpret_cast<const uint16_t*>(d[0]);
   uint16_t* dst = reinterpret_cast<uint16_t*>(d[1]);
   const int64_t rows = d[2], cols = d[3], sld = d[4], dld = d[5], scs = d[7], dcs = d[8];
+  if (scs == 1 && dld == 1 && dcs != 1) {
+    // element (r, c) -> dst[c * dcs + r]: source rows in, destination rows (= source columns) out
+    __shared__ uint16_t tile[64][66];
+    const int64_t tcols = (cols + 63) / 64, t = b - d[6];
+    const int64_t r0 = (t / tcols) * 64, c0 = (t % tcols) * 64;
+    const int tr = threadIdx.x >> 6, tl = threadIdx.x & 63;
+#pragma unroll 4
+    for (int rr = tr; rr < 64; rr += 4)
+      if (r0 + rr < rows && c0 + tl < cols) tile[rr][tl] = src[(r0 + rr) * sld + c0 + tl];
+    __syncthreads();
+#pragma unroll 4
+    for (int cc = tr; cc < 64; cc += 4)
+      if (c0 + cc < cols && r0 + tl < rows) dst[(c0 + cc) * dcs + r0 + tl] = tile[tl][cc];
+    return;
+  }
   const int64_t e0 = (b - d[6]) * kCopyBlockElems;
   const int64_t total = rows * cols;
   const int64_t e1 = min(total, e0 + kCopyBlockElems);

@@ -387,13 +387,9 @@ class Llama(nn.Module):
             return
         key = tuple((s.data_ptr(), d.data_ptr()) for s, d in pairs)
         if getattr(self, "_adapter_desc_key", None) != key:
-            rows, total = [], 0
-            for s, d in pairs:
-                assert s.shape == d.shape and s.element_size() == 2 and d.element_size() == 2
-                n = s.shape[0] * s.shape[1]
-                rows.append([s.data_ptr(), d.data_ptr(), s.shape[0], s.shape[1], s.stride(0), d.stride(0), total,
-                             s.stride(1), d.stride(1)])
-                total += (n + 4095) // 4096
+            from ..ops.linear import copy2d_plan
+
+            rows, total = copy2d_plan(pairs)
             self._adapter_desc = torch.tensor(rows, dtype=torch.int64, device=pairs[0][0].device)
             self._adapter_blocks = total
             self._adapter_desc_key = key

@@ -245,6 +245,23 @@ def transpose2d(t: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Ten
     return out if scale is None else (out * scale.to(out.dtype))
 
 
+def copy2d_plan(pairs) -> tuple[list[list[int]], int]:
+    """Descriptor rows and the block count of ONE ``copy2d_batched`` launch over ``pairs`` of 2-D
+    16-bit (src, dst) views of equal shape (csrc/kernels/misc.hip): 4,096 elements per block, or
+    one 64 x 64 source tile per block where the copy transposes (source rows contiguous, the
+    destination a column-major view)."""
+    rows, total = [], 0
+    for s, d in pairs:
+        assert s.shape == d.shape and s.dim() == 2 and s.element_size() == 2 and d.element_size() == 2
+        r, c = s.shape
+        rows.append([s.data_ptr(), d.data_ptr(), r, c, s.stride(0), d.stride(0), total, s.stride(1), d.stride(1)])
+        if s.stride(1) == 1 and d.stride(0) == 1 and d.stride(1) != 1:
+            total += ((r + 63) // 64) * ((c + 63) // 64)
+        else:
+            total += (r * c + 4095) // 4096
+    return rows, total
+
+
 _DW_TN = os.environ.get("MXLLM_DW_TN", "1") != "0"
 
 

@@ -1,6 +1,7 @@
 """Batched strided 2-D copy (csrc/kernels/misc.hip ``copy2d_batched``: every LoRA adapter into its
 augmented GEMM buffer in one launch) against torch's copy, on both of its paths: 16-B units for
-contiguous, 8-element-multiple rows on aligned bases, and the element-wise fallback."""
+contiguous, 8-element-multiple rows on aligned bases, 64 x 64 LDS tiles for transposing copies
+(column-major destination views), and the element-wise fallback."""
 import pytest
 import torch
 
@@ -8,12 +9,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _desc(pairs):
-    rows, total = [], 0
-    for s, d in pairs:
-        n = s.shape[0] * s.shape[1]
-        rows.append([s.data_ptr(), d.data_ptr(), s.shape[0], s.shape[1], s.stride(0), d.stride(0), total,
-                     s.stride(1), d.stride(1)])
-        total += (n + 4095) // 4096
+    from mxllm.ops.linear import copy2d_plan
+
+    rows, total = copy2d_plan(pairs)
     return torch.tensor(rows, dtype=torch.int64, device=pairs[0][0].device), total
 
 
@@ -31,8 +29,17 @@ def test_copy2d_batched_matches_torch(gpu):
     t_dst = torch.zeros(40, 24, dtype=torch.bfloat16, device=dev)
     off_dst = torch.zeros(8 * 1000 + 1, dtype=torch.bfloat16, device=dev)[1:].view(1000, 8)  # 2-B offset base
     off_src = torch.randn(1000, 8, device=dev).to(torch.bfloat16)
+    # transposing copies (the B^T / A images): a column-major destination view, 64 x 64 LDS tiles,
+    # ragged edges on both axes
+    bt = torch.zeros(48, 10240 + 64, dtype=torch.bfloat16, device=dev)
+    tr_src = torch.randn(10240, 48, device=dev).to(torch.bfloat16)
+    wxt = torch.zeros(8192, 8192 + 40, dtype=torch.bfloat16, device=dev)
+    tr_src2 = torch.randn(16, 8192, device=dev).to(torch.bfloat16)
+    rag_dst = torch.zeros(50, 100, dtype=torch.bfloat16, device=dev)
+    rag_src = torch.randn(70, 37, device=dev).to(torch.bfloat16)
     pairs = [(a, big[10240:10288, :8192]), (bmat, big[:10240, 8192:8208]), (odd_src, odd_dst[5:42, 3:16]),
-             (t_src, t_dst), (off_src, off_dst)]
+             (t_src, t_dst), (off_src, off_dst), (tr_src, bt[:, :10240].t()), (tr_src2, wxt[:, 8192:8208].t()),
+             (rag_src, rag_dst[3:40, 10:80].t())]
     want = [d.clone() for _, d in pairs]
     for (s, _), w in zip(pairs, want):
         w.copy_(s)
@@ -44,3 +51,6 @@ def test_copy2d_batched_matches_torch(gpu):
     # nothing outside the destination windows was written
     assert torch.count_nonzero(big[:10240, :8192]) == 0 and torch.count_nonzero(big[:, 8208:]) == 0
     assert torch.count_nonzero(odd_dst[:5]) == 0 and torch.count_nonzero(odd_dst[:, 16:]) == 0
+    assert torch.count_nonzero(bt[:, 10240:]) == 0 and torch.count_nonzero(wxt[:, :8192]) == 0
+    assert torch.count_nonzero(wxt[:, 8208:]) == 0
+    assert int(torch.count_nonzero(rag_dst)) == int(torch.count_nonzero(rag_src))
