@@ -195,6 +195,37 @@ bool gemm8(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::T
   return true;
 }
 
+// out[M, N] (bf16, beta 0) = alpha op(a) op(b) that also writes one fp32 sum of squares of the stored
+// values per 256 x 256 output tile into sq (>= (M / 256) * (N / 256) elements, row-major tile order):
+// the gradient-clip norm's partials straight from the weight-gradient GEMMs.  False: nothing launched.
+bool gemm8_sq(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::Tensor& out, at::Tensor& sq,
+              const c10::optional<at::Tensor>& alpha_t, double alpha_f) {
+  MX_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && sq.is_cuda(), "gemm8_sq: GPU tensors");
+  MX_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+               out.scalar_type() == at::kBFloat16 && sq.scalar_type() == at::kFloat,
+           "gemm8_sq: bf16 operands and output, f32 partials");
+  MX_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm8_sq: 2-D operands");
+  const int64_t M = a_kc ? a.size(0) : a.size(1), K = a_kc ? a.size(1) : a.size(0);
+  const int64_t N = b_kc ? b.size(0) : b.size(1), Kb = b_kc ? b.size(1) : b.size(0);
+  MX_CHECK(K == Kb && out.size(0) == M && out.size(1) == N, "gemm8_sq: shape mismatch");
+  if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1 || !sq.is_contiguous()) return false;
+  if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX || M % 256 || N % 256) return false;
+  MX_CHECK(sq.numel() >= (M / 256) * (N / 256), "gemm8_sq: partials buffer too small");
+  const float* sc = nullptr;
+  if (alpha_t.has_value()) {
+    MX_CHECK(alpha_t->scalar_type() == at::kFloat && alpha_t->numel() == 1 && alpha_t->device() == a.device(),
+             "gemm8_sq alpha_t: f32 scalar on the device");
+    sc = alpha_t->data_ptr<float>();
+  }
+  DevGuard g(a.device());
+  const int rc = mx_gemm8_sq(bf(a), a.stride(0), a_kc ? 1 : 0, bf(b), b.stride(0), b_kc ? 1 : 0, bfm(out),
+                             out.stride(0), (int)M, (int)N, (int)K, sc, (float)alpha_f, sq.data_ptr<float>(),
+                             cur_stream());
+  if (rc == -1) return false;
+  MX_OK(rc);
+  return true;
+}
+
 // out[M, N] (bf16) = op(a) op(b) with the tail-balanced launch (mx_gemm8_tail): the output split at
 // `at` columns (rows when `rows`) -- whole waves of tiles before it, half-K workgroups summed through
 // an fp32 workspace after it.  Returns false (nothing launched) for shapes it does not take.
@@ -1203,6 +1234,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4) -> bool");
   m.def("gemm8_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, Tensor(a!) q, Tensor(b!) k, Tensor(c!) v) -> bool");
   m.def("gemm8_swiglu(Tensor x, Tensor w, Tensor(a!) gu, Tensor(b!) m) -> bool");
+  m.def("gemm8_sq(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, Tensor(b!) sq, Tensor? alpha_t=None, float alpha=1.0) -> bool");
   m.def("gemm8_swiglu_bwd(Tensor dy, Tensor w, Tensor gu, Tensor(a!) dgu, Tensor(b!)? m=None) -> bool");
   m.def("sqnorm(Tensor x) -> Tensor");
   m.def("swiglu_fwd(Tensor gu, int out_pad=0) -> Tensor");
@@ -1253,6 +1285,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("gemm8_tail", &gemm8_tail);
   m.impl("gemm8_rope", &gemm8_rope);
   m.impl("gemm8_swiglu", &gemm8_swiglu);
+  m.impl("gemm8_sq", &gemm8_sq);
   m.impl("gemm8_swiglu_bwd", &gemm8_swiglu_bwd);
   m.impl("ce_inv_count", &ce_inv_count);
   m.impl("ce_chunk", &ce_chunk);

@@ -100,6 +100,7 @@ struct G8Epi {
   int F;
   const uint16_t* gu; // SWIGLU_BWD: the forward's [T, 2F] with row stride ldg
   int64_t ldg;
+  float* sq;          // plain bf16 beta-0 output: per-tile sum of squares of the stored values
 };
 
 // weight row feeding virtual tile column v (0..255) of output tile pn (G8_EPI_SWIGLU: absolute row)
@@ -166,6 +167,17 @@ __device__ __forceinline__ void g8_stamp(int wg, int row, int k, unsigned long l
 __device__ __forceinline__ void g8_stamp(int, int, int, unsigned long long) {}
 #endif
 
+// sum of squares of the 8 bf16 values packed in `o` (what the plain epilogue stored), added to s
+__device__ __forceinline__ float g8_sq8(const uint4& o, float s) {
+  const uint32_t v[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
+    s = __builtin_fmaf(lo, lo, s);
+    s = __builtin_fmaf(hi, hi, s);
+  }
+  return s;
+}
 __device__ __forceinline__ float g8_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float g8_rbf(float x) { return bf2f(f2bf(x)); }  // round through bf16
 
@@ -635,6 +647,7 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
 
   // ---- epilogue: lane holds C[m][n .. n+3] per block
   const float alpha = alpha_f * (alpha_t ? alpha_t[0] : 1.f);
+  float sqs = 0.f;  // ep.sq: this lane's sum of squares of the bf16 values it stores
   const int ml = m0 + wr * 128 + (lane & 15);
   const int nl = n0 + wc * 64 + 4 * (lane >> 4);
   if constexpr (EPI != G8_EPI_NONE) {
@@ -696,7 +709,23 @@ gemm8_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __rest
           o.z = s0[1];
           o.w = s1[1];
           *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(C) + m * ldc + n) = o;
+          if (!BETA && ep.sq) sqs = g8_sq8(o, sqs);
         }
+    }
+  }
+  if constexpr (!OUT_F32 && !BETA) {
+    if (ep.sq) {  // workgroup-uniform: one fixed-order partial per output tile (deterministic)
+      sqs = wave_sum(sqs);
+      __syncthreads();  // every wave is past the K loop's LDS reads (its DMA drained at the last tile)
+      float* red = reinterpret_cast<float*>(smem);
+      if (lane == 0) red[w] = sqs;
+      __syncthreads();
+      if (tid == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t += red[i];
+        ep.sq[pm * nN + pn] = t;
+      }
     }
   }
   if constexpr (ST) {
@@ -1180,6 +1209,37 @@ extern "C" int mx_gemm8_epi(const uint16_t* A, int64_t lda, const uint16_t* B, i
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+// Plain bf16, beta-0 gemm8 (any operand order, 4-phase schedule) that also writes one sum of squares
+// of the stored bf16 values per 256 x 256 output tile into sq[(m / 256) * (N / 256) + n / 256]: the
+// weight-gradient GEMMs hand the gradient-clip norm its partials (mxllm/train/trainer.py), so no
+// pass re-reads the gradient for it.  Returns -1 (nothing launched) where mx_gemm8 would.
+extern "C" int mx_gemm8_sq(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc,
+                           uint16_t* C, int64_t ldc, int M, int N, int K, const float* alpha_t, float alpha_f,
+                           float* sq, hipStream_t stream) {
+  if (!sq || M <= 0 || N <= 0 || K <= 0 || (M & 255) || (N & 255)) return -1;
+  if ((a_kc || b_kc) && (K % G8_BK)) return -1;
+  if (lda % 8 || ldb % 8 || ldc % 8 || ((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)C & 15)) return -1;
+  if (a_kc ? lda < K : lda < M) return -1;
+  if (b_kc ? ldb < K : ldb < N) return -1;
+  if (ldc < N) return -1;
+  const int64_t kpad = (int64_t)((K + G8_BK - 1) / G8_BK) * G8_BK;
+  const int64_t aspan = a_kc ? 256 * lda : kpad * lda;
+  const int64_t bspan = b_kc ? 256 * ldb : kpad * ldb;
+  if (aspan * 2 >= ((int64_t)1 << 31) || bspan * 2 >= ((int64_t)1 << 31)) return -1;
+  const int grid = (M >> 8) * (N >> 8);
+  G8Epi ep{};
+  ep.sq = sq;
+#define G8_SQ(AK, BK_)                                                                                           \
+  gemm8_kernel<AK, BK_, false, false, 0, 4><<<grid, 512, 0, stream>>>(A, lda, B, ldb, C, ldc, M, N, K, alpha_t, \
+                                                                     alpha_f, 0, 0, ep)
+  if (a_kc && b_kc) G8_SQ(true, true);
+  else if (a_kc) G8_SQ(true, false);
+  else if (b_kc) G8_SQ(false, true);
+  else G8_SQ(false, false);
+#undef G8_SQ
   return (int)hipGetLastError();
 }
 

@@ -166,3 +166,18 @@ def mm(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = N
     if a.is_cuda:  # bf16 operands, fp32 output (hipBLASLt D = C in fp32)
         return torch.ops.aten.addmm.dtype_out(out, A, B, odt, beta=beta, out=out)
     return out.mul_(beta).add_(A.float() @ B.float()) if beta != 0.0 else out.copy_(A.float() @ B.float())
+
+
+def mm_sq(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, sq: torch.Tensor,
+          alpha_t: torch.Tensor | None = None) -> bool:
+    """``out = alpha_t * op(a) op(b)`` (bf16, beta 0) on gemm8 that also writes one fp32 sum of squares of
+    the stored values per 256 x 256 output tile into ``sq`` (row-major tile order).  Only where the
+    dispatch puts this shape on the plain 4-phase gemm8 anyway (same kernel, same bits in ``out``);
+    False: nothing launched, the caller takes ``mm``."""
+    M, N, K = _dims(form, a, b)
+    if not (use_native(a) and a.dtype == b.dtype == out.dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0):
+        return False
+    if schedule(form, M, N, K, torch.bfloat16) != 4 or (form, M, N, K, "bf16") in _TAIL:
+        return False
+    a_kc, b_kc = _KC[form]
+    return bool(native().gemm8_sq(a, a_kc, b, b_kc, out, sq, alpha_t, 1.0))

@@ -324,7 +324,17 @@ def param_weight_grad(wp: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor
     if g is None:
         return weight_grad_(None, dy, x, dy_scale=dy_scale)
     fresh = getattr(wp, "_mx_grad_fresh", False)
-    weight_grad_(g, dy, x, beta=0.0 if fresh else 1.0, dy_scale=dy_scale)
+    # the trainer's fused clip norm (mxllm/train/trainer.py): a first write (beta 0) of a gradient
+    # whose owner armed `_mx_sq` also leaves the per-tile sums of squares of the stored values
+    armed = getattr(wp, "_mx_sq_done", None)
+    sq = getattr(wp, "_mx_sq", None) if fresh and armed is False else None
+    if sq is not None and g.dtype == dy.dtype == x.dtype == torch.bfloat16 and gemm.mm_sq(
+            "tt", dy, x, g, sq, None if dy_scale is None else dy_scale.reshape(1).float()):
+        wp._mx_sq_done = True
+    else:
+        if armed is True:  # a second write onto partials already taken: the trainer re-reads instead
+            wp._mx_sq_done = "dirty"
+        weight_grad_(g, dy, x, beta=0.0 if fresh else 1.0, dy_scale=dy_scale)
     if fresh:
         wp._mx_grad_fresh = False
     mark_ready(wp)

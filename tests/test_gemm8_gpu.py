@@ -47,6 +47,31 @@ def test_gemm8_orders(gpu, a_kc, b_kc, M, N, K, ph, monkeypatch):
     _check(out32, ref, 1e-5)
 
 
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1000), (1024, 4096, 4096)])
+def test_gemm8_sq_partials(gpu, a_kc, b_kc, M, N, K):
+    """gemm8_sq: the output is bitwise the 4-phase gemm8's, and sq holds one fp32 sum of squares of
+    the stored bf16 values per 256 x 256 tile (row-major tile order), device alpha included."""
+    if (a_kc or b_kc) and K % 64:
+        K = 1024
+    a = _mat(M, K, gpu, pad=8, seed=6) if a_kc else _mat(K, M, gpu, pad=16, seed=6)
+    b = _mat(N, K, gpu, pad=24, seed=7) if b_kc else _mat(K, N, gpu, pad=8, seed=7)
+    alpha = torch.tensor([0.61], device=gpu)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    sq = torch.full(((M // 256) * (N // 256) + 3,), -1.0, device=gpu)
+    assert _ops().gemm8_sq(a, a_kc, b, b_kc, out, sq, alpha, 1.0)
+    ref = torch.empty_like(out)
+    assert _ops().gemm8(a, a_kc, b, b_kc, ref, 0.0, alpha, 1.0, 4)
+    assert torch.equal(out, ref)
+    want = out.float().pow(2).view(M // 256, 256, N // 256, 256).sum(dim=(1, 3)).flatten()
+    got = sq[:want.numel()]
+    assert torch.allclose(got, want, rtol=1e-5, atol=0), (got - want).abs().max().item()
+    assert (sq[want.numel():] == -1.0).all()  # nothing past the tiles
+    b2 = _mat(128, K, gpu, seed=8) if b_kc else _mat(K, 128, gpu, seed=8)
+    out2 = torch.empty(M, 128, device=gpu, dtype=torch.bfloat16)
+    assert not _ops().gemm8_sq(a, a_kc, b2, b_kc, out2, sq, None, 1.0)  # N % 256: declined
+
+
 @pytest.mark.parametrize("f32", [True, False])
 def test_gemm8_beta_alpha(gpu, f32):
     M, N, K = 512, 1024, 384

@@ -305,3 +305,33 @@ def test_bucketed_grad_norm_overlap(gpu, gdt, accum, monkeypatch):
         if ov == "1":
             assert len(tr.ddp.buckets) > 3
     assert abs(first["1"] - first["0"]) <= 1e-6 * first["0"], first
+
+
+def test_fused_grad_norm_matches_full_pass(gpu, monkeypatch):
+    """The clip norm from the dW GEMMs' per-tile partials (gemm8_sq) plus a direct pass over the other
+    gradients equals the full pass over the flat gradient to fp32 rounding, every armed GEMM weight
+    took the fused path, and training stays on the same trajectory."""
+    monkeypatch.setenv("MXLLM_GEMM8", "all")  # the tiny shapes on gemm8 (the table holds real ones)
+    cfg = _cfg()
+    g = torch.Generator(device=gpu).manual_seed(3)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=g) for _ in range(3)]
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MXLLM_FUSED_GRAD_NORM", fused)
+        tr = _ddp_trainer(gpu, cfg, 5)
+        norms = []
+        for b in batches:
+            tr.train_step([(b, b)])
+            norms.append(float(tr.last_grad_norm))
+        if fused == "1":
+            done = [n for n, p in tr.model.named_parameters() if getattr(p, "_mx_sq_done", None) is True]
+            assert tr._sq_params and any("wgu" in n for n in done) and any("wd" in n for n in done), done
+            assert not any("tok_emb" in n for n in done)  # the embedding gradient is summed directly
+        else:
+            assert not tr._sq_params
+        res[fused] = (norms, _masters(tr))
+    (n1, m1), (n0, m0) = res["1"], res["0"]
+    for a, b in zip(n1, n0):
+        assert abs(a - b) <= 1e-5 * b, (n1, n0)
+    for k in m0:
+        assert torch.allclose(m1[k].float(), m0[k].float(), rtol=0, atol=1e-6), k
