@@ -16,6 +16,39 @@ cfg = get_config("llama3.1-8b").replace(n_layers=2)
 model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=0)
 tr = Trainer(model, DistEnv(device=dev, backend="nccl"), OptimConfig(lr=1e-4))
 ids = torch.randint(0, cfg.vocab_size, (2, 2048), device=dev)
+import importlib  # noqa: E402
+
+linear = importlib.import_module("mxllm.ops.linear")
+from mxllm.ops import gemm  # noqa: E402
+
+_real_mm_sq = gemm.mm_sq
+
+
+def _traced_mm_sq(form, a, b, out, sq, alpha_t=None):
+    ok = _real_mm_sq(form, a, b, out, sq, alpha_t)
+    M, N, K = gemm._dims(form, a, b)
+    print(f"mm_sq {form} M{M} N{N} K{K} a{tuple(a.shape)}/{a.stride()} {a.dtype} b{tuple(b.shape)}/{b.stride()} "
+          f"out{out.dtype} sched={gemm.schedule(form, M, N, K, torch.bfloat16)} -> {ok}")
+    return ok
+
+
+gemm.mm_sq = _traced_mm_sq
+_real_pwg = linear.param_weight_grad
+
+
+def _traced_pwg(wp, dy, x, dy_scale=None):
+    if wp is not None and getattr(wp, "_mx_sq", None) is not None:
+        print(f"param_weight_grad {tuple(wp.shape)} fresh={getattr(wp, '_mx_grad_fresh', None)} "
+              f"armed={getattr(wp, '_mx_sq_done', None)} dy{dy.dtype} x{x.dtype}")
+    return _real_pwg(wp, dy, x, dy_scale)
+
+
+linear.param_weight_grad = _traced_pwg
+_fused = importlib.import_module("mxllm.ops.fused")
+_loss = importlib.import_module("mxllm.ops.loss")
+
+_fused.param_weight_grad = _traced_pwg
+_loss.param_weight_grad = _traced_pwg
 for _ in range(2):
     tr.train_step([(ids, ids)])
 torch.cuda.synchronize()
