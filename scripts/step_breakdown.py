@@ -1,8 +1,8 @@
 """Per-step kernel time breakdown from a rocprofv3 kernel trace: the window
-between the last two grad-norm launches (one per optimizer step) -> one step.
+between the last two launches of a once-per-step kernel (the embedding lookup) -> one step.
 usage: python scripts/step_breakdown.py <run_kernel_trace.csv> [top] [marker]
-marker: kernel-name substring launched once per step (default: the grad-norm kernel; ZeRO-3 runs
-its norm per unit, so use e.g. ``embedding_fwd`` there)."""
+marker: kernel-name substring launched once per step (default: ``embedding_fwd``, else the grad-norm
+or AdamW kernel)."""
 import collections
 import csv
 import sys
@@ -25,8 +25,11 @@ def main():
     rows = _rows(sys.argv[1])
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # one grad-norm kernel per optimizer step (AdamW may be issued as several chunk launches)
-    key = "sqnorm_partial" if any("sqnorm_partial" in r["Kernel_Name"] for r in rows) else "adamw_kernel"
+    # a kernel launched once per step: the embedding lookup that opens every forward (the clip norm can
+    # run as several partial passes per step, AdamW as several chunk launches)
+    names = [r["Kernel_Name"] for r in rows]
+    key = next((k for k in ("embedding_fwd", "sqnorm_partial", "adamw_kernel") if any(k in n for n in names)),
+               "adamw_kernel")
     if len(sys.argv) > 3:
         key = sys.argv[3]
     marks = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
