@@ -448,12 +448,10 @@ class Trainer:
             plan = self._sq_plan[done] = (big, small)
         big, small = plan
         g = self.flat.grads
-        sq = self._sqbuf.sum().reshape(1)
-        for lo, hi in big:
-            sq = sq + ops.sq_norm(g[lo:hi])
+        parts = [self._sqbuf.sum().reshape(1)] + [ops.sq_norm(g[lo:hi]) for lo, hi in big]
         if small:
-            sq = sq + ops.sq_norm(torch.cat([g[lo:hi] for lo, hi in small]))
-        return sq
+            parts.append(ops.sq_norm(torch.cat([g[lo:hi] for lo, hi in small])))
+        return torch.cat(parts).sum().reshape(1)  # one fixed-order sum, not a chain of adds
 
     def _sync_adapters(self):
         """LoRA adapters -> their copies in the augmented GEMM weight buffers."""
