@@ -230,7 +230,7 @@ bool gemm8_sq(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at
 // `at` columns (rows when `rows`) -- whole waves of tiles before it, half-K workgroups summed through
 // an fp32 workspace after it.  Returns false (nothing launched) for shapes it does not take.
 bool gemm8_tail(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, at::Tensor& out, int64_t at,
-                bool rows, int64_t ph) {
+                bool rows, int64_t ph, const c10::optional<at::Tensor>& sq) {
   MX_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm8_tail: GPU tensors");
   MX_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
            "gemm8_tail: bf16 operands and output");
@@ -241,11 +241,19 @@ bool gemm8_tail(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, 
   const int64_t lim = rows ? M : N;
   if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1 || at <= 0 || at >= lim) return false;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return false;
+  float* sqp = nullptr;
+  if (sq.has_value()) {  // one sum of squares per 256 x 256 tile (plain part's tiles, then the split part's)
+    MX_CHECK(sq->scalar_type() == at::kFloat && sq->is_contiguous() && sq->device() == a.device(),
+             "gemm8_tail sq: contiguous f32 on the device");
+    if (M % 256 || N % 256) return false;
+    MX_CHECK(sq->numel() >= (M / 256) * (N / 256), "gemm8_tail sq: partials buffer too small");
+    sqp = sq->data_ptr<float>();
+  }
   DevGuard g(a.device());
   auto ws = at::empty({2 * (lim - at) * (rows ? N : M)}, a.options().dtype(at::kFloat));
   const int rc = mx_gemm8_tail(bf(a), a.stride(0), a_kc ? 1 : 0, bf(b), b.stride(0), b_kc ? 1 : 0, bfm(out),
                                out.stride(0), (int)M, (int)N, (int)K, rows ? 1 : 0, (int)at, ws.data_ptr<float>(),
-                               (int)ph, cur_stream());
+                               (int)ph, cur_stream(), sqp);
   if (rc == -1) return false;
   MX_OK(rc);
   return true;
@@ -1231,7 +1239,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("prefetch(Tensor t, int wgs) -> ()");
   m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);  // no tensor args: catch-all
   m.def("gemm8_stamps() -> Tensor", &gemm8_stamps);
-  m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4) -> bool");
+  m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4, Tensor(b!)? sq=None) -> bool");
   m.def("gemm8_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, Tensor(a!) q, Tensor(b!) k, Tensor(c!) v) -> bool");
   m.def("gemm8_swiglu(Tensor x, Tensor w, Tensor(a!) gu, Tensor(b!) m) -> bool");
   m.def("gemm8_sq(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, Tensor(b!) sq, Tensor? alpha_t=None, float alpha=1.0) -> bool");

@@ -1260,6 +1260,37 @@ __global__ void __launch_bounds__(256) g8_sum2_kernel(const float* __restrict__ 
   }
 }
 
+// g8_sum2 over whole 256 x 256 tiles of the K-part images (one workgroup per tile, the same
+// arithmetic), also writing one sum of squares of the stored bf16 values per tile into sq[tile]
+// (row-major tile order over the [M2, N2] region): the tail-balanced launch's share of the clip-norm
+// partials (mx_gemm8_sq for the rest)
+__global__ void __launch_bounds__(256) g8_sum2_sq_kernel(const float* __restrict__ P, int64_t part, int N2,
+                                                         uint16_t* __restrict__ C, int64_t ldc,
+                                                         float* __restrict__ sq) {
+  __shared__ float red[4];
+  const int tn = N2 >> 8, tm0 = blockIdx.x / tn, tn0 = blockIdx.x % tn;
+  const int cu = threadIdx.x & 31, r0 = threadIdx.x >> 5;  // 8-column unit, first row
+  float s = 0.f;
+  for (int r = r0; r < 256; r += 8) {
+    const int64_t m = (int64_t)tm0 * 256 + r;
+    const int n = tn0 * 256 + cu * 8;
+    const int64_t i = m * N2 + n;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(P + i), a1 = *reinterpret_cast<const f32x4*>(P + i + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(P + part + i), b1 = *reinterpret_cast<const f32x4*>(P + part + i + 4);
+    uint4 o;
+    o.x = pack_bf16x2(a0[0] + b0[0], a0[1] + b0[1]);
+    o.y = pack_bf16x2(a0[2] + b0[2], a0[3] + b0[3]);
+    o.z = pack_bf16x2(a1[0] + b1[0], a1[1] + b1[1]);
+    o.w = pack_bf16x2(a1[2] + b1[2], a1[3] + b1[3]);
+    *reinterpret_cast<uint4*>(C + m * ldc + n) = o;
+    s = g8_sq8(o, s);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) sq[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // Tail-balanced bf16 GEMM, beta 0, alpha 1: C[M, N] = op(A) op(B) where the tile count leaves a last
 // wave of <= 128 tiles on the 256 CUs (e.g. the 70B qkv forward: 16 x 40 = 640 tiles).  The output is
 // split at `at` (columns, or rows when `rows`): [0, at) runs as one plain launch of whole waves; the
@@ -1268,13 +1299,19 @@ __global__ void __launch_bounds__(256) g8_sum2_kernel(const float* __restrict__ 
 // (deterministic).  The last wave then takes half a wave's time.  `at` and the rest multiples of 256.
 extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc,
                              uint16_t* C, int64_t ldc, int M, int N, int K, int rows, int at, float* ws, int ph,
-                             hipStream_t stream) {
+                             hipStream_t stream, float* sq) {
   const int lim = rows ? M : N, rest = lim - at;
   if (at <= 0 || rest <= 0 || (at & 255) || (rest & 255) || K < 2 * G8_BK) return -1;
   if ((a_kc ? lda < K : lda < M) || (b_kc ? ldb < K : ldb < N) || ldb % 8 || lda % 8 || ldc % 8) return -1;
-  // plain part
-  int rc = rows ? mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, at, N, K, 0.f, nullptr, 1.f, ph, stream)
-                : mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, M, at, K, 0.f, nullptr, 1.f, ph, stream);
+  if (sq && (ph != 4 || (M & 255) || (N & 255))) return -1;  // partials: the 4-phase schedule, whole tiles
+  // plain part (sq: its tiles' partials first, then the split part's)
+  int rc;
+  if (sq)
+    rc = rows ? mx_gemm8_sq(A, lda, a_kc, B, ldb, b_kc, C, ldc, at, N, K, nullptr, 1.f, sq, stream)
+              : mx_gemm8_sq(A, lda, a_kc, B, ldb, b_kc, C, ldc, M, at, K, nullptr, 1.f, sq, stream);
+  else
+    rc = rows ? mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, at, N, K, 0.f, nullptr, 1.f, ph, stream)
+              : mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, M, at, K, 0.f, nullptr, 1.f, ph, stream);
   if (rc) return rc;
   const uint16_t* A2 = rows ? (a_kc ? A + (int64_t)at * lda : A + at) : A;
   const uint16_t* B2 = rows ? B : (b_kc ? B + (int64_t)at * ldb : B + at);
@@ -1300,6 +1337,11 @@ extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uin
   else if (b_kc) G8_T(false, true);
   else G8_T(false, false);
 #undef G8_T
+  if (sq) {
+    const int64_t nplain = rows ? (int64_t)(at >> 8) * (N >> 8) : (int64_t)(M >> 8) * (at >> 8);
+    g8_sum2_sq_kernel<<<(M2 >> 8) * (N2 >> 8), 256, 0, stream>>>(ws, part, N2, C2, ldc, sq + nplain);
+    return (int)hipGetLastError();
+  }
   int64_t blocks = (part / 8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   g8_sum2_kernel<<<(int)blocks, 256, 0, stream>>>(ws, part, N2, C2, ldc, part);

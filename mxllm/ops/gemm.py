@@ -177,7 +177,10 @@ def mm_sq(form: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, sq: to
     M, N, K = _dims(form, a, b)
     if not (use_native(a) and a.dtype == b.dtype == out.dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0):
         return False
-    if schedule(form, M, N, K, torch.bfloat16) != 4 or (form, M, N, K, "bf16") in _TAIL:
+    if schedule(form, M, N, K, torch.bfloat16) != 4:
         return False
     a_kc, b_kc = _KC[form]
+    t = _TAIL.get((form, M, N, K, "bf16"), 0)
+    if t and alpha_t is None:  # the tail-balanced launch, as ``mm`` takes it (its split part sums per tile)
+        return bool(native().gemm8_tail(a, a_kc, b, b_kc, out, abs(t), t < 0, 4, sq))
     return bool(native().gemm8_sq(a, a_kc, b, b_kc, out, sq, alpha_t, 1.0))

@@ -9,6 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 
 from mxllm.models import Llama, get_config  # noqa: E402
 from mxllm.parallel.runtime import DistEnv  # noqa: E402
+from mxllm import ops  # noqa: E402
 from mxllm.train.trainer import OptimConfig, Trainer  # noqa: E402
 
 dev = torch.device("cuda", 0)
@@ -51,6 +52,11 @@ _fused.param_weight_grad = _traced_pwg
 _loss.param_weight_grad = _traced_pwg
 for _ in range(2):
     tr.train_step([(ids, ids)])
+    torch.cuda.synchronize()
+    # the full pass over the same (still present: overwrite-style) gradient, for comparison
+    full = float(ops.sq_norm(tr.flat.grads).sqrt())
+    print(f"clip norm fused {float(tr.last_grad_norm):.8g} full pass {full:.8g} "
+          f"rel diff {abs(float(tr.last_grad_norm) - full) / full:.3g}")
 torch.cuda.synchronize()
 names = {id(p): n for n, p in model.named_parameters()}
 for p in tr._sq_params:

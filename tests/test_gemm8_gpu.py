@@ -154,6 +154,29 @@ def test_gemm8_tail_split(gpu, a_kc, b_kc, M, N, n1, K):
         _check(rows_out[m1:], ref[m1:], 5e-3)
 
 
+def _tile_sq(x):
+    M, N = x.shape
+    return x.float().pow(2).view(M // 256, 256, N // 256, 256).sum(dim=(1, 3)).flatten()
+
+
+@pytest.mark.parametrize("rows", [False, True])
+def test_gemm8_tail_sq_partials(gpu, rows):
+    """The tail-balanced launch with clip-norm partials: output bitwise the plain tail launch's, one
+    sum of squares per tile -- the plain part's tiles (row-major), then the split part's."""
+    M, N, K, at = (768, 512, 1024, 512) if rows else (512, 1280, 8256, 768)
+    a = _mat(K, M, gpu, seed=11)  # token-major dW form (both operands mn-contiguous)
+    b = _mat(K, N, gpu, seed=12)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    sq = torch.full(((M // 256) * (N // 256),), -1.0, device=gpu)
+    assert _ops().gemm8_tail(a, False, b, False, out, at, rows, 4, sq)
+    ref = torch.empty_like(out)
+    assert _ops().gemm8_tail(a, False, b, False, ref, at, rows, 4)
+    assert torch.equal(out, ref)
+    parts = (out[:at], out[at:]) if rows else (out[:, :at], out[:, at:])
+    want = torch.cat([_tile_sq(p.contiguous()) for p in parts])
+    assert torch.allclose(sq, want, rtol=1e-5, atol=0), (sq - want).abs().max().item()
+
+
 def test_gemm_dispatch_uses_tail_entry(gpu, monkeypatch):
     """A win-table entry with ``tail`` routes the forward GEMM through the tail-balanced launch."""
     from mxllm.ops import gemm
