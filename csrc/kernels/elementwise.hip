@@ -343,9 +343,12 @@ extern "C" int mx_swiglu_bwd(const uint16_t* dm, const uint16_t* gu, uint16_t* d
 static int adamw_grid_cap() {
   static int cap = -1;
   if (cap < 0) {
-    const char* e = getenv("MXLLM_ADAMW_GRID");  // experiments: fewer workgroups beside concurrent GEMMs
-    cap = e ? atoi(e) : 2048;
-    if (cap < 1) cap = 2048;
+    // workgroups of one AdamW launch (grid-stride beyond).  The overlapped update shares the GPU with the
+    // next forward's GEMMs: 1,024 beats 2,048 on config 2 by 1.2-1.8 ms per step and is neutral on the
+    // headline and the config-4 proxy; 768 and 512 lose (profiles/r5y/, r5z/).  MXLLM_ADAMW_GRID overrides.
+    const char* e = getenv("MXLLM_ADAMW_GRID");
+    cap = e ? atoi(e) : 1024;
+    if (cap < 1) cap = 1024;
   }
   return cap;
 }
