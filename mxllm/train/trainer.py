@@ -350,7 +350,10 @@ class Trainer:
         """Forward + backward of every micro-batch (gradients accumulated in the
         flat buffer, reduced across ranks by the DDP buckets).  Returns (sum of
         the micro-batch losses, scale that turns the flat gradient into the mean
-        gradient) — the flat buffer holds the SUM over ranks and micro-batches."""
+        gradient) — each backward runs on loss / n, so the flat buffer holds the
+        SUM over ranks of each rank's micro-batch MEAN and the scale is 1 / world
+        (it used to divide by n a second time: the clip norm read n x too small
+        under gradient accumulation)."""
         n = len(micro_batches)
         self.model.train()
         if self.zero1 is not None and getattr(self.model, "param_wait", None) is None:
@@ -381,7 +384,7 @@ class Trainer:
         if self.fresh_grads:
             self.flat.zero_unwritten_()
         with range_("grad_allreduce_wait"):
-            scale = self.ddp.finish() / n if n > 1 else self.ddp.finish()
+            scale = self.ddp.finish()
         if self._norm_side is not None and changed:
             # a gradient folded into the flat buffer after its bucket's norm was taken
             for bi in sorted({self.ddp._param_bucket[k] for k in changed}):

@@ -124,3 +124,21 @@ def test_fresh_guard_zeroes_stale_slot_before_autograd_accumulates():
     ((p * 2).sum() + (p * 3).sum()).backward()  # two contributions: zero once, then both accumulate
     assert torch.equal(p.grad, torch.full((4,), 5.0))
     assert p._mx_grad_fresh is False
+
+
+def test_grad_norm_under_accumulation_matches_one_batch(monkeypatch):
+    """World 1: two micro-batches of 2 sequences clip on the same gradient norm as one
+    micro-batch of the 4 (the flat buffer holds the micro-batch MEAN; the scale is 1/world)."""
+    monkeypatch.setenv("MXLLM_FORCE_CPU", "1")
+    from mxllm.models import Llama, get_config
+    from mxllm.parallel.runtime import DistEnv
+    from mxllm.train.trainer import OptimConfig, Trainer
+
+    cfg = get_config("tiny").replace(n_layers=2, vocab_size=300)
+    ids = torch.randint(0, cfg.vocab_size, (4, 32), generator=torch.Generator().manual_seed(3))
+    norms = []
+    for mbs in ([(ids, ids)], [(ids[:2], ids[:2]), (ids[2:], ids[2:])]):
+        tr = Trainer(Llama(cfg, dtype=torch.float32, seed=5), DistEnv(), OptimConfig(lr=1e-3, grad_clip=1.0))
+        tr.train_step(mbs)
+        norms.append(float(tr.last_grad_norm))
+    assert abs(norms[0] - norms[1]) < 1e-4 * norms[0], norms
