@@ -83,7 +83,7 @@ def parse(argv=None):
                          "auto = when the headline runs on 8 GPUs")
     ap.add_argument("--config4-micro-batch", type=int, default=4)
     # selective checkpointing of the first N of 80 layers (the rest keep their activations).  Emulated
-    # world-8 per-rank step, one box (profiles/r4g/c4_ck*.json): N = 56 3,298 ms / 223.5 GB reserved;
+    # world-8 per-rank step, one box (archive/profiles/r4g/c4_ck*.json): N = 56 3,298 ms / 223.5 GB reserved;
     # 40: 3,141 ms / 255.2 GB; 24: 2,990 ms / 286.9 GB (~2 GB per checkpointed layer).  Default: the
     # fewest checkpointed layers (>= 40) whose reserved peak + CONFIG4_MARGIN_GB fits the smallest free
     # HBM over the ranks (config4_plan).
@@ -451,7 +451,10 @@ def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "") 
     import io
     import tempfile
 
-    if a.device != "cpu" and torch.cuda.device_count() < world:
+    if (a.device != "cpu" and torch.cuda.device_count() < world
+            and os.environ.get("MXLLM_BENCH_SHARED_GPU", "0") != "1"):
+        # MXLLM_BENCH_SHARED_GPU=1 (rehearsals on a 1-GPU box, with MXLLM_BACKEND=gloo MXLLM_COMM=peer):
+        # the child's ranks share the visible GPU(s) (runtime.pick_device: local_rank % device_count)
         return {"skipped": f"this process sees {torch.cuda.device_count()} GPU(s), the child job needs {world}"}
     limit = child_timeout(a, timeout_s)
     if limit is None:
@@ -512,8 +515,8 @@ def run_config3(a, world: int, parallel: str = "ddp") -> dict:
 # the first n0 layers checkpointed, +per GB for each layer fewer.  The un-checkpointed layers
 # recompute m = swiglu(gu) (MXLLM_RECOMPUTE_SWIGLU) and the normed qkv / gate-up inputs
 # (MXLLM_RECOMPUTE_NORM) in the backward by default: 258.2 / 268.4 / 278.6 GB at 16 / 8 / 0
-# (profiles/r4_recompute/pass_u_*.json); m only: 237.8 GB at 40, +1.52 per layer (pass R);
-# nothing recomputed: profiles/r4g/c4_ck*.json.  Margin: RCCL buffers of the two ZeRO-3
+# (archive/profiles/r4_recompute/pass_u_*.json); m only: 237.8 GB at 40, +1.52 per layer (pass R);
+# nothing recomputed: archive/profiles/r4g/c4_ck*.json.  Margin: RCCL buffers of the two ZeRO-3
 # communicators + allocator slack of the real 8-rank job
 CONFIG4_RESERVED = (16, 258.2, 1.30)
 CONFIG4_RESERVED_M_ONLY = (40, 237.8, 1.56)
@@ -587,7 +590,7 @@ def run_config4(a, world: int, ckpt_layers: int = 40) -> dict:
 
 
 # peak HBM RESERVED by the caching allocator for a world-1 run of a configuration (driver record
-# BENCH_r02.json / profiles/r3h/bench_default.json), and the activation memory one checkpointed
+# BENCH_r02.json / archive/profiles/r3h/bench_default.json), and the activation memory one checkpointed
 # layer gives back (70B, 2 x 2048 tokens: ~150 GB of activations over 80 layers)
 RESERVED_GB = {("llama3.1-70b", "lora", 2, 2048): (294.3, 1.7)}
 RCCL_ALLOWANCE_GB = 3.0  # communicator buffers + DDP bucket slack at world > 1

@@ -128,7 +128,7 @@ def main():
     ops = native()
     T = a.tokens
     # warm the device (clocks, allocator, code objects) before the first timed case: in passes C
-    # and D whichever case ran first read ~15 % slow (profiles/r4d/layout.txt)
+    # and D whichever case ran first read ~15 % slow (archive/profiles/r4d/layout.txt)
     wa, wb = rnd(4096, 8192, dev=dev), rnd(8192, 8192, dev=dev)
     wo = torch.empty(4096, 8192, device=dev, dtype=torch.bfloat16)
     import time as _t

@@ -4,7 +4,7 @@
 the driver at round end).  PROJECTION, not measurement.
 
 Inputs: the measured one-GPU step (bench JSON), the measured fraction of the
-step spent in backward (roctx ranges of profiles/r1b_70b_lora_roctx_ranges.md:
+step spent in backward (roctx ranges of archive/profiles/r1b_70b_lora_roctx_ranges.md:
 ~2/3), the gradient bytes each step all-reduces, and an assumed achieved
 all-reduce bus bandwidth over xGMI (two cases: 150 GB/s = one ring bound to one
 153 GB/s link; 350 GB/s = RCCL multi-channel rings over several links).

@@ -576,7 +576,7 @@ attn_bwd8_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
     // spread (prio & 16, default): the next tile's DMA pieces go out one per S/dP k step and the
     // previous tile's dS stores one per dV/dK step -- issued in one burst at the loop top, the 8
     // waves' vector-memory instructions queued behind each other and the low-priority half
-    // stalled there ~2000 cycles per tile (phase profile, profiles/r2z_bwd8_phase_cycles.txt)
+    // stalled there ~2000 cycles per tile (phase profile, archive/profiles/r2z_bwd8_phase_cycles.txt)
     const bool spread = (prio & 16) != 0;
     const bool more = L + 1 < nit;
     if (!spread) {
@@ -787,13 +787,17 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   }
 }
 
+// ============================================================================================
+// Measured-slower backward variant: compiled only with -DMXLLM_ATTN_EXPERIMENTS.
+// The default build has ONE D = 128 backward family: attn_bwd8_kernel + attn_bwd_dq_kernel.
+#ifdef MXLLM_ATTN_EXPERIMENTS
 // Staggered split-mode key-block kernel (MXLLM_ATTN_BWD8=2).  Same work split
 // as attn_bwd8_kernel (8 waves = 4 key groups x 2 q halves, 128 keys of one q head per workgroup),
 // but the two q halves run HALF A TILE apart: each tile is two phases -- A: S = Q K^T, dP = dO V^T
 // and the softmax, B: dV^T += dO^T P, dK^T += Q^T dS -- separated by a barrier, and waves 4-7 start
 // one barrier late.  One half's softmax VALU then runs under the other half's MFMAs (in
 // attn_bwd8_kernel both halves hit the softmax at the same time behind one barrier per tile, and the
-// faster half waited ~1,260 cycles per tile: profiles/r4ad/README.md).  The offset needs the Q / dO
+// faster half waited ~1,260 cycles per tile: archive/profiles/r4ad/README.md).  The offset needs the Q / dO
 // tiles of THREE iterations in LDS (a 3-slot ring, 96 KB + the 64 KB K / V images = the CU's whole
 // 160 KB), so lse / delta no longer go through LDS: each wave loads its 32 rows' values one
 // iteration ahead into one VGPR (lanes 0-31 lse, 32-63 delta) and broadcasts them with shuffles.
@@ -1100,6 +1104,8 @@ attn_bwd8s_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K
   }
 }
 
+#endif  // MXLLM_ATTN_EXPERIMENTS
+
 // Deterministic dQ: dq[b,h,q,:] = sum over the key blocks that visited q (ascending kb)
 // of the partials written by attn_bwd_kernel<.., DQM=2>.  One thread per 4 floats.
 template <int D, bool CAUSAL>
@@ -1394,10 +1400,12 @@ static bool attn_bwd8_on() {
   }();
   return on;
 }
+#ifdef MXLLM_ATTN_EXPERIMENTS
 static bool attn_bwd8_stagger() {  // MXLLM_ATTN_BWD8=2: the staggered half-tile schedule (read per call: A/B)
   const char* e = getenv("MXLLM_ATTN_BWD8");
   return e && e[0] == '2';
 }
+#endif
 static int attn_bwd8_hpw(int B, int Hq, int Hkv, int S, int Sk, int D, int dq_mode) {
   (void)S;
   if (dq_mode != 3 || D != 128 || !attn_bwd8_on() || Hkv <= 0 || Hq % Hkv) return 1;
@@ -1438,27 +1446,32 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   const float sl = scale * 1.4426950408889634f;
   const int off = Sk - S;
   const int S_pad = (S + 63) / 64 * 64;  // dq / dS^T rows are padded (see contract above)
+#ifdef MXLLM_ATTN_EXPERIMENTS
   if (causal < 0) {  // ablation: no dQ work at all (timing experiments only; dq left untouched)
     attn_bwd_kernel<128, true, 0><<<grid, 256, 0, stream>>>(q, k, v, dout, lse, delta, dq, dkp, dvp, B, Hq, Hkv,
                                                             S, Sk, off, sl, scale, S_pad);
     return (int)hipGetLastError();
   }
+#else
+  if (causal < 0) return -1;
+#endif
   float* dqk = dq_mode == 1 ? dq : reinterpret_cast<float*>(work);
   const bool bwd8 = attn_bwd8_on();
   // MXLLM_ATTN_BWD8_PRIO (bit flags, default 273): 1 = s_setprio 1 for waves 4-7, 16 = spread the
   // DMA / dS-store issue over the MFMA steps; 256 (with 16) = counted end-of-tile wait that leaves
-  // the dS^T stores in flight (B2 S2048: 0.627 -> 0.599 ms, headline -2.9 ms; profiles/r4ad/);
+  // the dS^T stores in flight (B2 S2048: 0.627 -> 0.599 ms, headline -2.9 ms; archive/profiles/r4ad/);
   // 2 = timing ablation (same q tile every step, wrong results)
   static const int bwd8_prio = [] {
     const char* e = getenv("MXLLM_ATTN_BWD8_PRIO");
     return e && *e ? atoi(e) : 273;
   }();
+  const int hpw = attn_bwd8_hpw(B, Hq, Hkv, S, Sk, D, dq_mode);
+  const int grid8 = nkb * B * (Hq / hpw);
+#ifdef MXLLM_ATTN_EXPERIMENTS
   static const bool bwd8_prof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report of the 8-wave kernel (stderr)
     const char* e = getenv("MXLLM_ATTN_PROF");
     return e && e[0] == '1';
   }();
-  const int hpw = attn_bwd8_hpw(B, Hq, Hkv, S, Sk, D, dq_mode);
-  const int grid8 = nkb * B * (Hq / hpw);
   if (dq_mode == 3 && D == 128 && bwd8 && bwd8_prof) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     uint32_t* pbuf = nullptr;
@@ -1500,7 +1513,9 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
     else
       attn_bwd8s_kernel<false><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
                                                           off, sl, scale, S_pad, hpw);
-  } else if (dq_mode == 3 && D == 128 && bwd8) {
+  } else
+#endif
+  if (dq_mode == 3 && D == 128 && bwd8) {
     uint16_t* dst = reinterpret_cast<uint16_t*>(work);
     if (causal)
       attn_bwd8_kernel<true><<<grid8, 512, 0, stream>>>(q, k, v, dout, lse, delta, dst, dkp, dvp, B, Hq, Hkv, S, Sk,
@@ -1543,10 +1558,14 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
   } else if (dq_mode == 3) {
     // 128 q rows per workgroup (every K tile feeds two 64-row sub-blocks); D=32 keeps 64
     // MXLLM_ATTN_DQ_QB=2 (experiment): D = 128 with 128 q rows per workgroup and a 4-deep ring
+#ifdef MXLLM_ATTN_EXPERIMENTS
     static const int qb128 = [] {
       const char* e = getenv("MXLLM_ATTN_DQ_QB");
       return e && e[0] == '2' ? 2 : 4;
     }();
+#else
+    constexpr int qb128 = 4;
+#endif
     const int qbs = D == 128 ? qb128 : (D == 64 ? 2 : 1);
     const int qgrid = ((S + 64 * qbs - 1) / (64 * qbs)) * B * Hq;
     const uint16_t* dst = reinterpret_cast<const uint16_t*>(work);
@@ -1560,6 +1579,7 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
       attn_bwd_dq_kernel<DD, false, QB><<<qgrid, 256 * QB, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, \
                                                                         nkb * 128, scale, dqkv, ldq, cosb, sinb); \
   } while (0)
+#ifdef MXLLM_ATTN_EXPERIMENTS
     if (D == 128 && qbs == 2) {
       if (causal)
         attn_bwd_dq_kernel<128, true, 2><<<qgrid, 512, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad, nkb * 128,
@@ -1567,7 +1587,9 @@ extern "C" int mx_attn_bwd(const uint16_t* q, const uint16_t* k, const uint16_t*
       else
         attn_bwd_dq_kernel<128, false, 2><<<qgrid, 512, 0, stream>>>(dst, k, dq, B, Hq, Hkv, S, Sk, off, S_pad,
                                                                     nkb * 128, scale, dqkv, ldq, cosb, sinb);
-    } else if (D == 128) DQK(128);
+    } else
+#endif
+    if (D == 128) DQK(128);
     else if (D == 64) DQK(64);
     else DQK(32);
 #undef DQK

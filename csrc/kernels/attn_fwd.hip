@@ -65,7 +65,7 @@ __device__ __forceinline__ u16x4 tr_read(const char* p) {
 // (0.259 vs 0.257 ms at B2 S2048 Hq64 Hkv8 D128 causal: the stream is not the limiter)
 // R: depth of the K/V tile ring in LDS (R - 1 tiles in flight ahead of the one being consumed).
 // One tile of lookahead (R = 2) left about a quarter of every tile waiting for the next tile's DMA
-// (profiles/r4ah/README.md): the DMA round trip is longer than one tile of MFMAs.  With 8 waves per
+// (archive/profiles/r4ah/README.md): the DMA round trip is longer than one tile of MFMAs.  With 8 waves per
 // workgroup (one workgroup per CU, 256 query rows sharing every tile) a 3- or 4-deep ring fits the
 // CU's 160 KB of LDS (96 / 128 KB).
 // SR (split ring, 4 waves, D = 128): K in a 3-slot ring and V in a 2-slot ring = 80 KB, so two
@@ -462,6 +462,11 @@ attn_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, 
   }
 }
 
+// ============================================================================================
+// Measured-slower forward variants: compiled only with
+// -DMXLLM_ATTN_EXPERIMENTS (python -m mxllm._build with MXLLM_FILE_FLAGS="attn_fwd.hip=-DMXLLM_ATTN_EXPERIMENTS").
+// The default build has ONE forward family, attn_fwd_kernel<D, CAUSAL, 4>.
+#ifdef MXLLM_ATTN_EXPERIMENTS
 // ---------------------------------------------------------------------------------------------
 // D = 128 forward with a barrier-enforced ping-pong of two wave groups (opt-in MXLLM_ATTN_FWD=pp).
 // Per 64-key tile a wave's work is a serial chain -- QK^T MFMAs, the softmax VALU (32 exp2 per
@@ -750,7 +755,7 @@ attn_fwd_pp_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ 
 
 // ---------------------------------------------------------------------------------------------
 // D = 128 forward, software-pipelined (opt-in: MXLLM_ATTN_FWD=p; measured SLOWER than the kernel
-// above -- 0.300 vs 0.265 ms at B2 S2048 Hq64 Hkv8, see profiles/r1d_experiments.md -- and kept for
+// above -- 0.300 vs 0.265 ms at B2 S2048 Hq64 Hkv8, see archive/profiles/r1d_experiments.md -- and kept for
 // the record and further work).  One wave per SIMD owning the whole register file and 64 query rows (two 32-row blocks
 // that share every K / V^T fragment read, so LDS reads, LDS-DMA and address work per MFMA halve),
 // 4 waves = 256 rows per workgroup.  Per 64-key tile t a wave runs two phases:
@@ -1102,63 +1107,34 @@ attn_fwd_p_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K
   }
 }
 
-}  // namespace mx
 
-using namespace mx;
 
-// o: token-major [B, S, Hq*D] rows with row stride ldo (elements, >= Hq*D): the rows may
-// be the left part of the LoRA-augmented o-projection input (mxllm/ops/linear.py)
-extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B,
-                           int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, int ldo,
-                           hipStream_t stream) {
-  if (B <= 0 || S <= 0) return 0;
-  if (Hkv <= 0 || Hq % Hkv || ldo < Hq * D || ldo % 8) return -1;
-  const float sl = scale * 1.4426950408889634f;
-  const int off = Sk - S;
-  static const bool pipe = [] {  // MXLLM_ATTN_FWD=p: the software-pipelined 64-row-per-wave kernel (A/B)
-    const char* e = getenv("MXLLM_ATTN_FWD");
-    return e && e[0] == 'p' && e[1] != 'p';
-  }();
-  static const bool pingpong = [] {  // MXLLM_ATTN_FWD=pp: the 8-wave two-group ping-pong kernel
-    const char* e = getenv("MXLLM_ATTN_FWD");
-    return e && e[0] == 'p' && e[1] == 'p';
-  }();
-  if (D == 128 && pingpong) {
+// env-selected D = 128 variants (A/B only): MXLLM_ATTN_FWD=p | pp, MXLLM_ATTN_FWD_WAVES=8,
+// MXLLM_ATTN_FWD_RING=3 | 4 | k3, MXLLM_ATTN_PROF=1 (phase-cycle report, host-synchronising).
+// Returns 1 when none is selected (the caller launches the production kernel).
+static int attn_fwd_experiment(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
+                               int B, int Hq, int Hkv, int S, int Sk, int causal, int off, float sl, int ldo,
+                               int fflags, hipStream_t stream) {
+  const char* fe = getenv("MXLLM_ATTN_FWD");
+  const bool pipe = fe && fe[0] == 'p' && fe[1] != 'p', pingpong = fe && fe[0] == 'p' && fe[1] == 'p';
+  if (pingpong) {
     const unsigned grid = ((S + 255) / 256) * B * Hq;
     if (causal) attn_fwd_pp_kernel<true><<<grid, 512, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
     else attn_fwd_pp_kernel<false><<<grid, 512, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
     return (int)hipGetLastError();
   }
-  if (D == 128 && pipe) {
+  if (pipe) {
     const unsigned grid = ((S + 255) / 256) * B * Hq;
     if (causal) attn_fwd_p_kernel<true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
     else attn_fwd_p_kernel<false><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo);
     return (int)hipGetLastError();
   }
-  static const int nw128 = [] {  // MXLLM_ATTN_FWD_WAVES=8: the 8-wave (256-row) variant for D = 128 (A/B)
-    const char* e = getenv("MXLLM_ATTN_FWD_WAVES");
-    return (e && e[0] == '8') ? 8 : 4;
-  }();
-  // MXLLM_ATTN_FWD_RING=3|4: 8 waves with a 3- / 4-deep K/V ring; =k3: 4 waves, split ring (K 3, V 2
-  // slots, two barriers per tile) -- D = 128
-  static const int ring = [] {
-    const char* e = getenv("MXLLM_ATTN_FWD_RING");
-    if (e && e[0] == 'k' && e[1] == '3') return -3;
-    const int r = e && *e ? atoi(e) : 0;
-    return (r == 3 || r == 4) ? r : 0;
-  }();
-  static const int fflags = [] {  // MXLLM_ATTN_FWD_FLAGS (default 1): bit 0 = spread the K/V DMA issue
-    const char* e = getenv("MXLLM_ATTN_FWD_FLAGS");   // (B2 0.192 -> 0.186 ms, B16 1.372 -> 1.357 ms)
-    return e && *e ? atoi(e) : 1;
-  }();
-#define FWD(DD, C, NWV)                                                                                  \
-  attn_fwd_kernel<DD, C, NWV><<<((S + 32 * NWV - 1) / (32 * NWV)) * B * Hq, 64 * NWV, 0, stream>>>(     \
-      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
-  static const bool fprof = [] {  // MXLLM_ATTN_PROF=1: phase-cycle report (D = 128, 4 waves; stderr)
-    const char* e = getenv("MXLLM_ATTN_PROF");
-    return e && e[0] == '1';
-  }();
-  if (D == 128 && nw128 == 4 && causal && fprof) {
+  const char* we = getenv("MXLLM_ATTN_FWD_WAVES");
+  const int nw128 = (we && we[0] == '8') ? 8 : 4;
+  const char* re = getenv("MXLLM_ATTN_FWD_RING");
+  const int ring = (re && re[0] == 'k' && re[1] == '3') ? -3 : ((re && (atoi(re) == 3 || atoi(re) == 4)) ? atoi(re) : 0);
+  const char* pe = getenv("MXLLM_ATTN_PROF");
+  if (nw128 == 4 && causal && pe && pe[0] == '1') {
     const unsigned grid = ((S + 127) / 128) * B * Hq;
     const size_t n = (size_t)grid * 4 * 16;
     uint32_t* pbuf = nullptr;
@@ -1184,10 +1160,7 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
             sm[0] / nt, sm[1] / nt, sm[2] / nt, sm[3] / nt, sm[5] / nt, sm[6] / nwv, sm[7] / nwv, nt / nwv);
     return (int)hipGetLastError();
   }
-#define FWDR(C, RR)                                                                                    \
-  attn_fwd_kernel<128, C, 8, false, RR><<<((S + 255) / 256) * B * Hq, 512, 0, stream>>>(                 \
-      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
-  if (D == 128 && ring == -3) {
+  if (ring == -3) {
     const unsigned grid = ((S + 127) / 128) * B * Hq;
     if (causal)
       attn_fwd_kernel<128, true, 4, false, 2, true><<<grid, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk, off,
@@ -1197,18 +1170,56 @@ extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t*
                                                                               off, sl, ldo, fflags);
     return (int)hipGetLastError();
   }
-  if (D == 128 && ring > 0) {
+#define FWDR(C, RR)                                                                                    \
+  attn_fwd_kernel<128, C, 8, false, RR><<<((S + 255) / 256) * B * Hq, 512, 0, stream>>>(                 \
+      q, k, v, o, lse, B, Hq, Hkv, S, Sk, off, sl, ldo, fflags)
+  if (ring > 0) {
     if (ring == 3) { if (causal) FWDR(true, 3); else FWDR(false, 3); }
     else { if (causal) FWDR(true, 4); else FWDR(false, 4); }
     return (int)hipGetLastError();
   }
 #undef FWDR
-  if (D == 128) {
-    if (nw128 == 8) { if (causal) FWD(128, true, 8); else FWD(128, false, 8); }
-    else { if (causal) FWD(128, true, 4); else FWD(128, false, 4); }
+  if (nw128 == 8) {
+    if (causal)
+      attn_fwd_kernel<128, true, 8><<<((S + 255) / 256) * B * Hq, 512, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk,
+                                                                                    off, sl, ldo, fflags);
+    else
+      attn_fwd_kernel<128, false, 8><<<((S + 255) / 256) * B * Hq, 512, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, Sk,
+                                                                                     off, sl, ldo, fflags);
+    return (int)hipGetLastError();
   }
-  else if (D == 64) { if (causal) FWD(64, true, 4); else FWD(64, false, 4); }
-  else if (D == 32) { if (causal) FWD(32, true, 4); else FWD(32, false, 4); }
+  return 1;
+}
+#endif  // MXLLM_ATTN_EXPERIMENTS
+}  // namespace mx
+
+using namespace mx;
+
+// o: token-major [B, S, Hq*D] rows with row stride ldo (elements, >= Hq*D): the rows may
+// be the left part of the LoRA-augmented o-projection input (mxllm/ops/linear.py)
+extern "C" int mx_attn_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int B,
+                           int Hq, int Hkv, int S, int Sk, int D, int causal, float scale, int ldo,
+                           hipStream_t stream) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv || ldo < Hq * D || ldo % 8) return -1;
+  const float sl = scale * 1.4426950408889634f;
+  const int off = Sk - S;
+  static const int fflags = [] {  // MXLLM_ATTN_FWD_FLAGS (default 1): bit 0 = spread the K/V DMA issue
+    const char* e = getenv("MXLLM_ATTN_FWD_FLAGS");   // (B2 0.192 -> 0.186 ms, B16 1.372 -> 1.357 ms)
+    return e && *e ? atoi(e) : 1;
+  }();
+#ifdef MXLLM_ATTN_EXPERIMENTS
+  if (D == 128) {
+    const int rc = attn_fwd_experiment(q, k, v, o, lse, B, Hq, Hkv, S, Sk, causal, off, sl, ldo, fflags, stream);
+    if (rc != 1) return rc;  // 1: no experiment selected
+  }
+#endif
+#define FWD(DD, C)                                                                                       \
+  attn_fwd_kernel<DD, C, 4><<<((S + 127) / 128) * B * Hq, 256, 0, stream>>>(q, k, v, o, lse, B, Hq, Hkv, S, \
+                                                                             Sk, off, sl, ldo, fflags)
+  if (D == 128) { if (causal) FWD(128, true); else FWD(128, false); }
+  else if (D == 64) { if (causal) FWD(64, true); else FWD(64, false); }
+  else if (D == 32) { if (causal) FWD(32, true); else FWD(32, false); }
   else return -1;
 #undef FWD
   return (int)hipGetLastError();

@@ -193,8 +193,8 @@ extern "C" int mx_w8a16_gemm(const uint16_t* x, int64_t ldx, const uint8_t* q, c
   if (M > 32 || N % 16 || K % 512 || ldx % 8 || ldy % 4 || ldx < K || ldy < N) return -1;
   // two channel groups per wave for 6..16 tokens when that still leaves >= 256 workgroups
   // (70B fp8 decode step, one group -> two: 22.0 -> 21.1 ms at 8 tokens, but 18.5 -> 19.3 ms
-  // at 4; profiles/r1g_fp8_decode_ab.md), and for 4..5 tokens on the long-K projections
-  // (70B down, 4 tokens: 50.8 -> 44.1 us; profiles/r4x/).
+  // at 4; archive/profiles/r1g_fp8_decode_ab.md), and for 4..5 tokens on the long-K projections
+  // (70B down, 4 tokens: 50.8 -> 44.1 us; archive/profiles/r4x/).
   // Effective routing: mxllm/serve/quant.py sends calls of more than SMALL_M (8) tokens to
   // hipBLASLt's fp8 GEMM, so from Python the two-group variant runs at 6..8 tokens; 9..16
   // reach it only through a direct w8_linear call (or MXLLM_W8_SMALL_M=16).

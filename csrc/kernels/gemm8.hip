@@ -8,7 +8,7 @@
 //   input gr dX = dY W   : A = dY [T][out] (k-contiguous), B = W [out][in] = [k][n] (n-contiguous)
 //   weight gr dW = dY^T X: A = dY [T][out] = [k][m] (m-contiguous), B = X [T][in] = [k][n]
 // ("NN"-form dX ran at ~1.32 PF in hipBLASLt; token-major dW needed 6.8 / 73 ms of transposes
-// per 8B / 70B-ZeRO-3 step, profiles/r3o, r3p, r3d).
+// per 8B / 70B-ZeRO-3 step, archive/profiles/r3o, r3p, r3d).
 //
 // Structure (CDNA guide §5 "The 256² 8-phase template", T1-T5, T10), designed here for the two
 // operand orders:
@@ -1304,6 +1304,17 @@ extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uin
   if (at <= 0 || rest <= 0 || (at & 255) || (rest & 255) || K < 2 * G8_BK) return -1;
   if ((a_kc ? lda < K : lda < M) || (b_kc ? ldb < K : ldb < N) || ldb % 8 || lda % 8 || ldc % 8) return -1;
   if (sq && (ph != 4 || (M & 255) || (N & 255))) return -1;  // partials: the 4-phase schedule, whole tiles
+  // every check of the split part BEFORE the plain part launches: a -1 after a launch would
+  // leave sq partials of a GEMM the caller then recomputes another way (a double-counted clip norm)
+  const uint16_t* A2 = rows ? (a_kc ? A + (int64_t)at * lda : A + at) : A;
+  const uint16_t* B2 = rows ? B : (b_kc ? B + (int64_t)at * ldb : B + at);
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)A2 | (uintptr_t)B2 | (uintptr_t)ws) & 15) return -1;
+  if ((a_kc || b_kc) && (K % G8_BK)) return -1;
+  {
+    const int64_t kpad = (int64_t)((K + G8_BK - 1) / G8_BK) * G8_BK;
+    const int64_t aspan = a_kc ? 256 * lda : kpad * lda, bspan = b_kc ? 256 * ldb : kpad * ldb;
+    if (aspan * 2 >= ((int64_t)1 << 31) || bspan * 2 >= ((int64_t)1 << 31) || ldc < N) return -1;
+  }
   // plain part (sq: its tiles' partials first, then the split part's)
   int rc;
   if (sq)
@@ -1313,12 +1324,9 @@ extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uin
     rc = rows ? mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, at, N, K, 0.f, nullptr, 1.f, ph, stream)
               : mx_gemm8(A, lda, a_kc, B, ldb, b_kc, C, ldc, 0, M, at, K, 0.f, nullptr, 1.f, ph, stream);
   if (rc) return rc;
-  const uint16_t* A2 = rows ? (a_kc ? A + (int64_t)at * lda : A + at) : A;
-  const uint16_t* B2 = rows ? B : (b_kc ? B + (int64_t)at * ldb : B + at);
   uint16_t* C2 = rows ? C + (int64_t)at * ldc : C + at;
   const int M2 = rows ? rest : M, N2 = rows ? N : rest;
   const int k0 = (K / G8_BK / 2) * G8_BK;  // part 0: floor(K-tiles / 2) tiles
-  if (((uintptr_t)A2 | (uintptr_t)B2 | (uintptr_t)ws) & 15) return -1;
   const int64_t part = (int64_t)M2 * N2;
   const dim3 grid((M2 >> 8) * (N2 >> 8), 2);
   const char* phs = getenv("MXLLM_GEMM8_PH");

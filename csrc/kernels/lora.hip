@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float
     // narrow G (one 16-column block, 2 KiB per 64-row block): a stage is X 8 KiB + G 2 KiB, so the
     // wave's 32 KiB hold THREE stages -- two blocks in flight behind the one being read instead of
     // one (~80 KiB of DMA in flight per CU, the HBM-latency cover of MI355X_MICROARCH §Indexed
-    // rows; with two stages these streams ran at ~3.6 TB/s, profiles/r4_final6)
+    // rows; with two stages these streams ran at ~3.6 TB/s, archive/profiles/r4_final6)
     constexpr int STN = XB + 2048;
     auto issue3 = [&](int b, int st) {
       const int64_t t0 = (int64_t)b * 64;
@@ -959,7 +959,7 @@ static int lora_splits(int tiles, int blocks, int smax) {
 // "lds" (default) = the 64-row LDS-DMA kernel, "reg" = the register-fragment kernel (both on all
 // 64 padded rows of V), "tile" = lora_xwt_tile_kernel (adapter rows only; needs M % 16, K % 128,
 // <= 64 adapter rows, 16-B aligned rows).  The tile kernel measured 3-7 us SLOWER on the 64-84 MB
-// calls of the 70B step (profiles/r4i: those calls are bound by their fixed cost, not by bytes).
+// calls of the 70B step (archive/profiles/r4i: those calls are bound by their fixed cost, not by bytes).
 static int xwt_mode() {
   const char* kv = getenv("MXLLM_LORA_XWT");
   if (kv && !strcmp(kv, "reg")) return 2;

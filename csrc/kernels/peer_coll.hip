@@ -34,6 +34,13 @@
 // Reduction: fp32, in rank order 0..W-1 -> every rank computes the identical
 // bits for its chunk, and an all-reduce (RS + AG) is bitwise identical on all
 // ranks.
+//
+// Failure: once the error word is set, no collective result is
+// silently partial -- a launch that finds it set at entry, and a workgroup
+// whose spin timed out, fill the output they own with NaN (so nothing that
+// consumes it can look valid) and stop; the host side checks the word after
+// synchronising on the communicator's last collective before the optimizer
+// reads a result (mxllm/parallel/comm.py ``verify``).
 #include "common.h"
 
 namespace {
@@ -91,6 +98,15 @@ struct Vec<uint16_t> {
   }
 };
 
+// NaN over out [lo, hi) (16-B vectors), grid-strided with stride `step` vectors starting at `first`.
+template <typename T>
+__device__ __forceinline__ void poison(T* out, int64_t lo, int64_t hi, int64_t first, int64_t step) {
+  constexpr int V = Vec<T>::N;
+  const uint32_t w = sizeof(T) == 4 ? 0x7FC00000u : 0x7FC07FC0u;
+  const u32x4 nan = {w, w, w, w};
+  for (int64_t i = lo + first * V; i < hi; i += step * V) *reinterpret_cast<u32x4*>(out + i) = nan;
+}
+
 __device__ __forceinline__ uint32_t* flag_ptr(char* base, int g, int src) {
   return reinterpret_cast<uint32_t*>(base) + ((size_t)g * kMaxRanks + src) * kFlagStride;
 }
@@ -108,6 +124,11 @@ __global__ __launch_bounds__(256) void peer_coll_kernel(Bases P, const T* __rest
   const int g = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
   const int slot_elems = slot_bytes / (int)sizeof(T);
   const int64_t npieces = (m + slot_elems - 1) / slot_elems;
+  // a communicator already broken (a peer timed out earlier): poison, move nothing, keep the epochs
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+    poison(out, 0, MODE == 0 ? m : n, (int64_t)g * 256 + tid, (int64_t)G * 256);
+    return;
+  }
   uint32_t epoch = epochs[g];
   if (tid == 0) bad = 0;
   __syncthreads();
@@ -152,7 +173,20 @@ __global__ __launch_bounds__(256) void peer_coll_kernel(Bases P, const T* __rest
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (bad) break;
+    if (bad) {  // this workgroup's pieces from k on are never exchanged: poison them
+      for (int64_t q = k; q < npieces; q += G) {
+        const int64_t qo = q * (int64_t)slot_elems, qe = min(qo + (int64_t)slot_elems, m);
+        if (MODE == 0) {
+          poison(out, qo, qe, tid, 256);
+        } else {
+          for (int p = 0; p < world; ++p) {
+            const int64_t b0 = (int64_t)p * m;
+            poison(out, b0 + qo, min(b0 + qe, n), tid, 256);
+          }
+        }
+      }
+      break;
+    }
     // 4. consume the W slots of this piece (my own contribution straight from `in`)
     const T* mine = reinterpret_cast<const T*>(P.b[rank] + kFlagBytes + ((size_t)g * 2 + half) * world * slot_bytes);
     if (MODE == 0) {

@@ -1,7 +1,7 @@
 // bf16 weight-streaming GEMM for decode on gfx950: Y[M, N] = X[M, K] . W[N, K]^T with M <= 32
 // tokens (serving path, SURVEY §2.4 K14 neighbourhood).  A decode step reads every weight once;
 // for the small projections of an 8B model (34-117 MB) hipBLASLt's skinny solutions stream at
-// 1.7-4.5 TB/s (profiles/r2x_skinny_gemm.md), latency-bound: too few bytes in flight per CU.
+// 1.7-4.5 TB/s (archive/profiles/r2x_skinny_gemm.md), latency-bound: too few bytes in flight per CU.
 //
 // Same structure as the fp8 weight kernel (fp8_gemm.hip) without the dequantisation:
 //  * workgroup = 8 waves = 16 output channels; the waves split K in eight contiguous parts
@@ -264,7 +264,7 @@ extern "C" int mx_skinny_gemm(const uint16_t* x, int64_t ldx, const uint16_t* w,
   if (M > 32 || N % 16 || K % 512 || ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K || ldy < N) return -1;
   // MXLLM_SKINNY_NC: channel groups per workgroup (1, 2 or 4; default 1).  Two or four groups
   // cut the X traffic but halve / quarter the workgroups; measured at the Llama 8B / 70B decode
-  // shapes they won only on the 8B qkv projection (profiles/r2x_skinny_gemm.md)
+  // shapes they won only on the 8B qkv projection (archive/profiles/r2x_skinny_gemm.md)
   static const int nc_env = [] {
     const char* e = getenv("MXLLM_SKINNY_NC");
     return e && *e ? atoi(e) : 0;

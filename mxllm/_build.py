@@ -98,6 +98,11 @@ def _attn_bwd_counted_wait_ok(asm: str) -> tuple[bool, str]:
                 kk -= 1
             if n < 4:
                 return False, f"{fn}: {n} vector-memory ops between the last LDS-DMA and the counted wait"
+    if found == 0:
+        # the counted-wait schedule is compiled in (the check runs only on that build) but no
+        # ``vmcnt(4) lgkmcnt(0)`` + barrier pair survived codegen (merged / reordered by the waitcnt
+        # pass): nothing was verified, so take the safe schedule
+        return False, "no counted wait found in the attn_bwd8 kernels (nothing verified)"
     return True, f"{found} counted waits checked"
 
 

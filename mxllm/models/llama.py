@@ -156,7 +156,7 @@ class FusedLinear(nn.Module):
 
 # LoRA projections that keep a transposed [W; A] image for the input-gradient GEMM
 # (FusedLinear.wxt): hipBLASLt's TN form instead of the ~15 % slower NN form, for one more
-# copy of W.  Measured 70B LoRA step, same box (profiles/r2n_dx_image_ab.md): qkv,o 1001.3 ms
+# copy of W.  Measured 70B LoRA step, same box (archive/profiles/r2n_dx_image_ab.md): qkv,o 1001.3 ms
 # (267.4 GB reserved) / qkv,d 990.8 ms (294.3 GB) / qkv,o,d 985.5 ms (305.3 GB of 309: too
 # little headroom for multi-GPU runs).  Default qkv + d.
 DX_IMAGE = tuple(x for x in os.environ.get("MXLLM_DX_IMAGE", "qkv,d").split(",") if x)

@@ -3,7 +3,7 @@
 VERDICT r4 item 5: in the 8B full fine-tune (BASELINE config 2) the forward's memory-bound
 passes -- RoPE + head split (``rope_split``) after the qkv projection, SwiGLU after the
 gate-up projection -- ran 3.6-11x off their rooflines because the overlapped AdamW saturates
-HBM beside them (profiles/r4g/step_breakdown_8b_full.txt).  Here the hand-written MFMA GEMM
+HBM beside them (archive/profiles/r4g/step_breakdown_8b_full.txt).  Here the hand-written MFMA GEMM
 (csrc/kernels/gemm8.hip, ``G8_EPI_ROPE`` / ``G8_EPI_SWIGLU``) applies them to its accumulators
 before the stores, so neither the [T, 6144] qkv activation nor a separate SwiGLU pass ever
 touches HBM:
@@ -47,12 +47,24 @@ def _norm_input(h: torch.Tensor, nw: torch.Tensor, eps: float) -> torch.Tensor:
     return native().rmsnorm_fwd(h.reshape(-1, h.shape[-1]).contiguous(), None, nw, eps, 0)[0]
 
 
+def _g8_operands_ok(a2: torch.Tensor, w: torch.Tensor) -> bool:
+    """What ``mx_gemm8_epi`` (csrc/kernels/gemm8.hip) checks of two k-contiguous operands beyond the
+    shapes: row strides in 16-B units, 16-B aligned bases, and both operand spans
+    (256 rows of A, all N rows of W) under 2^31 bytes -- so a predicate that says yes never meets a
+    declined launch (a 405B-class gate-up, 106,496 x 16,384, is over the span and stays unfused)."""
+    lda, ldb = a2.stride(0), w.stride(0)
+    return (lda % 8 == 0 and ldb % 8 == 0 and lda >= a2.shape[1] and ldb >= w.shape[1]
+            and a2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and 256 * lda * 2 < 2 ** 31 and w.shape[0] * ldb * 2 < 2 ** 31)
+
+
 def qkv_attention_ok(x: torch.Tensor, w: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, D: int) -> bool:
     """Shapes the fused qkv epilogue takes (full fine-tuning: no LoRA buffer)."""
     x2 = _x2(x)
     return (_ON and use_native(x2) and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and D == 128
             and S % 256 == 0 and x2.shape[0] == B * S and x2.shape[1] % 64 == 0 and x2.stride(1) == 1
-            and w.stride(1) == 1 and w.shape[0] == (Hq + 2 * Hkv) * D and not gemm.deterministic())
+            and w.stride(1) == 1 and w.shape[0] == (Hq + 2 * Hkv) * D and not gemm.deterministic()
+            and _g8_operands_ok(x2, w))
 
 
 class _QKVAttentionFn(torch.autograd.Function):
@@ -108,7 +120,7 @@ def gate_up_swiglu_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     x2 = _x2(x)
     return (_ON and use_native(x2) and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x2.shape[0] % 256 == 0 and x2.shape[1] % 64 == 0 and w.shape[0] % 256 == 0 and x2.stride(1) == 1
-            and w.stride(1) == 1 and not gemm.deterministic())
+            and w.stride(1) == 1 and not gemm.deterministic() and _g8_operands_ok(x2, w))
 
 
 class _GateUpSwiGLUFn(torch.autograd.Function):
@@ -168,7 +180,8 @@ def swiglu_bwd_gemm(dy: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor, want_m
 def gate_up_swiglu_down_ok(x: torch.Tensor, wgu: torch.Tensor, wd: torch.Tensor) -> bool:
     return (_BWD_ON and gate_up_swiglu_ok(x, wgu) and wd.dim() == 2 and wd.dtype == torch.bfloat16
             and 2 * wd.shape[1] == wgu.shape[0] and wd.shape[1] % 256 == 0 and wd.shape[0] % 64 == 0
-            and wd.stride(1) == 1)
+            and wd.stride(1) == 1 and wd.stride(0) % 8 == 0 and wd.data_ptr() % 16 == 0
+            and 256 * wd.shape[0] * 2 < 2 ** 31 and wd.shape[0] * wd.stride(0) * 2 < 2 ** 31)
 
 
 class _GateUpSwiGLUDownFn(torch.autograd.Function):

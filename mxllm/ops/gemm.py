@@ -15,7 +15,7 @@ the CUs runs as twice as many half-K workgroups, e.g. the 16 x 40-tile 70B qkv f
 (``mxllm/tuning/gemm8_gfx950.json``, written from ``bench/gemm8_probe.py`` runs), or for every
 shape it takes in deterministic mode (``MXLLM_DETERMINISTIC=1``: one workgroup per output tile,
 a fixed K order, no split-K or atomics — the step is bitwise reproducible; vendor stream-K
-solutions are not, profiles/r3aa).  ``MXLLM_GEMM8=0`` disables it, ``=all`` forces it wherever
+solutions are not, archive/profiles/r3aa).  ``MXLLM_GEMM8=0`` disables it, ``=all`` forces it wherever
 it takes the shape (A/B runs).
 """
 from __future__ import annotations

@@ -277,7 +277,7 @@ def weight_grad_(out: torch.Tensor | None, dy: torch.Tensor, x: torch.Tensor, be
     token-contiguous images by the HIP transpose (4.4-6.4 TB/s) and the GEMM
     runs in the reduction-contiguous form the forward uses: dW = dyT @ xT^T,
     12-20 % faster including the transposes
-    (bench/dw_layout_probe.py, profiles/r1e_dw_layout_probe.md).
+    (bench/dw_layout_probe.py, archive/profiles/r1e_dw_layout_probe.md).
     ``dy_scale``: 1-element device tensor multiplying dy (folded into dy's
     transpose on that path; the cross-entropy's upstream gradient)."""
     f32 = out is not None and out.dtype == torch.float32 and dy.dtype != torch.float32
@@ -467,7 +467,7 @@ def normed_linear(x: torch.Tensor, h: torch.Tensor, nw: torch.Tensor, eps: float
 
 # decode-sized GEMMs (bf16, no autograd) on the weight-streaming HIP kernel
 # (csrc/kernels/skinny_gemm.hip) where it beat hipBLASLt inside the decode step
-# (bench/serve_bench.py A/B, profiles/r2x_skinny_gemm.md): one token row for every projection
+# (bench/serve_bench.py A/B, archive/profiles/r2x_skinny_gemm.md): one token row for every projection
 # and the LM head; 2..SKINNY_M rows for weights of <= 128 M elements (all Llama-3.1-8B
 # projections; the 70B ones lost at 4 rows).  MXLLM_SKINNY_M=0 keeps every GEMM on hipBLASLt.
 SKINNY_M = int(os.environ.get("MXLLM_SKINNY_M", "8"))
@@ -509,7 +509,7 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
 
 # rows up to which the RMSNorm runs in the decode GEMM's prologue (every workgroup recomputes the
 # rows): measured same box, 8B decode batch 1 3.607 -> 3.479 ms and 70B 26.22 -> 24.98 ms, but batch 4
-# 3.83 -> 4.04 ms (profiles/r2s3_decode_ab/); the kernel takes up to 4
+# 3.83 -> 4.04 ms (archive/profiles/r2s3_decode_ab/); the kernel takes up to 4
 NORM_M = int(os.environ.get("MXLLM_NORM_FUSED_M", "2"))
 
 

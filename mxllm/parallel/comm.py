@@ -108,6 +108,7 @@ class PeerCollectives:
                                                self.timeout_s)
         self.stream = torch.cuda.Stream(device)
         self._broken = False
+        self._last = None  # event of the last collective issued (sync_check)
 
     # ------------------------------------------------------------------ bootstrap
     def handle(self) -> list[int]:
@@ -159,6 +160,7 @@ class PeerCollectives:
             fn()
             ev = torch.cuda.Event()
             ev.record(self.stream)
+        self._last = ev
         for t in tensors:
             t.record_stream(self.stream)  # the allocator keeps it until the comm stream is past it
         w = PeerWork(ev, self)
@@ -241,15 +243,41 @@ class PeerCollectives:
         self.all_reduce(t)
 
     def check(self):
-        if self._c.error():
+        """Raise if any collective so far timed out.  Non-blocking: it sees a timeout of a
+        collective that has already RUN; ``sync_check`` first waits for the last one."""
+        if self._broken or self._c.error():
             self._broken = True
-            raise RuntimeError("peer-memory collective timed out waiting for a peer (MXLLM_PEER_TIMEOUT_S)")
+            raise RuntimeError("peer-memory collective timed out waiting for a peer (MXLLM_PEER_TIMEOUT_S); "
+                               "the communicator is broken and its outputs since then are NaN")
+
+    def sync_check(self):
+        """Host-wait for the last collective issued, then ``check``: called before the optimizer
+        consumes reduced gradients (DDP / ZeRO-1 ``finish``, ZeRO-3's step), so a timed-out
+        exchange stops training with an error instead of feeding AdamW or a checkpoint."""
+        if self._last is not None:
+            self._last.synchronize()
+        self.check()
 
     def close(self):
         try:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
         finally:
             self._c.close()
+
+
+def verify(*comms) -> None:
+    """Before state is updated from collective results: for every peer-memory communicator
+    among ``comms``, wait for its last collective and raise if a peer timed out.
+    RCCL / gloo communicators report their own failures (watchdog / exceptions): no-op.
+    ``MXLLM_PEER_SYNC_CHECK=0`` skips the host wait (the error then surfaces at a later wait)."""
+    if os.environ.get("MXLLM_PEER_SYNC_CHECK", "1") == "0":
+        return
+    seen = set()
+    for c in comms:
+        f = getattr(c, "sync_check", None)
+        if f is not None and id(c) not in seen:
+            seen.add(id(c))
+            f()
 
 
 def peer_eligible(group=None, device: torch.device | None = None) -> bool:

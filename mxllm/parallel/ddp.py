@@ -75,6 +75,9 @@ class DDP:
             del end
         self._timing = self.enabled
         self._last_events = None
+        # buckets whose all-reduce a gradient hook issued DURING the backward in the last
+        # step (the rest were issued by finish(): unused parameters, or a broken overlap)
+        self.fired_in_backward = 0
         self._hooks = []
         self.on_ready = None  # callback(bucket) once a bucket's gradient is final (set_on_ready)
         if self.enabled:
@@ -140,6 +143,7 @@ class DDP:
     def finish(self) -> float:
         """Wait for every bucket (launching any whose hooks did not all fire, e.g.
         unused params) and return the gradient scale (1/world) to apply."""
+        self.fired_in_backward = sum(b.fired for b in self.buckets)
         if not self.enabled and self.on_ready is None:
             return 1.0
         for b in self.buckets:
@@ -162,6 +166,9 @@ class DDP:
         if timing:
             e1.record()
             self._last_events = (e0, e1)
+        from .comm import verify
+
+        verify(self.comm)  # peer path: a timed-out bucket stops the step here, before AdamW
         return 1.0 / self.world
 
     def exposed_comm_ms(self) -> float | None:

@@ -113,6 +113,9 @@ class Zero1(DDP):
         if timing:
             e1.record()
             self._last_events = (e0, e1)
+        from .comm import verify
+
+        verify(self.comm)  # peer path: a timed-out exchange stops the step before AdamW reads the shard
         return 1.0 / self.world
 
     # ------------------------------------------------------------ parameters

@@ -737,6 +737,10 @@ class Zero3Trainer:
                 u.grad_shard.zero_()
             u.grad_written = False
         scale = 1.0 / (self.world * n)
+        if self.comm.real:
+            from .comm import verify
+
+            verify(self.comm.rs, self.comm.ag)  # peer path: a timed-out exchange stops here, before AdamW
         self.step_num += 1
         o = self.opt
         if o.grad_clip and o.grad_clip > 0:

@@ -49,12 +49,12 @@ _ROPE_FUSED = os.environ.get("MXLLM_ROPE_FUSED", "1") != "0"  # A/B switch: RoPE
 # the split-K attention merge in the o-projection GEMM's prologue (decode rows <= 4): OFF by
 # default -- measured 8B decode, same box: batch 1 3.424 vs 3.433 ms (a wash), batch 4 4.113 vs
 # 3.841 ms (the prologue slows the weight stream more than the combine launch costs;
-# profiles/r3d_decode_merge_ab.md).  MXLLM_MERGE_FUSED=1 turns it on.
+# archive/profiles/r3d_decode_merge_ab.md).  MXLLM_MERGE_FUSED=1 turns it on.
 _MERGE_FUSED = os.environ.get("MXLLM_MERGE_FUSED", "0") == "1"
 # Small-batch decode: while the (latency-bound) attention runs, a side-stream kernel reads
 # the layer's o-projection weight so the o-projection GEMM streams it from the Infinity
 # Cache instead of HBM (MXLLM_DECODE_PREFETCH=1; up to PREFETCH_MAX_B rows).  Measured
-# slower (fork/join + competing reads; profiles/r3g/README.md): off by default.
+# slower (fork/join + competing reads; archive/profiles/r3g/README.md): off by default.
 _PREFETCH = os.environ.get("MXLLM_DECODE_PREFETCH", "0") == "1"
 PREFETCH_MAX_B = 8
 log = logging.getLogger("mxllm.engine")
@@ -146,7 +146,7 @@ class Engine:
         # MXLLM_DECODE_COMBINE=fused: the split-K partials merge inside the attention launch (the
         # last workgroup of each (seq, kv-head) combines; these counters stay zero between calls)
         # instead of the combine kernel -- measured slower in the graphed step at every batch
-        # (profiles/r3g/README.md), so off by default
+        # (archive/profiles/r3g/README.md), so off by default
         self._attn_cnt = None
         if self.device.type == "cuda" and os.environ.get("MXLLM_DECODE_COMBINE", "kernel") == "fused":
             self._attn_cnt = torch.zeros((n_slots + 64) * self.kv.k[0].shape[1], dtype=torch.int32,

@@ -34,7 +34,7 @@ E4M3_MAX = 448.0
 # weights streamed once per call); larger calls quantise the activations per token too
 # and run hipBLASLt's fp8 MFMA GEMM (W8A8).  The threshold is aligned to the graphed
 # decode's power-of-two batch buckets (mxllm/serve/engine.py), which is where it was
-# measured (70B decode step, profiles/r1g_fp8_decode_ab.md): the 8-row bucket 21.1 ms on
+# measured (70B decode step, archive/profiles/r1g_fp8_decode_ab.md): the 8-row bucket 21.1 ms on
 # the HIP kernel vs 27.7 ms on hipBLASLt, the 16-row bucket (9..16 live sequences; the
 # profile's "12 tokens" row also ran 16-row GEMMs) 25.2 vs 24.6 ms.  Eager calls with 9..15
 # rows were not measured separately.  Decode accuracy of both routings at the 16-row

@@ -3,7 +3,7 @@
 ``MXLLM_DETERMINISTIC=1`` routes every GEMM of the step that the 8-phase MFMA kernel takes
 (csrc/kernels/gemm8.hip: one workgroup per output tile, a fixed K order, no split-K, no atomics)
 through it instead of hipBLASLt / rocBLAS, whose stream-K / atomic solutions made two identical
-runs diverge (profiles/r3aa).  Every other kernel of the step is already fixed-order (attention's
+runs diverge (archive/profiles/r3aa).  Every other kernel of the step is already fixed-order (attention's
 default split backward, sorted embedding backward, fixed-order norms / CE / grad norm, elementwise
 AdamW).  Two from-scratch Llama-3.2-1B full fine-tunes must then agree bitwise: every step's loss
 and every final weight.

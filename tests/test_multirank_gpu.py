@@ -16,11 +16,16 @@ bootstrap (handle exchange, desync checksums).
   that need padding, two communicators in flight at once, uneven arrival,
   inputs dropped right after an async call (the allocator must not hand their
   memory out before the collective is done), the bounded-spin timeout;
-* trainer level: the DDP trainer (full fine-tune, overlapped AdamW) and the
-  ZeRO-3 trainer (split communicators, overlapped per-unit AdamW, gradient
+* trainer level: the DDP trainer (full fine-tune, overlapped AdamW), the
+  headline's own path — LoRA DDP, whose fused kernels write dA / dB straight
+  into the flat buffer and launch buckets through ``mark_ready`` — ZeRO-1 and
+  the ZeRO-3 trainer (split communicators, overlapped per-unit AdamW, gradient
   accumulation 2, one checkpointed layer) at world 2 and 4 equal the world-1
   run over the same micro-batches per parameter, and the replicas pass
-  ``check_in_sync`` after 5 steps.
+  ``check_in_sync`` after 5 steps.  DDP and LoRA run with buckets small enough
+  that >= 4 all-reduces fire DURING the backward, and every parameter's reduced
+  gradient of the first 3 steps is compared with the world-1 gradient (a dropped
+  or stale bucket is off by O(1), summation order by ~1e-3).
 Reference: /root/reference/docs/troubleshooting.md:55-63 (nodes out of sync);
 /root/reference/README.md:7,9 (DDP over NCCL).
 """
@@ -140,12 +145,19 @@ def _coll_worker(rank, world, port, q):
             a._c.set_timeout(0.5)
             t = torch.ones(64, device=dev)
             a.all_reduce(t, async_op=True)
-            torch.cuda.synchronize()
-            try:
-                a.all_reduce(torch.ones(64, device=dev), async_op=True).wait()
+            try:  # the host check the trainers run before AdamW (comm.verify)
+                a.sync_check()
                 out["timeout_raised"] = False
             except RuntimeError:
                 out["timeout_raised"] = True
+            # nothing partial survives: the timed-out reduce-scatter poisons its pieces and the
+            # all-gather behind it, finding the error word set, fills the whole output with NaN
+            out["poisoned"] = bool(torch.isnan(t).all())
+            try:  # a broken communicator refuses further collectives
+                a.all_reduce(torch.ones(64, device=dev), async_op=True).wait()
+                out["refused"] = False
+            except RuntimeError:
+                out["refused"] = True
         dist.barrier()
         runtime.cleanup()
     except Exception as e:  # noqa: BLE001
@@ -163,13 +175,14 @@ def test_peer_collectives_exact_on_shared_gpu(gpu, world):
     for r in range(world):
         assert "exc" not in res[r], res[r]["exc"]
         assert res[r]["kinds"] == ("peer", "peer") and res[r]["ok"] and res[r]["identical"], res[r]
-    assert res[0]["timeout_raised"], res[0]
+    assert res[0]["timeout_raised"] and res[0]["poisoned"] and res[0]["refused"], res[0]
 
 
 # ---------------------------------------------------------------------------- trainer level
 
 
 STEPS = 5
+GRAD_STEPS = 3
 
 
 def _batches(cfg, world, steps, per_rank, seq):
@@ -194,12 +207,31 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
         cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
         opt = OptimConfig(lr=1e-3, grad_clip=1.0, weight_decay=0.01)
         seq = 128
-        if mode in ("ddp", "zero1"):
-            model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=1234)
-            tr = Trainer(model, env, opt, shard_optimizer=mode == "zero1")
+        if mode in ("ddp", "zero1", "lora"):
+            lora = mode == "lora"
+            model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=1234, lora_r=16 if lora else 0)
+            if lora:  # non-zero B: every adapter gets a gradient (dA = (s dy B)^T x)
+                with torch.no_grad():
+                    for i, mod in enumerate(model.modules()):
+                        if getattr(mod, "lora_r", 0):
+                            for blk in mod.lora_b_blocks():
+                                blk.copy_(torch.randn(blk.shape, generator=torch.Generator().manual_seed(i)) * 0.02)
+            # many small buckets: >= 4 all-reduces issued from gradient hooks during the backward
+            bkw = {"ddp": dict(bucket_mb=2.0, first_bucket_mb=0.5), "lora": dict(bucket_mb=0.15, first_bucket_mb=0.05),
+                   "zero1": {}}[mode]
+            tr = Trainer(model, env, opt, shard_optimizer=mode == "zero1", **bkw)
             # ZeRO-1: sharded AdamW, then the all-gathers the next forward waits on per layer
-            out["overlap"] = tr.overlap_optimizer if mode == "ddp" else (tr.zero1 is not None) == (world > 1)
+            out["overlap"] = (tr.overlap_optimizer if mode == "ddp" else
+                              (tr.zero1 is not None) == (world > 1) if mode == "zero1" else True)
             out["comm"] = getattr(tr.ddp.comm, "kind", None)
+            out["n_buckets"] = len(tr.ddp.buckets)
+            if lora:  # the rank-r products run on the HIP kernels (lora_grads + mark_ready), not hipBLASLt
+                from mxllm.ops.linear import _lora_native
+
+                lin = model.layers[0].wqkv
+                x = torch.empty(2 * seq, cfg.hidden, dtype=torch.bfloat16, device=dev)
+                out["native_lora"] = _lora_native(x, sum(lin.splits), cfg.hidden, lin.splits, lin.lora_r,
+                                                  getattr(lin, "wbt", None))
             per_rank = 2
         else:
             from mxllm.parallel.zero3 import Zero3Trainer
@@ -210,14 +242,27 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
             out["split"] = tr.comm.real and tr.comm.rs is not tr.comm.ag
             per_rank = 2  # two micro-batches of 1 sequence: gradient accumulation 2
         data = _batches(cfg, ref_world, STEPS, per_rank, seq)
-        losses = []
+        losses, grads, fired = [], [], []
         for s in range(STEPS):
             ranks = range(ref_world) if world == 1 else [rank]
             if mode != "zero3":
                 mbs = [(data[s][r].to(dev), data[s][r].to(dev)) for r in ranks]
             else:
                 mbs = [(data[s][r][i:i + 1].to(dev), data[s][r][i:i + 1].to(dev)) for r in ranks for i in range(2)]
-            losses.append(tr.train_step(mbs))
+            if mode in ("ddp", "lora") and s < GRAD_STEPS:
+                # Trainer._train_step split open: the reduced gradient is read between the
+                # backward (+ bucket all-reduces) and the optimizer step
+                total, scale = tr.compute_grads(mbs)
+                fired.append(tr.ddp.fired_in_backward)
+                g = tr.flat.grads
+                grads.append({sl.name: (g[sl.offset:sl.offset + sl.numel].float() * scale).cpu().numpy().copy()
+                              for sl in tr.flat.slots})
+                tr.step_num += 1
+                tr._optimizer_step(scale)
+                losses.append(total / len(mbs))
+            else:
+                losses.append(tr.train_step(mbs))
+        out["fired"] = fired
         losses = [float(x) for x in losses]
         if mode != "zero3":
             tr.params_ready()
@@ -232,6 +277,7 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
         out["losses"] = [t / world for t in tot]
         if rank == 0:
             out["master"] = {k: v.numpy().copy() for k, v in master.items()}
+            out["grads"] = grads
         runtime.cleanup()
     except Exception:  # noqa: BLE001
         import traceback
@@ -242,7 +288,7 @@ def _trainer_worker(rank, world, port, q, mode, ref_world):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode", ["ddp", "zero1", "zero3"])
+@pytest.mark.parametrize("mode", ["ddp", "lora", "zero1", "zero3"])
 def test_trainers_multirank_on_shared_gpu_match_world1(gpu, mode):
     ref = None
     for world in (2, 4):
@@ -255,8 +301,24 @@ def test_trainers_multirank_on_shared_gpu_match_world1(gpu, mode):
             assert res[r]["in_sync"], (world, r)
             if mode == "zero3":
                 assert res[r]["split"]
+            if mode in ("ddp", "lora"):
+                # every bucket's all-reduce was issued from a gradient hook during the backward
+                nb = res[r]["n_buckets"]
+                assert nb >= 4 and res[r]["fired"] == [nb] * GRAD_STEPS, (world, r, nb, res[r]["fired"])
+            if mode == "lora":
+                assert res[r]["native_lora"], "tiny-d128 LoRA must take the HIP lora_grads + mark_ready path"
         got = res[0]
-        assert r1["losses"][-1] < r1["losses"][0]  # it trains
+        if mode in ("ddp", "lora"):
+            for s_, (g1, gn) in enumerate(zip(r1["grads"], got["grads"])):
+                assert set(g1) == set(gn)
+                for n, a in g1.items():
+                    ref_norm = float((a.astype("float64") ** 2).sum()) ** 0.5
+                    err = float(((gn[n].astype("float64") - a) ** 2).sum()) ** 0.5
+                    # summation order (bf16 accumulation of 2 micro-batches vs the fp32 rank-ordered
+                    # sum) moves a gradient by ~1e-3 of its norm; a dropped / stale bucket by O(1)
+                    assert err <= 2e-2 * ref_norm + 1e-6, (world, s_, n, err, ref_norm)
+        if mode != "lora":  # rank-16 adapters on fresh uniform-random tokens barely move the loss in 5 steps:
+            assert r1["losses"][-1] < r1["losses"][0]  # it trains (LoRA: the per-step gradients above are the check)
         for x, y in zip(r1["losses"], got["losses"]):
             assert abs(x - y) < 3e-3 * max(1.0, abs(x)), (world, r1["losses"], got["losses"])
         assert set(r1["master"]) == set(got["master"])

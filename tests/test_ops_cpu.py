@@ -405,3 +405,26 @@ def test_swiglu_linear_recompute_matches_saved_activation(monkeypatch):
         assert abs(l0 - l1) < 1e-6
         for k in g0:
             torch.testing.assert_close(g1[k], g0[k], rtol=1e-5, atol=1e-6)
+
+
+def test_fused_epilogue_predicates_match_native_limits():
+    """the fused-epilogue predicates check what mx_gemm8_epi declines (strides,
+    alignment, the 2^31-byte operand spans), so a predicate that says yes is never met by a
+    declined launch; a 405B-class gate-up weight stays on the unfused path."""
+    from mxllm.ops.fused import _g8_operands_ok
+
+    x = torch.empty(4096, 8192, dtype=torch.bfloat16, device="meta")
+    assert _g8_operands_ok(x, torch.empty(57344, 8192, dtype=torch.bfloat16, device="meta"))  # 70B gate-up
+    assert not _g8_operands_ok(torch.empty(4096, 16384, dtype=torch.bfloat16, device="meta"),
+                               torch.empty(106496, 16384, dtype=torch.bfloat16, device="meta"))
+    assert not _g8_operands_ok(torch.empty(4096, 8196, dtype=torch.bfloat16, device="meta")[:, :8192],
+                               torch.empty(57344, 8192, dtype=torch.bfloat16, device="meta"))  # lda % 8
+
+
+def test_counted_wait_isa_check_fails_closed():
+    """an assembly with no counted wait left is NOT a pass."""
+    from mxllm._build import _attn_bwd_counted_wait_ok
+
+    asm = "_ZN2mx16attn_bwd8_kernelILi1EEEvv:\n s_waitcnt vmcnt(0)\n s_barrier\n.Lfunc_end0:\n"
+    ok, detail = _attn_bwd_counted_wait_ok(asm)
+    assert not ok and "nothing verified" in detail
