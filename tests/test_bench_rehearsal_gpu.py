@@ -42,6 +42,8 @@ def test_bench_two_rank_flow_on_shared_gpu(gpu):
     with open(log, "w") as f:
         r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=f, text=True, timeout=400)
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    with open(os.path.join(ROOT, "gpurun_out", "bench_rehearsal.json"), "w") as f:
+        f.write(r.stdout)  # the one line, kept as evidence (profiles/r6_rehearsal/)
     tail = open(log).read()[-4000:]
     assert r.returncode == 0, tail
     assert len(lines) == 1, r.stdout[-3000:]
