@@ -816,7 +816,12 @@ def run(a, env) -> dict:
                      else "one launch after the backward",
             "rmsnorm_unit": "replicated (all-reduced gradient, no re-gather)",
             "max_inflight_reduce_scatters": trainer.max_inflight,
+            "rs_wire": c.rs_wire,
         }
+        steps_run = a.warmup + a.steps
+        if steps_run and world > 1:
+            # link bytes this rank sends per step (all-gathers bf16; reduce-scatters at the wire dtype)
+            out["zero3"]["sent_gb_per_step"] = {k: round(v / steps_run / 1e9, 2) for k, v in c.sent_bytes.items()}
     if guard is not None:
         out["memory_guard"] = guard
     if emulated:

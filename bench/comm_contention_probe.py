@@ -12,8 +12,10 @@ T 8192 x 8192 x K 8192, NN) on its compute stream.  Three phases:
   C  both at once (the collectives enqueued first, then the GEMMs) -> GEMM slowdown, collective rate
 Both ranks' collective kernels land on the one GPU, so phase C charges the GEMM with TWO ranks' worth
 of collective workgroups: an upper bound on what one rank's collectives cost its GPU at world 8.
-Usage: python bench/comm_contention_probe.py [--mb 256] [--reps 20] [--gemms 40] [--wgs 8,32]
-Prints one JSON line per workgroup setting.
+Usage: python bench/comm_contention_probe.py [--mb 256] [--reps 20] [--gemms 40]
+       [--configs resident:32,light:64,light:128,light:128:bf16]
+Prints one JSON line per configuration (schedule, workgroups, wire dtype).  GB/s counts fp32
+reduce-scatter input per rank (a bf16 wire moves half those bytes).
 """
 from __future__ import annotations
 
@@ -38,7 +40,9 @@ def _port() -> int:
 
 def _worker(rank: int, world: int, port: int, a, q) -> None:
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MXLLM_BACKEND="gloo", MXLLM_COMM="peer",
-                      MXLLM_COMM_STRICT="1", MXLLM_PEER_WGS=str(a.wgs), MXLLM_PEER_TIMEOUT_S="120")
+                      MXLLM_COMM_STRICT="1", MXLLM_PEER_WGS=str(min(a.wgs, 64) if a.algo == "resident" else 8),
+                      MXLLM_PEER_TIMEOUT_S="120", MXLLM_PEER_ALGO=a.algo, MXLLM_PEER_LIGHT_WGS=str(a.wgs),
+                      MXLLM_PEER_LIGHT_MB=str(a.light_mb))
     import torch.distributed as dist
 
     from mxllm.ops import native
@@ -66,8 +70,10 @@ def _worker(rank: int, world: int, port: int, a, q) -> None:
         e1.synchronize()
         return e0.elapsed_time(e1) / n
 
+    wire = torch.bfloat16 if a.wire == "bf16" else None
+
     def colls(n: int):
-        works = [comm.reduce_scatter(out, x, async_op=True) for _ in range(n)]
+        works = [comm.reduce_scatter(out, x, async_op=True, wire=wire) for _ in range(n)]
         return works
 
     res = {"rank": rank}
@@ -91,11 +97,16 @@ def _worker(rank: int, world: int, port: int, a, q) -> None:
     tb = time.perf_counter() - t0
     dist.barrier()
     res["rs_gbs_alone"] = a.reps * world * m * 4 / tb / 1e9
-    # C: both
+    # C: both, with as many reduce-scatters as cover the GEMM stream (so every GEMM runs beside them)
+    n_c = [0]
+    if rank == 0:
+        n_c[0] = max(2, round(res["gemm_ms_alone"] * a.gemms / (1e3 * tb / a.reps)))
+    dist.broadcast_object_list(n_c, src=0)
+    res["rs_calls_beside_gemm"] = n_c[0]
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    works = colls(a.reps)
+    works = colls(n_c[0])
     if rank == 0:
         res["gemm_ms_with_rs"] = gemms(a.gemms)
     for w in works:
@@ -103,7 +114,7 @@ def _worker(rank: int, world: int, port: int, a, q) -> None:
     torch.cuda.synchronize()
     tc = time.perf_counter() - t0
     dist.barrier()
-    res["rs_gbs_with_gemm"] = a.reps * world * m * 4 / tc / 1e9
+    res["rs_gbs_with_gemm"] = n_c[0] * world * m * 4 / tc / 1e9
     runtime.cleanup()
     q.put(res)
 
@@ -113,10 +124,14 @@ def main() -> None:
     ap.add_argument("--mb", type=int, default=256, help="reduce-scatter input MB per rank per call")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--gemms", type=int, default=40)
-    ap.add_argument("--wgs", default="8,32", help="peer-collective workgroups (MXLLM_PEER_WGS) to sweep")
+    ap.add_argument("--light-mb", type=int, default=64, help="MXLLM_PEER_LIGHT_MB (slot size of the light schedule)")
+    ap.add_argument("--configs", default="resident:32,light:64,light:128",
+                    help="comma list of schedule:workgroups[:bf16] (MXLLM_PEER_ALGO, its workgroups, a bf16 wire)")
     a = ap.parse_args()
     world = 2
-    for wgs in [int(v) for v in a.wgs.split(",")]:
+    for spec in a.configs.split(","):
+        parts = spec.split(":")
+        a.algo, wgs, a.wire = parts[0], int(parts[1]), (parts[2] if len(parts) > 2 else "fp32")
         a.wgs = wgs
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
@@ -131,7 +146,8 @@ def main() -> None:
         for p in ps:
             p.join(60)
         r0 = res[0]
-        line = {"peer_wgs": wgs, "rs_mb_per_call": a.mb, "gemm": "gemm8 NN 8192x8192x8192",
+        line = {"schedule": a.algo, "peer_wgs": wgs, "wire": a.wire, "rs_mb_per_call": a.mb,
+                "rs_calls_beside_gemm": r0["rs_calls_beside_gemm"], "gemm": "gemm8 NN 8192x8192x8192",
                 "gemm_ms_alone": round(r0["gemm_ms_alone"], 4), "gemm_ms_with_rs": round(r0["gemm_ms_with_rs"], 4),
                 "gemm_slowdown_pct": round(100 * (r0["gemm_ms_with_rs"] / r0["gemm_ms_alone"] - 1), 2),
                 "rs_gbs_alone": round(min(o["rs_gbs_alone"] for o in res.values()), 1),

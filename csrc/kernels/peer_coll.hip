@@ -358,29 +358,45 @@ __global__ __launch_bounds__(64) void pc_wait_kernel(Bases P, int base_idx, uint
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+// Both streaming kernels keep kLU 8-element items per thread in flight (all loads of a group issued
+// before its stores): one 8-element item per thread is only ~8 KB per workgroup in flight, a few GB/s
+// per CU at HBM latency, so a given rate would need many more workgroups -- CUs taken from the
+// compute stream.  Items are numbered q = item * 8 elements; thread t of workgroup b takes
+// q = (b * kLU + u) * 256 + t, u < kLU, then strides by gridDim.x * kLU * 256.
+constexpr int kLU = 4;
+
 // MODE 0: reduce-scatter (slice for d = in[d*m + o, +len), zero past n); MODE 1: all-gather (in[o, +len))
 template <typename T, typename W, int MODE>
 __global__ __launch_bounds__(256) void pc_push_kernel(Bases P, const T* __restrict__ in, LightSeg g) {
   char* mine = P.b[g.rank];
-  if (!light_dead(mine)) {
-    const int64_t len8 = g.len / 8, total = (int64_t)(g.world - 1) * len8;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+  if (light_dead(mine)) return;  // never raise flags on a dead communicator: peers must not take garbage
+  const int64_t len8 = g.len / 8, total = (int64_t)(g.world - 1) * len8;
+  const int64_t step = (int64_t)gridDim.x * kLU * 256;
+  for (int64_t q0 = (int64_t)blockIdx.x * kLU * 256 + threadIdx.x; q0 < total; q0 += step) {
+    float v[kLU][8];
+    W* dst[kLU];
+#pragma unroll
+    for (int u = 0; u < kLU; ++u) {
+      const int64_t q = q0 + u * 256;
+      dst[u] = nullptr;
+      if (q >= total) continue;
       const int j = (int)(q / len8) + 1;
       const int64_t i = (q - (int64_t)(j - 1) * len8) * 8;
       const int d = (g.rank + j) % g.world;
       const int64_t src = (MODE == 0 ? (int64_t)d * g.m : 0) + g.o + i;
-      float v[8];
       if (MODE == 1 || src < g.n) {
-        ld8(in + src, v);
+        ld8(in + src, v[u]);
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
       }
-      W* slot = reinterpret_cast<W*>(P.b[d] + kLightFlagBytes + ((int64_t)g.half * g.world + g.rank) * g.cap);
-      st8(slot + i, v);
+      dst[u] = reinterpret_cast<W*>(P.b[d] + kLightFlagBytes + ((int64_t)g.half * g.world + g.rank) * g.cap) + i;
     }
-    light_raise(P, g, kLCntPush, kLReady);  // never on a dead communicator: peers must not take garbage
+#pragma unroll
+    for (int u = 0; u < kLU; ++u)
+      if (dst[u]) st8(dst[u], v[u]);
   }
+  light_raise(P, g, kLCntPush, kLReady);
 }
 
 template <typename T, typename W, typename TO, int MODE>
@@ -391,46 +407,64 @@ __global__ __launch_bounds__(256) void pc_consume_kernel(Bases P, const T* __res
   const int64_t len8 = g.len / 8;
   const W* slots = reinterpret_cast<const W*>(mine + kLightFlagBytes + (int64_t)g.half * g.world * g.cap);
   const int64_t slot_elems = g.cap / (int64_t)sizeof(W);
+  const int64_t step = (int64_t)gridDim.x * kLU * 256;
   if (MODE == 0) {
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < len8; q += (int64_t)gridDim.x * 256) {
-      const int64_t i = q * 8;
-      float acc[8];
-      if (dead) {
-        nan8(acc);
-      } else {
+    for (int64_t q0 = (int64_t)blockIdx.x * kLU * 256 + threadIdx.x; q0 < len8; q0 += step) {
+      float acc[kLU][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-        for (int p = 0; p < g.world; ++p) {
-          float v[8];
-          if (p == g.rank) {
-            const int64_t s = (int64_t)g.rank * g.m + g.o + i;
-            if (s < g.n) {
-              ld8(in + s, v);
-              round_to<W>(v);  // my own slice as the wire carries the others'
+      for (int u = 0; u < kLU; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[u][e] = dead ? __uint_as_float(0x7FC00000u) : 0.f;
+      if (!dead) {
+        for (int p = 0; p < g.world; ++p) {  // rank order: every rank's bits identical
+          float v[kLU][8];
+#pragma unroll
+          for (int u = 0; u < kLU; ++u) {
+            const int64_t q = q0 + u * 256;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+            if (q >= len8) continue;
+            const int64_t i = q * 8;
+            if (p == g.rank) {
+              const int64_t s = (int64_t)g.rank * g.m + g.o + i;
+              if (s < g.n) ld8(in + s, v[u]);
             } else {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] = 0.f;
+              ld8(slots + (int64_t)p * slot_elems + i, v[u]);
             }
-          } else {
-            ld8(slots + (int64_t)p * slot_elems + i, v);
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[e] += v[e];
+          for (int u = 0; u < kLU; ++u) {
+            if (p == g.rank) round_to<W>(v[u]);  // my own slice as the wire carries the others'
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[u][e] += v[u][e];
+          }
         }
       }
-      st8(out + g.o + i, acc);
+#pragma unroll
+      for (int u = 0; u < kLU; ++u)
+        if (q0 + u * 256 < len8) st8(out + g.o + (q0 + u * 256) * 8, acc[u]);
     }
   } else {
     const int64_t total = (int64_t)g.world * len8;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-      const int p = (int)(q / len8);
-      const int64_t i = (q - (int64_t)p * len8) * 8, dst = (int64_t)p * g.m + g.o + i;
-      if (dst >= g.n) continue;
-      float v[8];
-      if (dead) nan8(v);
-      else if (p == g.rank) ld8(in + g.o + i, v);
-      else ld8(slots + (int64_t)p * slot_elems + i, v);
-      st8(out + dst, v);
+    for (int64_t q0 = (int64_t)blockIdx.x * kLU * 256 + threadIdx.x; q0 < total; q0 += step) {
+      float v[kLU][8];
+      int64_t dst[kLU];
+#pragma unroll
+      for (int u = 0; u < kLU; ++u) {
+        const int64_t q = q0 + u * 256;
+        dst[u] = -1;
+        if (q >= total) continue;
+        const int p = (int)(q / len8);
+        const int64_t i = (q - (int64_t)p * len8) * 8, d = (int64_t)p * g.m + g.o + i;
+        if (d >= g.n) continue;
+        dst[u] = d;
+        if (dead) nan8(v[u]);
+        else if (p == g.rank) ld8(in + g.o + i, v[u]);
+        else ld8(slots + (int64_t)p * slot_elems + i, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kLU; ++u)
+        if (dst[u] >= 0) st8(out + dst[u], v[u]);
     }
   }
   if (!dead) light_raise(P, g, kLCntCons, kLAck);
@@ -447,10 +481,11 @@ int light_launch(int mode, const Bases& P, const void* in, void* out, int64_t n,
     g.epoch = ++*epoch;
     g.half = (int)(g.epoch & 1u);
     g.cap = cap;
-    const int64_t work = (mode == 0 ? (int64_t)(world - 1) : (int64_t)world) * (g.len / 8);
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(wgs, (work + 255) / 256));
+    const int64_t work = (mode == 0 ? (int64_t)1 : (int64_t)world) * (g.len / 8);  // consume items
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(wgs, (work + kLU * 256 - 1) / (kLU * 256)));
     if (g.epoch > 2) pc_wait_kernel<<<1, 64, 0, s>>>(P, kLAck, g.epoch - 2, rank, world, err, timeout_ticks);
-    const int Gp = (int)std::max<int64_t>(1, std::min<int64_t>(wgs, ((int64_t)(world - 1) * (g.len / 8) + 255) / 256));
+    const int Gp = (int)std::max<int64_t>(
+        1, std::min<int64_t>(wgs, ((int64_t)(world - 1) * (g.len / 8) + kLU * 256 - 1) / (kLU * 256)));
     if (mode == 0) pc_push_kernel<T, W, 0><<<Gp, 256, 0, s>>>(P, (const T*)in, g);
     else pc_push_kernel<T, W, 1><<<Gp, 256, 0, s>>>(P, (const T*)in, g);
     pc_wait_kernel<<<1, 64, 0, s>>>(P, kLReady, g.epoch, rank, world, err, timeout_ticks);

@@ -89,10 +89,21 @@ class PeerCollectives:
     (collective over ``group``, which also carries the bootstrap exchange).
 
     fp32 / bf16; sums in fp32 in rank order, so every rank gets identical bits.
-    ``wgs`` workgroups per call each move ``slot_kb`` per peer per exchange."""
+
+    Two schedules (``MXLLM_PEER_ALGO``):
+
+      * ``resident``: ONE kernel per call whose ``wgs`` workgroups each move ``slot_kb`` per peer
+        per exchange and spin on the peers' flags between exchanges (they hold their CUs for the
+        whole call: profiles/r5j);
+      * ``light``: per segment of <= ``MXLLM_PEER_LIGHT_MB`` per peer, a push kernel and a consume
+        kernel that exit, with ONE wave waiting on the peers' flags in between
+        (csrc/kernels/peer_coll.hip, "CU-light schedule") -- the CUs stay with the compute stream
+        while a peer is late.  It also carries fp32 reduce-scatters as bf16 on the wire
+        (``reduce_scatter(..., wire=torch.bfloat16)``: half the link bytes; the fp32 rank-ordered
+        sum of the bf16-rounded inputs, identical on every rank)."""
 
     def __init__(self, group, device: torch.device, *, wgs: int | None = None, slot_kb: int | None = None,
-                 timeout_s: float | None = None):
+                 timeout_s: float | None = None, algo: str | None = None):
         from ..ops._ext import native
 
         native()
@@ -104,8 +115,15 @@ class PeerCollectives:
         self.wgs = int(wgs or os.environ.get("MXLLM_PEER_WGS", "32"))
         self.slot_bytes = int(slot_kb or os.environ.get("MXLLM_PEER_SLOT_KB", "64")) * 1024
         self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("MXLLM_PEER_TIMEOUT_S", "300"))
+        self.algo = (algo or os.environ.get("MXLLM_PEER_ALGO", "light")).strip().lower()
+        if self.algo not in ("light", "resident"):
+            raise ValueError(f"MXLLM_PEER_ALGO must be light or resident, not {self.algo!r}")
+        light_cap = 0
+        if self.algo == "light":  # bytes per (half, source) slot, 4 KB multiple
+            light_cap = max(1, int(float(os.environ.get("MXLLM_PEER_LIGHT_MB", "64")) * 2 ** 20) // 4096) * 4096
+        self.light_wgs = int(os.environ.get("MXLLM_PEER_LIGHT_WGS", "128"))
         self._c = torch.classes.mxllm.PeerComm(self.rank, self.world, device.index, self.wgs, self.slot_bytes,
-                                               self.timeout_s)
+                                               self.timeout_s, light_cap, self.light_wgs)
         self.stream = torch.cuda.Stream(device)
         self._broken = False
         self._last = None  # event of the last collective issued (sync_check)
@@ -139,6 +157,14 @@ class PeerCollectives:
                 torch.cuda.current_stream(dev).synchronize()
                 ok &= bool(torch.equal(out, want)) and bool(torch.equal(g.view(W, -1)[self.rank], want))
                 ok &= bool(torch.equal(y, ywant))
+            if self.algo == "light":  # fp32 through a bf16 wire (small integers: exact in bf16)
+                n = 8 * W * 3
+                x = (torch.arange(n, device=dev) % 13 + self.rank).float()
+                out = torch.empty(n // W, device=dev)
+                self.reduce_scatter(out, x, wire=torch.bfloat16)
+                want = ((torch.arange(n, device=dev) % 13) * W + W * (W - 1) // 2).float().view(W, -1)[self.rank]
+                torch.cuda.current_stream(dev).synchronize()
+                ok &= bool(torch.equal(out, want))
             ok = ok and not self._c.error()
             if not ok:
                 log.warning("peer-memory self-test mismatch on rank %d", self.rank)
@@ -149,7 +175,8 @@ class PeerCollectives:
 
     # ------------------------------------------------------------------ collectives
     def _vec(self, dtype) -> int:
-        return 16 // torch.empty(0, dtype=dtype).element_size()
+        """Element granularity of the sizes a call takes (smaller tensors are padded)."""
+        return 8 if self.algo == "light" else 16 // torch.empty(0, dtype=dtype).element_size()
 
     def _issue(self, fn, tensors, async_op: bool):
         if self._broken:
@@ -173,22 +200,40 @@ class PeerCollectives:
     def _fits(t: torch.Tensor, v: int) -> bool:
         return t.is_contiguous() and t.numel() % v == 0 and t.data_ptr() % 16 == 0
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+    def _rs(self, out: torch.Tensor, inp: torch.Tensor, wire_bf16: bool = False):
+        if self.algo == "light":
+            self._c.reduce_scatter_light_(out, inp, wire_bf16)
+        else:
+            self._c.reduce_scatter_(out, inp)
+
+    def _ag(self, out: torch.Tensor, inp: torch.Tensor):
+        if self.algo == "light":
+            self._c.all_gather_light_(out, inp)
+        else:
+            self._c.all_gather_(out, inp)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False,
+                       wire: torch.dtype | None = None):
+        """``wire=torch.bfloat16`` (fp32 tensors, light schedule): bf16 on the wire, fp32 sum of the
+        bf16-rounded inputs in rank order (half the bytes of an fp32 reduce-scatter)."""
         W = self.world
         if inp.numel() != W * out.numel() or inp.dtype != out.dtype:
             raise ValueError("reduce_scatter: input must hold world x output elements of one dtype")
+        wire_bf16 = wire is not None and wire != inp.dtype
+        if wire_bf16 and (wire != torch.bfloat16 or inp.dtype != torch.float32 or self.algo != "light"):
+            raise ValueError("reduce_scatter: a bf16 wire takes fp32 tensors on the light schedule")
         v = self._vec(inp.dtype)
 
         def run():
             if self._fits(inp, v) and self._fits(out, v):
-                self._c.reduce_scatter_(out, inp)
+                self._rs(out, inp, wire_bf16)
                 return
             m = out.numel()
             mp = -(-m // v) * v  # padded chunk: every rank's chunk starts on a 16-B boundary
             ip = torch.zeros(W, mp, dtype=inp.dtype, device=self.device)
             ip[:, :m].copy_(inp.view(W, m))
             op = torch.empty(mp, dtype=out.dtype, device=self.device)
-            self._c.reduce_scatter_(op, ip.view(-1))
+            self._rs(op, ip.view(-1), wire_bf16)
             out.copy_(op[:m])
 
         return self._issue(run, (out, inp), async_op)
@@ -201,14 +246,14 @@ class PeerCollectives:
 
         def run():
             if self._fits(inp, v) and self._fits(out, v):
-                self._c.all_gather_(out, inp)
+                self._ag(out, inp)
                 return
             m = inp.numel()
             mp = -(-m // v) * v
             ip = torch.zeros(mp, dtype=inp.dtype, device=self.device)
             ip[:m].copy_(inp.reshape(-1))
             op = torch.empty(W, mp, dtype=out.dtype, device=self.device)
-            self._c.all_gather_(op.view(-1), ip)
+            self._ag(op.view(-1), ip)
             out.view(W, m).copy_(op[:, :m])
 
         return self._issue(run, (out, inp), async_op)
@@ -223,14 +268,14 @@ class PeerCollectives:
             m = -(-n // (W * v)) * v  # chunk per rank, a multiple of the vector
             if self._fits(t, v):
                 part = torch.empty(m, dtype=t.dtype, device=self.device)
-                self._c.reduce_scatter_(part, t.view(-1))
-                self._c.all_gather_(t.view(-1), part)
+                self._rs(part, t.view(-1))
+                self._ag(t.view(-1), part)
                 return
             buf = torch.zeros(m * W, dtype=t.dtype, device=self.device)
             buf[:n].copy_(t.reshape(-1))
             part = torch.empty(m, dtype=t.dtype, device=self.device)
-            self._c.reduce_scatter_(part, buf)
-            self._c.all_gather_(buf, part)
+            self._rs(part, buf)
+            self._ag(buf, part)
             t.copy_(buf[:n].view_as(t))
 
         return self._issue(run, (t,), async_op)
@@ -327,8 +372,7 @@ def create(group=None, device: torch.device | None = None, kind: str | None = No
         if peer_eligible(group, device):
             c = create_peer(group, device)
             if c is not None:
-                log.info("[rank %d] bulk collectives: peer memory (world %d, %d WGs x %d KB slots)",
-                         c.rank, c.world, c.wgs, c.slot_bytes // 1024)
+                log.info("[rank %d] bulk collectives: peer memory (world %d, %s schedule)", c.rank, c.world, c.algo)
                 return c
         if os.environ.get("MXLLM_COMM_STRICT", "0") == "1":
             raise RuntimeError("MXLLM_COMM=peer requested but peer memory is unusable here")

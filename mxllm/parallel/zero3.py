@@ -164,6 +164,17 @@ class Comm:
 
             self.ag = comm_mod.create(ag_pg, device)
             self.rs = self.ag if rs_pg is ag_pg else comm_mod.create(rs_pg, device)
+        # MXLLM_Z3_RS_WIRE=bf16 (VERDICT r5 Missing 4): the fp32 gradient reduce-scatters travel as
+        # bf16 -- half the link bytes -- and are summed in fp32 in rank order at the owner (the
+        # peer-memory light schedule, mxllm/parallel/comm.py).  RCCL sums bf16 in bf16 hop by hop,
+        # so on the torch.distributed path the option is refused rather than silently weakened.
+        # The emulated proxy rounds its stand-in operands to bf16 the same way.
+        self.sent_bytes = {"ag": 0, "rs": 0}  # bytes this rank puts on its links (bench: per step)
+        self.rs_wire = os.environ.get("MXLLM_Z3_RS_WIRE", "fp32").strip().lower()
+        if self.rs_wire not in ("fp32", "bf16"):
+            raise ValueError(f"MXLLM_Z3_RS_WIRE must be fp32 or bf16, not {self.rs_wire!r}")
+        if self.rs_wire == "bf16" and self.real and getattr(self.rs, "algo", None) != "light":
+            raise RuntimeError("MXLLM_Z3_RS_WIRE=bf16 needs MXLLM_COMM=peer with the light schedule")
         # emulated world N: the local stand-ins (a broadcast copy for the all-gather, an N-way sum
         # for the reduce-scatter) run on the caller's stream by default -- every byte of them on
         # the critical path, a conservative proxy.  MXLLM_Z3_EMUL_ASYNC=1 issues the async ones
@@ -200,18 +211,32 @@ class Comm:
         return getattr(self.ag, "kind", "none")
 
     def all_gather(self, full: torch.Tensor, shard: torch.Tensor, async_op: bool):
+        self.sent_bytes["ag"] += shard.numel() * shard.element_size() * (self.world - 1)
         if self.real:
             return self.ag.all_gather(full, shard, async_op=async_op)
         return self._emu("ag", lambda: full.view(self.world, -1).copy_(shard.unsqueeze(0).expand(self.world, -1)),
                          (full, shard), async_op)
 
     def reduce_scatter(self, out: torch.Tensor, full: torch.Tensor, async_op: bool):
+        wire = self.rs_wire == "bf16" and full.dtype == torch.float32
+        self.sent_bytes["rs"] += self.rs_wire_bytes(full.numel(), full.dtype)
         if self.real:
+            if wire:
+                return self.rs.reduce_scatter(out, full, async_op=async_op, wire=torch.bfloat16)
             return self.rs.reduce_scatter(out, full, async_op=async_op)
         if self.world == 1:
             out.copy_(full)
             return None
+        if wire:  # the owner's fp32 sum of bf16-rounded contributions
+            return self._emu("rs", lambda: torch.sum(full.view(self.world, -1).to(torch.bfloat16).float(), dim=0,
+                                                     out=out), (out, full), async_op)
         return self._emu("rs", lambda: torch.sum(full.view(self.world, -1), dim=0, out=out), (out, full), async_op)
+
+    def rs_wire_bytes(self, numel: int, dtype: torch.dtype) -> int:
+        """Bytes one reduce-scatter of ``numel`` elements puts on this rank's links: (W-1)/W of the
+        tensor, at the wire's element size."""
+        es = 2 if (self.rs_wire == "bf16" and dtype == torch.float32) else torch.empty(0, dtype=dtype).element_size()
+        return numel * es * (self.world - 1) // max(1, self.world)
 
     def all_reduce(self, t: torch.Tensor, async_op: bool = False):
         if self.real:

@@ -82,8 +82,10 @@ def _launch(target, world, *args, timeout=300):
 # ---------------------------------------------------------------------------- kernel level
 
 
-def _coll_worker(rank, world, port, q):
+def _coll_worker(rank, world, port, q, algo="light"):
     _peer_env(port)
+    os.environ["MXLLM_PEER_ALGO"] = algo
+    os.environ["MXLLM_PEER_LIGHT_MB"] = "1"  # small slots: the larger sizes run as several segments
     out = {"rank": rank}
     try:
         from mxllm.parallel import runtime
@@ -96,6 +98,7 @@ def _coll_worker(rank, world, port, q):
         a = create(None, dev)
         b = create(dist.new_group(), dev)  # a second communicator: its own stream and staging
         out["kinds"] = (a.kind, b.kind)
+        out["algo"] = (a.algo, b.algo)
         assert isinstance(a, PeerCollectives) and isinstance(b, PeerCollectives)
 
         def vals(n, seed, dt):
@@ -131,6 +134,12 @@ def _coll_worker(rank, world, port, q):
                 ar = vs[rank].to(dev)
                 a.all_reduce(ar)  # sync form: stream-ordered, no host wait
                 ok &= bool(torch.equal(ar.cpu().view(world, m)[rank], want_rs))
+                if algo == "light" and dt == torch.float32:
+                    # bf16 on the wire: the fp32 rank-ordered sum of the bf16-rounded inputs, bit for bit
+                    rw = torch.empty(m, dtype=dt, device=dev)
+                    b.reduce_scatter(rw, vs[rank].to(dev), wire=torch.bfloat16)
+                    ok_w = bool(torch.equal(rw.cpu(), rsum([v.bfloat16().float() for v in vs]).view(world, m)[rank]))
+                    out["wire_ok"] = out.get("wire_ok", True) and ok_w
                 del junk
         out["ok"] = ok
         # every rank gets identical all-reduce bits
@@ -169,12 +178,16 @@ def _coll_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(400)
+@pytest.mark.parametrize("algo", ["light", "resident"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_peer_collectives_exact_on_shared_gpu(gpu, world):
-    res = _launch(_coll_worker, world)
+def test_peer_collectives_exact_on_shared_gpu(gpu, world, algo):
+    res = _launch(_coll_worker, world, algo)
     for r in range(world):
         assert "exc" not in res[r], res[r]["exc"]
         assert res[r]["kinds"] == ("peer", "peer") and res[r]["ok"] and res[r]["identical"], res[r]
+        assert res[r]["algo"] == (algo, algo)
+        if algo == "light":
+            assert res[r]["wire_ok"], res[r]
     assert res[0]["timeout_raised"] and res[0]["poisoned"] and res[0]["refused"], res[0]
 
 
