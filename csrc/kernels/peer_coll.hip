@@ -272,14 +272,18 @@ __device__ __forceinline__ uint32_t* lword(char* lbase, int idx) {
   return reinterpret_cast<uint32_t*>(lbase) + (size_t)idx * kFlagStride;
 }
 
-// 8 elements <-> 8 floats (exact for bf16 <-> fp32 widening, round-to-nearest-even narrowing)
+// 8 elements <-> 8 floats (exact for bf16 <-> fp32 widening, round-to-nearest-even narrowing).  Default
+// cache policy: non-temporal loads / stores (and 8 items in flight) measured slower here, with no
+// smaller GEMM slowdown beside them (profiles/r6b/README.md).
+__device__ __forceinline__ u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ void st16(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
 __device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
-  const u32x4 a = *reinterpret_cast<const u32x4*>(p), b = *reinterpret_cast<const u32x4*>(p + 4);
+  const u32x4 a = ld16(p), b = ld16(p + 4);
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = __uint_as_float(a[j]), v[4 + j] = __uint_as_float(b[j]);
 }
 __device__ __forceinline__ void ld8(const uint16_t* p, float (&v)[8]) {
-  const u32x4 a = *reinterpret_cast<const u32x4*>(p);
+  const u32x4 a = ld16(p);
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[2 * j] = __uint_as_float(a[j] << 16), v[2 * j + 1] = __uint_as_float(a[j] & 0xFFFF0000u);
 }
@@ -287,14 +291,14 @@ __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
   u32x4 a, b;
 #pragma unroll
   for (int j = 0; j < 4; ++j) a[j] = __float_as_uint(v[j]), b[j] = __float_as_uint(v[4 + j]);
-  *reinterpret_cast<u32x4*>(p) = a;
-  *reinterpret_cast<u32x4*>(p + 4) = b;
+  st16(p, a);
+  st16(p + 4, b);
 }
 __device__ __forceinline__ void st8(uint16_t* p, const float (&v)[8]) {
   u32x4 a;
 #pragma unroll
   for (int j = 0; j < 4; ++j) a[j] = mx::pack_bf16x2(v[2 * j], v[2 * j + 1]);
-  *reinterpret_cast<u32x4*>(p) = a;
+  st16(p, a);
 }
 template <typename W>
 __device__ __forceinline__ void round_to(float (&v)[8]) {
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(64) void pc_wait_kernel(Bases P, int base_idx, uint
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
-// Both streaming kernels keep kLU 8-element items per thread in flight (all loads of a group issued
+// Both streaming kernels keep kLU (4) 8-element items per thread in flight (all loads of a group issued
 // before its stores): one 8-element item per thread is only ~8 KB per workgroup in flight, a few GB/s
 // per CU at HBM latency, so a given rate would need many more workgroups -- CUs taken from the
 // compute stream.  Items are numbered q = item * 8 elements; thread t of workgroup b takes
