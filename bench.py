@@ -103,6 +103,10 @@ def parse(argv=None):
                     help="with config 3: ALSO measure it with the optimizer sharded (ZeRO-1: reduce-scatter, "
                          "AdamW on 1/N of the state, all-gather), after config 4 and only if the time budget "
                          "is left; auto = on GPUs")
+    ap.add_argument("--config3-peer", choices=["auto", "on", "off"], default="auto",
+                    help="with config 3: ALSO measure it with the gradient buckets all-reduced by mxllm's own peer-memory "
+                         "collectives (MXLLM_COMM=peer, light schedule) instead of RCCL -- last, only if the time "
+                         "budget is left; auto = on GPUs")
     ap.add_argument("--config3-timeout", type=float, default=300.0,
                     help="hard limit for the config-3 child job; the headline line is printed either way")
     ap.add_argument("--config2-mb4", choices=["auto", "on", "off"], default="auto",
@@ -260,8 +264,11 @@ def main(argv=None):
     if c4:
         children.append(("config4", "config4_full_zero3"))
     if c3 and env.world_size > 1 and (a.config3_zero1 == "on" or (a.config3_zero1 == "auto" and cuda)):
-        # the same DDP fine-tune with the optimizer sharded: last, so it never costs config 4 its budget
+        # the same DDP fine-tune with the optimizer sharded: after config 4, so it never costs it its budget
         children.append(("config3z", f"config3_8b_full_dp{env.world_size}_zero1"))
+    if c3 and env.world_size > 1 and (a.config3_peer == "on" or (a.config3_peer == "auto" and cuda)):
+        # the same DDP fine-tune over mxllm's own peer-memory collectives: last of all
+        children.append(("config3p", f"config3_8b_full_dp{env.world_size}_peer"))
     try:
         if cuda and a.calibrate:
             # box speed next to the number: fixed GEMM + copy after the timed steps
@@ -308,7 +315,8 @@ def main(argv=None):
                 if kind == "config4":
                     out[key] = run_config4_planned(a, env.world_size, free_gb)
                 else:
-                    out[key] = run_config3(a, env.world_size, "zero1" if kind == "config3z" else "ddp")
+                    out[key] = run_config3(a, env.world_size, "zero1" if kind == "config3z" else "ddp",
+                                           comm="peer" if kind == "config3p" else None)
             except Exception as e:  # noqa: BLE001  the headline (and later phases) survive any phase error
                 out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
         out["child_phases"]["elapsed_s"] = round(time.time() - _T0, 1)
@@ -441,7 +449,7 @@ def _budget_skip(a) -> dict:
                        f"left (a phase needs --child-min-s {a.child_min_s:.0f} + {EMIT_MARGIN_S:.0f})"}
 
 
-def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "") -> dict:
+def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "", extra_env: dict | None = None) -> dict:
     """Run bench.py ``argv`` as a fresh ``world``-rank torchrun child job (rendezvous on
     127.0.0.1) and return its parsed JSON line (or the error).  ``timeout_s`` is capped by
     the remaining ``--time-budget-s``; below ``--child-min-s`` the job is not started.
@@ -472,6 +480,7 @@ def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "") 
     if fault and tag and fault.split(":")[0] == tag:
         keep.update(MXLLM_FAULT_KIND=fault.split(":", 1)[1], MXLLM_FAULT_RANK="0", MXLLM_FAULT_STEP="0")
     keep.pop("MXLLM_BENCH_CHILD_FAULT", None)
+    keep.update(extra_env or {})
     t0 = time.time()
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):  # the child's own JSON line must not become a second output line
@@ -493,7 +502,7 @@ def _run_child(a, world: int, argv: list[str], timeout_s: float, tag: str = "") 
     return res
 
 
-def run_config3(a, world: int, parallel: str = "ddp") -> dict:
+def run_config3(a, world: int, parallel: str = "ddp", comm: str | None = None) -> dict:
     """BASELINE config 3: Llama-3.1-8B FULL fine-tune, DDP over ``world`` GPUs, as a fresh child
     job after the headline.  ``parallel`` = "zero1": the same data-parallel step with the
     optimizer sharded (mxllm/parallel/zero1.py: the buckets are reduce-scattered, each rank runs
@@ -502,9 +511,13 @@ def run_config3(a, world: int, parallel: str = "ddp") -> dict:
     argv = ["--model", a.full_model, "--finetune", "full", "--parallel", parallel, "--micro-batch",
             str(a.micro_batch), "--seq-len", str(a.seq_len), "--steps", str(a.full_steps), "--warmup",
             str(a.full_warmup)]
-    res = _run_child(a, world, argv, a.config3_timeout, tag="config3" if parallel == "ddp" else "config3z")
+    tag = "config3p" if comm == "peer" else ("config3" if parallel == "ddp" else "config3z")
+    res = _run_child(a, world, argv, a.config3_timeout, tag=tag,
+                     extra_env={"MXLLM_COMM": "peer"} if comm == "peer" else None)
     name = PRETTY.get(a.full_model, a.full_model)
     how = "DDP" if parallel == "ddp" else "DDP with a ZeRO-1 sharded optimizer"
+    if comm == "peer":
+        how += " over mxllm's peer-memory collectives (MXLLM_COMM=peer)"
     res["metric"] = f"fine-tune tokens/sec (whole node) {name} FULL-parameter {how}"
     res["label"] = (f"BASELINE config 3: {name} full-parameter fine-tune, {how} over {world} GPUs, "
                     f"measured after the headline in a separate job")

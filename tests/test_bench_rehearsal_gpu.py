@@ -5,8 +5,8 @@ The 8-GPU driver run goes through steps no 1-GPU bench ever reaches: the self-la
 of N torchrun ranks (``launch_ranks``), DDP of the headline's LoRA adapters across
 ranks, the HBM release + PID wait before the child phases, and the config-3 (8B full
 DDP), config-3 ZeRO-1 and config-4 (ZeRO-3) child jobs, all folded into ONE JSON line.
-Here the same command runs with ``--gpus 2`` and both ranks of every job on the box's
-GPU: ``MXLLM_BACKEND=gloo`` carries the bootstrap, ``MXLLM_COMM=peer`` gives the
+Here the same command runs with ``--gpus 2`` and ``--gpus 8`` (the driver's own N) and every
+rank of every job on the box's GPU: ``MXLLM_BACKEND=gloo`` carries the bootstrap, ``MXLLM_COMM=peer`` gives the
 bulk collectives RCCL's stream-ordered semantics over peer memory
 (mxllm/parallel/comm.py), and ``MXLLM_BENCH_SHARED_GPU=1`` lets ``_run_child`` start
 2-rank children on 1 GPU.  Small models stand in for the real ones (the headline
@@ -27,34 +27,38 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.timeout(420)
-def test_bench_two_rank_flow_on_shared_gpu(gpu):
+@pytest.mark.timeout(560)
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_multi_rank_flow_on_shared_gpu(gpu, world):
+    """``world`` = 8 is the driver's own N: every rank count, bucket split, child-job size and
+    communicator of the 8-GPU run, with the ranks sharing the one GPU."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     env.update(MXLLM_BACKEND="gloo", MXLLM_COMM="peer", MXLLM_COMM_STRICT="1", MXLLM_BENCH_SHARED_GPU="1",
                MXLLM_PEER_WGS="8", MXLLM_PEER_TIMEOUT_S="60", MXLLM_BENCH_SMI="0", PYTHONUNBUFFERED="1")
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    log = os.path.join(ROOT, "gpurun_out", "bench_rehearsal.log")  # progress a long run keeps writing
-    cmd = [sys.executable, "bench.py", "--gpus", "2", "--layers", "2", "--steps", "2", "--warmup", "1",
+    log = os.path.join(ROOT, "gpurun_out", f"bench_rehearsal_w{world}.log")  # progress a long run keeps writing
+    cmd = [sys.executable, "bench.py", "--gpus", str(world), "--layers", "2", "--steps", "2", "--warmup", "1",
            "--seq-len", "1024", "--config3", "on", "--config4", "on", "--config4-model", "tiny-d128",
            "--config4-steps", "2", "--config4-warmup", "1", "--full-model", "tiny-d128", "--full-steps", "2",
-           "--full-warmup", "1", "--no-calibrate", "--time-budget-s", "400", "--child-min-s", "40"]
+           "--full-warmup", "1", "--no-calibrate", "--time-budget-s", "500", "--child-min-s", "40"]
     with open(log, "w") as f:
-        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=f, text=True, timeout=400)
+        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=f, text=True, timeout=540)
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    with open(os.path.join(ROOT, "gpurun_out", "bench_rehearsal.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"bench_rehearsal_w{world}.json"), "w") as f:
         f.write(r.stdout)  # the one line, kept as evidence (profiles/r6_rehearsal/)
     tail = open(log).read()[-4000:]
     assert r.returncode == 0, tail
     assert len(lines) == 1, r.stdout[-3000:]
     j = lines[0]
     # the headline: LoRA DDP over 2 ranks, adapter buckets all-reduced through the peer communicator
-    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["value"] > 0, j
+    assert j["n_gpus"] == world and j["config"]["parallelism"] == f"dp{world}" and j["value"] > 0, j
     assert j["grad_comm"] == "peer" and j["allreduce_mb_per_step"] > 0, j
     assert j["child_phases"]["headline_ranks_exited_s"] is not None, j["child_phases"]
-    for key, par in (("config3_8b_full_dp2", "dp2"), ("config3_8b_full_dp2_zero1", "dp2-zero1"),
-                     ("config4_full_zero3", "zero3-dp2")):
+    for key, par in ((f"config3_8b_full_dp{world}", f"dp{world}"), (f"config3_8b_full_dp{world}_zero1", f"dp{world}-zero1"),
+                     ("config4_full_zero3", f"zero3-dp{world}"), (f"config3_8b_full_dp{world}_peer", f"dp{world}")):
         c = j[key]
         assert "error" not in c and "skipped" not in c, (key, c)
-        assert c["n_gpus"] == 2 and c["value"] > 0 and c["config"]["parallelism"] == par, (key, c)
+        assert c["n_gpus"] == world and c["value"] > 0 and c["config"]["parallelism"] == par, (key, c)
     assert j["config4_full_zero3"]["zero3"]["comm_backend"] == "peer", j["config4_full_zero3"]["zero3"]
+    assert j[f"config3_8b_full_dp{world}_peer"]["grad_comm"] == "peer"
