@@ -169,6 +169,9 @@ RECOMPUTE_SWIGLU = os.environ.get("MXLLM_RECOMPUTE_SWIGLU", "auto")
 # same layers: the normed inputs of the qkv and gate-up projections are recomputed from the
 # residual stream in their backward instead of saved (ops.normed_linear); 0 = save them
 RECOMPUTE_NORM = os.environ.get("MXLLM_RECOMPUTE_NORM", "auto")
+# those layers' MLP through the fused gate-up + SwiGLU epilogue (m rebuilt by the dm GEMM's epilogue
+# in the backward) instead of GEMM + a standalone SwiGLU pass; 0 = the unfused recompute (A/B)
+REC_FUSED = os.environ.get("MXLLM_REC_FUSED", "1") != "0"
 
 
 class LlamaLayer(nn.Module):
@@ -277,7 +280,12 @@ class Llama(nn.Module):
         a = layer.wo(o)
         x, h = ops.add_rms_norm(a, h, layer.mlp_norm, cfg.norm_eps, out_pad=self._pad(layer.wgu),
                                 grad_pad=self._pad(layer.wo))
-        if rec:  # m = swiglu(gu) (and the gate-up input x) recomputed in the backward
+        if rec and REC_FUSED and fused.gate_up_swiglu_down_ok(x, layer.wgu.weight, layer.wd.weight):
+            # the same recompute (only gu, and h for x, kept) with the SwiGLU in the gate-up GEMM's
+            # epilogue and m rebuilt by the backward's dm GEMM epilogue: no standalone SwiGLU pass
+            d = fused.gate_up_swiglu_down(x, layer.wgu.weight, layer.wd.weight,
+                                          norm=(h, layer.mlp_norm, cfg.norm_eps) if rec_x else None, recompute_m=True)
+        elif rec:  # m = swiglu(gu) (and the gate-up input x) recomputed in the backward
             gu = ops.normed_linear(x, h, layer.mlp_norm, cfg.norm_eps, layer.wgu.weight) if rec_x else layer.wgu(x)
             d = ops.swiglu_linear(gu, layer.wd.weight)
         elif (not layer.wgu.lora_r and not layer.wd.lora_r

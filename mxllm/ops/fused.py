@@ -187,10 +187,16 @@ def gate_up_swiglu_down_ok(x: torch.Tensor, wgu: torch.Tensor, wd: torch.Tensor)
 class _GateUpSwiGLUDownFn(torch.autograd.Function):
     """y = swiglu(x Wgu^T) Wd^T: the gate-up GEMM with the SwiGLU epilogue, then the down GEMM;
     backward: dgu from the down projection's dX GEMM epilogue, dWd from the saved m, then the
-    gate-up dX / dW GEMMs.  Weight gradients go the ``_LinearFn`` way."""
+    gate-up dX / dW GEMMs.  Weight gradients go the ``_LinearFn`` way.
+
+    ``recompute_m``: m is NOT saved (the activation-memory budget of the un-checkpointed layers of
+    a selectively checkpointed run, models/llama.py ``_recompute_m``): the down projection's dX
+    GEMM epilogue writes the recomputed m next to dgu (``G8_EPI_SWIGLU_BWD`` with ``ep.m``) for
+    dWd -- the same saved tensors as the unfused recompute path (gu, and h when x is rebuilt), but
+    no standalone SwiGLU pass in the forward."""
 
     @staticmethod
-    def forward(ctx, x, wgu, wd, h, nw, eps):
+    def forward(ctx, x, wgu, wd, h, nw, eps, recompute_m=False):
         x2 = _x2(x)
         T, F2 = x2.shape[0], wgu.shape[0]
         gu = torch.empty(T, F2, dtype=x.dtype, device=x.device)
@@ -199,18 +205,23 @@ class _GateUpSwiGLUDownFn(torch.autograd.Function):
             raise RuntimeError("gemm8_swiglu declined a shape gate_up_swiglu_down_ok accepted")
         y = gemm.mm("tn", m, wd)
         keep_x = h is None
+        if recompute_m:
+            del m
+            m = None
         ctx.save_for_backward(x2 if keep_x else h, wgu, wd, gu, m, nw)
         ctx.wgp = wgu if wgu.is_leaf else None
         ctx.wdp = wd if wd.is_leaf else None
-        ctx.dims = (x.shape, keep_x, eps)
+        ctx.dims = (x.shape, keep_x, eps, bool(recompute_m))
         return y.view(*x.shape[:-1], wd.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         xs, wgu, wd, gu, m, nw = ctx.saved_tensors
-        xshape, keep_x, eps = ctx.dims
+        xshape, keep_x, eps, rec = ctx.dims
         dy2 = dy.reshape(-1, wd.shape[0])
-        dgu, _ = swiglu_bwd_gemm(dy2, wd, gu)
+        dgu, m_re = swiglu_bwd_gemm(dy2, wd, gu, want_m=rec and ctx.needs_input_grad[2])
+        if rec:
+            m = m_re
         del gu
         dwd = param_weight_grad(ctx.wdp, dy2, m) if ctx.needs_input_grad[2] else None
         del m
@@ -219,12 +230,12 @@ class _GateUpSwiGLUDownFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             x2 = xs if keep_x else _norm_input(xs, nw, eps)
             dwgu = param_weight_grad(ctx.wgp, dgu, x2)
-        return dx, dwgu, dwd, None, None, None
+        return dx, dwgu, dwd, None, None, None, None
 
 
 def gate_up_swiglu_down(x: torch.Tensor, wgu: torch.Tensor, wd: torch.Tensor,
-                        norm: tuple | None = None) -> torch.Tensor:
+                        norm: tuple | None = None, recompute_m: bool = False) -> torch.Tensor:
     """The MLP body swiglu(x Wgu^T) Wd^T (callers check ``gate_up_swiglu_down_ok``); ``norm`` as in
-    ``gate_up_swiglu``."""
+    ``gate_up_swiglu``; ``recompute_m``: keep only gu, rebuild m in the backward's dm GEMM."""
     h, nw, eps = norm if norm is not None else (None, None, 0.0)
-    return _GateUpSwiGLUDownFn.apply(x, wgu, wd, h, nw, eps)
+    return _GateUpSwiGLUDownFn.apply(x, wgu, wd, h, nw, eps, bool(recompute_m))

@@ -166,3 +166,33 @@ def test_fused_mlp_backward_matches_two_step(gpu, monkeypatch):
     assert l1 == l0
     for n in g0:
         assert torch.equal(g1[n], g0[n]), n
+
+
+def test_fused_mlp_recompute_m_bitwise(gpu, monkeypatch):
+    """the recompute path (un-checkpointed layers of a selectively checkpointed
+    run keep only gu and rebuild m) through the fused gate-up + SwiGLU epilogue, with m rebuilt by the
+    dm GEMM's epilogue, gives bitwise the loss and gradients of the fused path that SAVES m -- and
+    no standalone SwiGLU pass runs (``swiglu_linear`` is not called)."""
+    from mxllm.models import Llama, get_config, llama
+    from mxllm.ops import linear as lin_mod
+
+    monkeypatch.setenv("MXLLM_GEMM8", "all")
+    cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=torch.Generator(device=gpu).manual_seed(4))
+    res = {}
+    for rec in ("1", "0"):
+        monkeypatch.setattr(llama, "RECOMPUTE_SWIGLU", rec)
+        monkeypatch.setattr(llama, "RECOMPUTE_NORM", "0")
+        calls = []
+        real = lin_mod.swiglu_linear
+        monkeypatch.setattr(llama.ops, "swiglu_linear", lambda *a, **k: (calls.append(1), real(*a, **k))[1],
+                            raising=False)
+        model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3)
+        loss = model(ids, ids)
+        loss.backward()
+        res[rec] = (float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+        assert not calls, "the recompute path must not run the standalone SwiGLU"
+    (l1, g1), (l0, g0) = res["1"], res["0"]
+    assert l1 == l0
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
