@@ -174,7 +174,6 @@ def test_fused_mlp_recompute_m_bitwise(gpu, monkeypatch):
     dm GEMM's epilogue, gives bitwise the loss and gradients of the fused path that SAVES m -- and
     no standalone SwiGLU pass runs (``swiglu_linear`` is not called)."""
     from mxllm.models import Llama, get_config, llama
-    from mxllm.ops import linear as lin_mod
 
     monkeypatch.setenv("MXLLM_GEMM8", "all")
     cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
@@ -184,9 +183,8 @@ def test_fused_mlp_recompute_m_bitwise(gpu, monkeypatch):
         monkeypatch.setattr(llama, "RECOMPUTE_SWIGLU", rec)
         monkeypatch.setattr(llama, "RECOMPUTE_NORM", "0")
         calls = []
-        real = lin_mod.swiglu_linear
-        monkeypatch.setattr(llama.ops, "swiglu_linear", lambda *a, **k: (calls.append(1), real(*a, **k))[1],
-                            raising=False)
+        real = llama.ops.swiglu_linear
+        monkeypatch.setattr(llama.ops, "swiglu_linear", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
         model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3)
         loss = model(ids, ids)
         loss.backward()
