@@ -142,3 +142,33 @@ def test_grad_norm_under_accumulation_matches_one_batch(monkeypatch):
         tr.train_step(mbs)
         norms.append(float(tr.last_grad_norm))
     assert abs(norms[0] - norms[1]) < 1e-4 * norms[0], norms
+
+
+def test_finish_runs_the_peer_sync_check(monkeypatch):
+    """DDP.finish waits for a peer communicator's last collective and raises on a
+    timeout BEFORE the optimizer consumes the reduced gradient (comm.verify); RCCL / gloo
+    communicators have no such hook and pass through; MXLLM_PEER_SYNC_CHECK=0 skips it."""
+    monkeypatch.setenv("MXLLM_FORCE_CPU", "1")
+    from mxllm.models import Llama, get_config
+    from mxllm.parallel.ddp import DDP
+    from mxllm.parallel.flat import FlatParams, production_order
+
+    class BrokenPeer:
+        kind = "peer"
+        checked = 0
+
+        def all_reduce(self, t, async_op=False):
+            return None
+
+        def sync_check(self):
+            BrokenPeer.checked += 1
+            raise RuntimeError("peer-memory collective timed out")
+
+    model = Llama(get_config("tiny").replace(n_layers=1, vocab_size=64), dtype=torch.float32, seed=1)
+    flat = FlatParams(production_order(model, [(n, p) for n, p in model.named_parameters()]), reverse=False)
+    ddp = DDP(flat, enabled=True, comm=BrokenPeer())
+    with pytest.raises(RuntimeError, match="timed out"):
+        ddp.finish()
+    assert BrokenPeer.checked == 1
+    monkeypatch.setenv("MXLLM_PEER_SYNC_CHECK", "0")
+    assert ddp.finish() == 1.0  # world 1 scale; the check skipped
