@@ -35,7 +35,12 @@ def test_bench_multi_rank_flow_on_shared_gpu(gpu, world):
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     env.update(MXLLM_BACKEND="gloo", MXLLM_COMM="peer", MXLLM_COMM_STRICT="1", MXLLM_BENCH_SHARED_GPU="1",
-               MXLLM_PEER_WGS="8", MXLLM_PEER_TIMEOUT_S="60", MXLLM_BENCH_SMI="0", PYTHONUNBUFFERED="1")
+               MXLLM_PEER_WGS="8", MXLLM_PEER_TIMEOUT_S="120", MXLLM_BENCH_SMI="0", PYTHONUNBUFFERED="1")
+    if world > 4:
+        # 8 processes x HIP's default 4 hardware queues oversubscribe the one GPU's queue slots: an
+        # unmapped queue holding a peer's push never runs while a mapped one spins in its flag wait
+        # (on the 8-GPU node every rank has a GPU of its own); 2 queues per process fit
+        env["GPU_MAX_HW_QUEUES"] = "2"
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     log = os.path.join(ROOT, "gpurun_out", f"bench_rehearsal_w{world}.log")  # progress a long run keeps writing
     cmd = [sys.executable, "bench.py", "--gpus", str(world), "--layers", "2", "--steps", "2", "--warmup", "1",
