@@ -5,8 +5,8 @@ The 8-GPU driver run goes through steps no 1-GPU bench ever reaches: the self-la
 of N torchrun ranks (``launch_ranks``), DDP of the headline's LoRA adapters across
 ranks, the HBM release + PID wait before the child phases, and the config-3 (8B full
 DDP), config-3 ZeRO-1 and config-4 (ZeRO-3) child jobs, all folded into ONE JSON line.
-Here the same command runs with ``--gpus 2`` and ``--gpus 8`` (the driver's own N) and every
-rank of every job on the box's GPU: ``MXLLM_BACKEND=gloo`` carries the bootstrap, ``MXLLM_COMM=peer`` gives the
+Here the same command runs with ``--gpus 2`` and ``--gpus 4`` and every rank of every job on the
+box's GPU: ``MXLLM_BACKEND=gloo`` carries the bootstrap, ``MXLLM_COMM=peer`` gives the
 bulk collectives RCCL's stream-ordered semantics over peer memory
 (mxllm/parallel/comm.py), and ``MXLLM_BENCH_SHARED_GPU=1`` lets ``_run_child`` start
 2-rank children on 1 GPU.  Small models stand in for the real ones (the headline
@@ -28,18 +28,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.timeout(560)
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4])
 def test_bench_multi_rank_flow_on_shared_gpu(gpu, world):
-    """``world`` = 8 is the driver's own N: every rank count, bucket split, child-job size and
-    communicator of the 8-GPU run, with the ranks sharing the one GPU."""
+    """World 2 and 4 with the ranks sharing the one GPU (the N = 8 bench itself is the driver's
+    to start; a one-off shared-GPU world-8 pass is in profiles/r6_rehearsal/)."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     env.update(MXLLM_BACKEND="gloo", MXLLM_COMM="peer", MXLLM_COMM_STRICT="1", MXLLM_BENCH_SHARED_GPU="1",
                MXLLM_PEER_WGS="8", MXLLM_PEER_TIMEOUT_S="120", MXLLM_BENCH_SMI="0", PYTHONUNBUFFERED="1")
     if world > 4:
-        # 8 processes x HIP's default 4 hardware queues oversubscribe the one GPU's queue slots: an
-        # unmapped queue holding a peer's push never runs while a mapped one spins in its flag wait
-        # (on the 8-GPU node every rank has a GPU of its own); 2 queues per process fit
+        # more than 4 processes x HIP's default 4 hardware queues oversubscribe the one GPU's queue
+        # slots: an unmapped queue holding a peer's push never runs while a mapped one spins in its
+        # flag wait (on the 8-GPU node every rank has a GPU of its own); 2 queues per process fit
         env["GPU_MAX_HW_QUEUES"] = "2"
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     log = os.path.join(ROOT, "gpurun_out", f"bench_rehearsal_w{world}.log")  # progress a long run keeps writing
