@@ -384,6 +384,9 @@ struct XtgArgs {
   int accumulate;
   int fused_red;  // 1: last-arriving workgroup reduces; 0: lora_xtg_reduce_kernel does
   int narrow3;    // 1: narrow-G problems stream through three stages per wave (0: two, A/B)
+  int wt;         // 1: each WAVE owns a 64-col tile over all T rows (4 adjacent tiles per workgroup,
+                  // S == 1, no cross-wave reduction); 0: the 4 waves split one tile's rows
+                  // (xtg_wave_tiles: the large launches only)
 };
 
 // 16-B chunk swizzle of a 128-B LDS row: conflict-free ds_read_b64_tr_b16 of
@@ -395,7 +398,10 @@ __global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float
   constexpr int XB = 8192, STG = 16384, WREG = 2 * STG;  // per wave: 2 stages x (X 8 KiB + G <= 8 KiB)
   __shared__ __attribute__((aligned(16))) char smem[4 * WREG];
   __shared__ int s_last;
-  const int tile = blockIdx.x, split = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps the block loop scalar
+  const int tile = a.wt ? blockIdx.x * 4 + w : blockIdx.x, split = blockIdx.y;
+  if (a.wt && tile >= a.ntiles) return;  // wave-uniform; the wt path has no workgroup barrier
   // this tile's problem, selected with uniform conditional copies (a dynamic index
   // into the kernel-argument array would be lowered through scratch)
   XtgProb P = a.p[0];
@@ -405,10 +411,8 @@ __global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float
   const int n0 = (tile - P.tile0) * 64;
   const bool wide = P.JB > 1;
   const int JB = P.JB;
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps the block loop scalar
   const int qq = c >> 2, pp = c & 3;
-  const int nblk = a.T >> 6, nw = a.S * 4, gw = split * 4 + w;
+  const int nblk = a.T >> 6, nw = a.wt ? a.S : a.S * 4, gw = a.wt ? split : split * 4 + w;
   const int b0 = (int)((int64_t)gw * nblk / nw), b1 = (int)((int64_t)(gw + 1) * nblk / nw);
   char* wreg = smem + w * WREG;
   const uint32_t wbase = lds_addr(wreg);
@@ -581,6 +585,19 @@ __global__ void __launch_bounds__(256, 1) lora_xtg_kernel(const XtgArgs a, float
 #pragma unroll
       for (int e = 0; e < 4; ++e) rw[(16 * i + 4 * g + e) * kRS + 16 * j + c] = acc[i][j][e];
     }
+  if (a.wt) {  // this wave's whole tile (S == 1): read its own image back, write the outputs
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int J = 16 * JB, nel = 64 * J;
+    const bool jfast = P.os_j == 1;
+    for (int e = lane; e < nel; e += 64) {
+      const int n = jfast ? e / J : (e & 63), j = jfast ? e % J : (e >> 6);
+      uint16_t* o = P.out + (int64_t)(n0 + n) * P.os_n + (int64_t)j * P.os_j;
+      const float r = a.alpha * rw[n * kRS + j] + (a.accumulate ? bf2f(*o) : 0.f);
+      *o = f2bf(r);
+    }
+    return;
+  }
   __syncthreads();
   const int J = 16 * JB, nel = 64 * J;
   const bool jfast = P.os_j == 1;
@@ -955,6 +972,15 @@ static int lora_splits(int tiles, int blocks, int smax) {
   return S;
 }
 
+// lora_xtg with one 64-col tile per WAVE (XtgArgs::wt) where that still fills the chip with one
+// workgroup per CU and no row split (>= 4 x MXLLM_LORA_WGS tiles: the 70B gate-up gradients, 1,024
+// tiles): 119.1 -> 100.1 us per launch at T 4096 (profiles/r6g/: one round of 256 workgroups instead
+// of four of 1,024, and no cross-wave reduction); the smaller launches do not qualify and measured
+// the same when forced.  MXLLM_LORA_XTG_WT=0 restores the row-split form (read per call: A/B)
+static bool xtg_wave_tiles(int ntiles) {
+  return lora_env("MXLLM_LORA_XTG_WT", 1) == 1 && ntiles >= 4 * lora_env("MXLLM_LORA_WGS", 256);
+}
+
 // lora_xwt kernel choice (MXLLM_LORA_XWT, read per call: an in-process A/B can flip it):
 // "lds" (default) = the 64-row LDS-DMA kernel, "reg" = the register-fragment kernel (both on all
 // 64 padded rows of V), "tile" = lora_xwt_tile_kernel (adapter rows only; needs M % 16, K % 128,
@@ -990,6 +1016,7 @@ extern "C" int64_t mx_lora_xwt_ws(int M, int K, int rows) {
   return dma;
 }
 extern "C" int64_t mx_lora_xtg_ws(int ntiles, int T) {
+  if (xtg_wave_tiles(ntiles)) return 0;
   const int S = lora_splits(ntiles, T / 64, 8);
   return S > 1 ? (int64_t)S * ntiles * 4096 : 0;
 }
@@ -1059,11 +1086,13 @@ extern "C" int mx_lora_xtg(const int64_t* desc, int np, int T, float alpha, int 
     ntiles += p.Nx / 64;
   }
   if (ntiles > kMaxTiles) return (int)hipErrorInvalidValue;
-  a.np = np, a.T = T, a.S = lora_splits(ntiles, T / 64, 8), a.ntiles = ntiles, a.alpha = alpha;
+  a.np = np, a.T = T, a.ntiles = ntiles, a.alpha = alpha;
+  a.wt = xtg_wave_tiles(ntiles);
+  a.S = a.wt ? 1 : lora_splits(ntiles, T / 64, 8);
   a.accumulate = accumulate;
-  a.fused_red = lora_env("MXLLM_LORA_FUSED_RED", 0);
+  a.fused_red = a.wt ? 0 : lora_env("MXLLM_LORA_FUSED_RED", 0);
   a.narrow3 = lora_env("MXLLM_LORA_XTG_STAGES", 3) == 3;
-  lora_xtg_kernel<<<dim3(ntiles, a.S), 256, 0, stream>>>(a, ws);
+  lora_xtg_kernel<<<dim3(a.wt ? (ntiles + 3) / 4 : ntiles, a.S), 256, 0, stream>>>(a, ws);
   if (a.S > 1 && !a.fused_red) lora_xtg_reduce_kernel<<<ntiles, 256, 0, stream>>>(a, ws);
   return (int)hipGetLastError();
 }

@@ -558,10 +558,23 @@ def test_lora_grads(gpu, T, K, splits, r, acc, monkeypatch):
     _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
     assert torch.equal(ga1, ga) and torch.equal(gb1, gb)  # bit-reproducible
     monkeypatch.setenv("MXLLM_LORA_FUSED_RED", "1")
+    monkeypatch.setenv("MXLLM_LORA_XTG_WT", "0")
     for _ in range(2):
         ga1, gb1 = ga0.clone(), gb0.clone()
         _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
         assert torch.equal(ga1, ga) and torch.equal(gb1, gb)
+    # one 64-col tile per wave over all rows (MXLLM_LORA_XTG_WT=1; the WGS target lowered so these
+    # shapes qualify): same products to fp32 rounding, off-diagonal blocks untouched, reproducible
+    monkeypatch.setenv("MXLLM_LORA_XTG_WT", "1")
+    monkeypatch.setenv("MXLLM_LORA_WGS", "4")
+    outs = []
+    for _ in range(2):
+        ga1, gb1 = ga0.clone(), gb0.clone()
+        _ops().lora_grads(x2, dy2, g, st, ga1, gb1, splits, r, acc)
+        assert rel_err(ga1, want_a) < 1e-2 and rel_err(gb1, want_b) < 1e-2
+        assert torch.equal(gb1[mask], gb0[mask])
+        outs.append((ga1, gb1))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("R,C,ld", [(4096, 8192, None), (64, 64, None), (37, 130, None), (130, 4096, 4160),
