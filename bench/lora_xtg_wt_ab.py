@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--tokens", type=int, default=4096)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--calls", type=int, default=20)
-    ap.add_argument("--wgs", default="256", help="MXLLM_LORA_WGS (the wave-tile mode needs >= 4x this many tiles)")
+    ap.add_argument("--wgs", default="256", help="MXLLM_LORA_WGS")
+    ap.add_argument("--wt-min", default="1024", help="MXLLM_LORA_XTG_WT_MIN: tiles a launch needs for the wave-tile form")
     a = ap.parse_args()
     os.environ["MXLLM_LORA_WGS"] = a.wgs
+    os.environ["MXLLM_LORA_XTG_WT_MIN"] = a.wt_min
     dev = torch.device("cuda", 0)
     ops = native()
     T, r, pad = a.tokens, 16, 64

@@ -973,12 +973,11 @@ static int lora_splits(int tiles, int blocks, int smax) {
 }
 
 // lora_xtg with one 64-col tile per WAVE (XtgArgs::wt) where that still fills the chip with one
-// workgroup per CU and no row split (>= 4 x MXLLM_LORA_WGS tiles: the 70B gate-up gradients, 1,024
-// tiles): 119.1 -> 100.1 us per launch at T 4096 (profiles/r6g/: one round of 256 workgroups instead
+// workgroup per CU and no row split (>= 4 waves x 256 CUs = 1,024 tiles: the 70B gate-up gradients): 119.1 -> 100.1 us per launch at T 4096 (profiles/r6g/: one round of 256 workgroups instead
 // of four of 1,024, and no cross-wave reduction); the smaller launches do not qualify and measured
 // the same when forced.  MXLLM_LORA_XTG_WT=0 restores the row-split form (read per call: A/B)
 static bool xtg_wave_tiles(int ntiles) {
-  return lora_env("MXLLM_LORA_XTG_WT", 1) == 1 && ntiles >= 4 * lora_env("MXLLM_LORA_WGS", 256);
+  return lora_env("MXLLM_LORA_XTG_WT", 1) == 1 && ntiles >= lora_env("MXLLM_LORA_XTG_WT_MIN", 1024);
 }
 
 // lora_xwt kernel choice (MXLLM_LORA_XWT, read per call: an in-process A/B can flip it):
