@@ -294,6 +294,42 @@ bool gemm8_rope(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cos,
   return true;
 }
 
+// gemm8_rope on the tail-balanced schedule (mx_gemm8_rope_tail): columns [0, at) through the RoPE
+// epilogue, the rest as half-K images summed, rotated and scattered by one pass -- bitwise
+// gemm8_tail(at) followed by rope_split.  Returns false (nothing launched) for shapes it does not take.
+bool gemm8_rope_tail(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
+                     int64_t S, int64_t Hq, int64_t Hkv, at::Tensor& q, at::Tensor& k, at::Tensor& v, int64_t at) {
+  MX_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+           "gemm8_rope_tail: bf16 GPU operands");
+  MX_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1) && x.size(0) == B * S, "gemm8_rope_tail: shapes");
+  MX_CHECK(w.size(0) == (Hq + 2 * Hkv) * 128, "gemm8_rope_tail: head dim 128");
+  MX_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+               sin.is_contiguous() && cos.size(-1) == 64 && cos.size(0) >= S && sin.sizes() == cos.sizes(),
+           "gemm8_rope_tail: f32 [>= S, 64] tables");
+  for (const at::Tensor* t : {&q, &k, &v})
+    MX_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous(), "gemm8_rope_tail: bf16 outputs");
+  MX_CHECK(q.numel() == B * Hq * S * 128 && k.numel() == B * Hkv * S * 128 && v.numel() == k.numel(),
+           "gemm8_rope_tail: output sizes");
+  if (x.stride(1) != 1 || w.stride(1) != 1 || at <= 0 || at >= w.size(0)) return false;
+  if (x.size(0) > INT32_MAX || x.size(1) > INT32_MAX) return false;
+  DevGuard g(x.device());
+  auto ws = at::empty({2 * x.size(0) * (w.size(0) - at)}, x.options().dtype(at::kFloat));
+  MxG8Epi ep{};
+  ep.q = bfm(q);
+  ep.k = bfm(k);
+  ep.v = bfm(v);
+  ep.cosb = cos.data_ptr<float>();
+  ep.sinb = sin.data_ptr<float>();
+  ep.S = (int)S;
+  ep.Hq = (int)Hq;
+  ep.Hkv = (int)Hkv;
+  const int rc = mx_gemm8_rope_tail(bf(x), x.stride(0), bf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
+                                    (int)x.size(1), (int)at, ws.data_ptr<float>(), ep, cur_stream());
+  if (rc == -1) return false;
+  MX_OK(rc);
+  return true;
+}
+
 // Forward gate-up projection with SwiGLU in the GEMM epilogue (gemm8 G8_EPI_SWIGLU): x [T, K],
 // w = [gate; up] [2F, K] -> gu [T, 2F] (the projection output, kept for the backward) and
 // m = silu(gate) * up [T, F].  Returns false (nothing launched) for shapes the kernel does not take.
@@ -1241,6 +1277,7 @@ TORCH_LIBRARY(mxllm, m) {
   m.def("gemm8_stamps() -> Tensor", &gemm8_stamps);
   m.def("gemm8_tail(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, int at, bool rows=False, int ph=4, Tensor(b!)? sq=None) -> bool");
   m.def("gemm8_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, Tensor(a!) q, Tensor(b!) k, Tensor(c!) v) -> bool");
+  m.def("gemm8_rope_tail(Tensor x, Tensor w, Tensor cos, Tensor sin, int B, int S, int Hq, int Hkv, Tensor(a!) q, Tensor(b!) k, Tensor(c!) v, int at) -> bool");
   m.def("gemm8_swiglu(Tensor x, Tensor w, Tensor(a!) gu, Tensor(b!) m) -> bool");
   m.def("gemm8_sq(Tensor a, bool a_kc, Tensor b, bool b_kc, Tensor(a!) out, Tensor(b!) sq, Tensor? alpha_t=None, float alpha=1.0) -> bool");
   m.def("gemm8_swiglu_bwd(Tensor dy, Tensor w, Tensor gu, Tensor(a!) dgu, Tensor(b!)? m=None) -> bool");
@@ -1292,6 +1329,7 @@ TORCH_LIBRARY_IMPL(mxllm, CUDA, m) {
   m.impl("gemm8", &gemm8);
   m.impl("gemm8_tail", &gemm8_tail);
   m.impl("gemm8_rope", &gemm8_rope);
+  m.impl("gemm8_rope_tail", &gemm8_rope_tail);
   m.impl("gemm8_swiglu", &gemm8_swiglu);
   m.impl("gemm8_sq", &gemm8_sq);
   m.impl("gemm8_swiglu_bwd", &gemm8_swiglu_bwd);

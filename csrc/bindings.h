@@ -59,6 +59,8 @@ int mx_gemm8_sq(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int
 int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uint16_t* B, int64_t ldb, int b_kc, uint16_t* C,
                   int64_t ldc, int M, int N, int K, int rows, int at, float* ws, int ph, hipStream_t stream,
                   float* sq = nullptr);
+int mx_gemm8_rope_tail(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N, int K, int at,
+                       float* ws, MxG8Epi ep, hipStream_t stream);
 int mx_adamw(float* p, void* g, int grad_bf16, float* m, float* v, uint16_t* lowp, int16_t* lo, int64_t n,
              float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, const float* scale_t,
              float scale_f, int zero_grad, hipStream_t stream);

@@ -24,6 +24,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// Rotate-half RoPE of the pair (a, b) = (x[d], x[d + D/2]) by (c, s) = (cos, sin) of d's frequency,
+// with the contraction pinned (one explicit fma each) so every kernel that applies it -- rope_split,
+// the gemm8 RoPE epilogue and the tail-balanced sum pass -- produces the same bits.
+__device__ __forceinline__ float rope_lo(float a, float b, float c, float s) { return __builtin_fmaf(a, c, -(b * s)); }
+__device__ __forceinline__ float rope_hi(float a, float b, float c, float s) { return __builtin_fmaf(b, c, a * s); }
 __device__ __forceinline__ float bf2f(uint16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
 
 __device__ __forceinline__ uint16_t f2bf(float f) {

@@ -236,8 +236,8 @@ __device__ __forceinline__ void g8_epilogue_fused(f32x4 (&acc)[8][4], float alph
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const float a = x0[jl][c], bb = x1[jl][c];
-              x0[jl][c] = a * cs[c] - bb * sn[c];
-              x1[jl][c] = bb * cs[c] + a * sn[c];
+              x0[jl][c] = rope_lo(a, bb, cs[c], sn[c]);
+              x1[jl][c] = rope_hi(a, bb, cs[c], sn[c]);
             }
           }
         }
@@ -1353,6 +1353,103 @@ extern "C" int mx_gemm8_tail(const uint16_t* A, int64_t lda, int a_kc, const uin
   int64_t blocks = (part / 8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   g8_sum2_kernel<<<(int)blocks, 256, 0, stream>>>(ws, part, N2, C2, ldc, part);
+  return (int)hipGetLastError();
+}
+
+// Split part of mx_gemm8_rope_tail: the two fp32 K-part images P0, P1 [M, N2] of columns [col0, col0 + N2)
+// -> bf16(P0 + P1) in a fixed order (= g8_sum2_kernel), then, per 128-column head, the rotate-half RoPE
+// of rope_split_kernel (csrc/kernels/rope.hip: the same expression on the same bf16 values, so bitwise
+// the tail-balanced GEMM followed by rope_split) and the head-major scatter; v heads are copied.
+// One thread per (row, head, 8-column group of the head's first half).
+__global__ void __launch_bounds__(256) g8_sum2_rope_kernel(const float* __restrict__ P, int64_t part, int N2, int col0,
+                                                          int M, G8Epi ep) {
+  const int nh = N2 >> 7;
+  const int64_t n = (int64_t)M * nh * 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int g = (int)(i & 7);
+    const int64_t th = i >> 3;
+    const int hl = (int)(th % nh);
+    const int64_t m = th / nh;
+    const int head = (col0 >> 7) + hl;
+    const int b = (int)(m / ep.S), sq = (int)(m - (int64_t)b * ep.S);
+    const int c = hl * 128 + 8 * g;  // column inside the split part (first half of the head)
+    const float* p0 = P + m * N2 + c;
+    const float* p1 = P + part + m * N2 + c;
+    float x1[8], x2[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(p0 + 4 * h), b0 = *reinterpret_cast<const f32x4*>(p1 + 4 * h);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(p0 + 64 + 4 * h);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(p1 + 64 + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x1[4 * h + j] = bf2f(f2bf(a0[j] + b0[j]));
+        x2[4 * h + j] = bf2f(f2bf(a1[j] + b1[j]));
+      }
+    }
+    uint16_t* dst;
+    if (head < ep.Hq) {
+      dst = ep.q + (((int64_t)b * ep.Hq + head) * ep.S + sq) * 128;
+    } else if (head < ep.Hq + ep.Hkv) {
+      dst = ep.k + (((int64_t)b * ep.Hkv + (head - ep.Hq)) * ep.S + sq) * 128;
+    } else {
+      dst = ep.v + (((int64_t)b * ep.Hkv + (head - ep.Hq - ep.Hkv)) * ep.S + sq) * 128;
+      u16x8 y1, y2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y1[j] = f2bf(x1[j]), y2[j] = f2bf(x2[j]);
+      *reinterpret_cast<u16x8*>(dst + 8 * g) = y1;
+      *reinterpret_cast<u16x8*>(dst + 64 + 8 * g) = y2;
+      continue;
+    }
+    const float* cp = ep.cosb + (int64_t)sq * 64 + 8 * g;
+    const float* sp = ep.sinb + (int64_t)sq * 64 + 8 * g;
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(sp), s1 = *reinterpret_cast<const f32x4*>(sp + 4);
+    u16x8 y1, y2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cj = j < 4 ? c0[j & 3] : c1[j & 3];
+      const float sj = j < 4 ? s0[j & 3] : s1[j & 3];
+      const float a = x1[j], bb = x2[j];
+      y1[j] = f2bf(rope_lo(a, bb, cj, sj));
+      y2[j] = f2bf(rope_hi(a, bb, cj, sj));
+    }
+    *reinterpret_cast<u16x8*>(dst + 8 * g) = y1;
+    *reinterpret_cast<u16x8*>(dst + 64 + 8 * g) = y2;
+  }
+}
+
+// qkv projection (A = x [M][K], B = W [N][K], both k-contiguous; N = (Hq + 2 Hkv) * 128, M = B * S) with
+// the RoPE + head split fused, on the tail-balanced schedule of mx_gemm8_tail: columns [0, at) (whole
+// waves of tiles) through the G8_EPI_ROPE epilogue, columns [at, N) as twice as many half-K workgroups
+// into the two fp32 images in `ws` (2 * M * (N - at) floats), finished by g8_sum2_rope_kernel.  Removes
+// the qkv round trip through HBM and the rope_split pass of the LoRA-augmented qkv forward, whose GEMM
+// runs this tail-balanced launch anyway (70B: 16 x 40 tiles, `at` 8192 = the q heads).  Returns -1
+// (nothing launched) for shapes it does not take.
+extern "C" int mx_gemm8_rope_tail(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N, int K,
+                                  int at, float* ws, G8Epi ep, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K < 2 * G8_BK || (M & 255) || (N & 255) || K % G8_BK) return -1;
+  if (at <= 0 || at >= N || (at & 255)) return -1;
+  if (lda % 8 || ldb % 8 || lda < K || ldb < K || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)ws) & 15)) return -1;
+  const int64_t aspan = 256 * lda, bspan = (int64_t)N * ldb;
+  if (aspan * 2 >= ((int64_t)1 << 31) || bspan * 2 >= ((int64_t)1 << 31)) return -1;
+  if (N != (ep.Hq + 2 * ep.Hkv) * 128 || ep.S <= 0 || ep.S % 256 || M % ep.S || !ep.q || !ep.k || !ep.v ||
+      !ep.cosb || !ep.sinb || (((uintptr_t)ep.q | (uintptr_t)ep.k | (uintptr_t)ep.v) & 15) ||
+      (((uintptr_t)ep.cosb | (uintptr_t)ep.sinb) & 15))
+    return -1;
+  // plain part: the epilogue writes q / k / v of the heads in [0, at) (tile pn covers heads 2 pn, 2 pn + 1)
+  gemm8_kernel<true, true, false, false, 0, 4, G8_EPI_ROPE><<<(M >> 8) * (at >> 8), 512, 0, stream>>>(
+      A, lda, B, ldb, nullptr, 0, M, at, K, nullptr, 1.f, 0, 0, ep);
+  // split part: columns [at, N), two half-K images
+  const int N2 = N - at;
+  const int k0 = (K / G8_BK / 2) * G8_BK;
+  const int64_t part = (int64_t)M * N2;
+  const dim3 grid((M >> 8) * (N2 >> 8), 2);
+  gemm8_kernel<true, true, true, false, 0, 4><<<grid, 512, 0, stream>>>(A, lda, B + (int64_t)at * ldb, ldb, ws, N2, M,
+                                                                        N2, K, nullptr, 1.f, k0, part);
+  int64_t blocks = ((int64_t)M * (N2 >> 7) * 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  g8_sum2_rope_kernel<<<(int)blocks, 256, 0, stream>>>(ws, part, N2, at, M, ep);
   return (int)hipGetLastError();
 }
 

@@ -55,8 +55,8 @@ __global__ void __launch_bounds__(256) rope_split_kernel(const uint16_t* __restr
       const float cj = j < 4 ? c0[j & 3] : c1[j & 3];
       const float sj = j < 4 ? s0[j & 3] : s1[j & 3];
       const float a = bf2f(x1[j]), bb = bf2f(x2[j]);
-      y1[j] = f2bf(a * cj - bb * sj);
-      y2[j] = f2bf(bb * cj + a * sj);
+      y1[j] = f2bf(rope_lo(a, bb, cj, sj));
+      y2[j] = f2bf(rope_hi(a, bb, cj, sj));
     }
     *reinterpret_cast<u16x8*>(dst + c) = y1;
     *reinterpret_cast<u16x8*>(dst + HALF + c) = y2;

@@ -258,12 +258,20 @@ class Llama(nn.Module):
         layer = self.layers[i]
         rec = self._recompute_m(layer, i)
         rec_x = rec and RECOMPUTE_NORM != "0"
+        lora_at = (ops.lora_qkv_attention_at(x, layer.wqkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim)
+                   if self.seq_parallel is None and layer.wqkv.lora_r and not rec_x else 0)
         if (self.seq_parallel is None and not layer.wqkv.lora_r
                 and fused.qkv_attention_ok(x, layer.wqkv.weight, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim)):
             # projection + RoPE + head split in ONE GEMM epilogue (mxllm/ops/fused.py)
             o = fused.qkv_attention(x, layer.wqkv.weight, self.rope_cos, self.rope_sin, B, S, cfg.n_heads,
                                     cfg.n_kv_heads, cfg.head_dim, causal=True, out_pad=self._pad(layer.wo),
                                     norm=(h, layer.attn_norm, cfg.norm_eps) if rec_x else None)
+            qkv = None
+        elif lora_at:
+            # LoRA: the augmented projection with RoPE + head split in its tail-balanced GEMM
+            # (mxllm/ops/linear.py lora_qkv_attention): no qkv activation, no rope_split pass
+            o = ops.lora_qkv_attention(x, layer.wqkv, self.rope_cos, self.rope_sin, B, S, cfg.n_heads,
+                                       cfg.n_kv_heads, cfg.head_dim, lora_at, causal=True, out_pad=self._pad(layer.wo))
             qkv = None
         else:
             qkv = (ops.normed_linear(x, h, layer.attn_norm, cfg.norm_eps, layer.wqkv.weight) if rec_x

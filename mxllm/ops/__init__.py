@@ -9,5 +9,5 @@ from .activation import lora_tail_ok, swiglu  # noqa: F401
 from .loss import linear_cross_entropy, cross_entropy  # noqa: F401
 from .optim import SplitMaster, adamw_step_, sq_norm  # noqa: F401
 from .embedding import embedding  # noqa: F401
-from .linear import linear, lora_linear, lora_linear_aug, linear_swiglu, norm_linear, normed_linear, qkv_rope_linear, qkv_rope_ok, swiglu_linear, transpose2d  # noqa: F401
+from .linear import linear, lora_linear, lora_linear_aug, lora_qkv_attention, lora_qkv_attention_at, linear_swiglu, norm_linear, normed_linear, qkv_rope_linear, qkv_rope_ok, swiglu_linear, transpose2d  # noqa: F401
 from . import reference  # noqa: F401

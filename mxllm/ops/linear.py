@@ -25,6 +25,7 @@ cast or accumulate kernels — and DDP is told via ``mark_ready``.
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Sequence
 
@@ -115,6 +116,64 @@ def _lora_native(x2: torch.Tensor, N: int, K: int, splits, r: int, wbt) -> bool:
             and r <= 64 and all(n % 64 == 0 for n in splits) and x2.dtype == torch.bfloat16)
 
 
+def _lora_aug_backward(ctx, xa, wbuf, dy, dy_tail: bool, need_a: bool, need_b: bool):
+    """Backward of the augmented LoRA projection (``_LoRAAugFn``; also the LoRA half of
+    ``_LoRAQKVAttnFn``): (dx reshaped to the input, dA or None, dB or None).  ``ctx`` carries
+    ``dims`` = (N, K, s, splits, r, pad, xshape, nat, tr) and ``lora_a`` / ``lora_b`` / ``wbt`` / ``wxt``."""
+    N, K, s, splits, r, pad, xshape, nat, tr = ctx.dims
+    R = r * len(splits)
+    dy2 = dy.reshape(-1, N)
+    dya = _padded_rows(dy2, pad) if dy_tail else None
+    if dya is None:  # ``dy_tail``: the SwiGLU backward already wrote s dy B into the pad columns
+        dya = _augment(dy2, pad)
+        if nat:
+            native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s, len(splits) * r)  # g = s dy B, zero in the pad columns
+        else:
+            bmat = wbuf[K:, :N].t() if tr else wbuf[:N, K:]  # B [N, pad]
+            dya[:, N:].addmm_(dy2, bmat, beta=0.0, alpha=s)
+    g = dya[:, N:N + R]
+    x2, st = xa[:, :K], xa[:, K:K + R]
+    da = db = None
+    ga = direct_grad(ctx.lora_a) if need_a else None
+    gb = direct_grad(ctx.lora_b) if need_b else None
+    if nat and need_a and need_b:
+        # dA and every diagonal dB_i in one launch, straight into the flat grads when present
+        acc = ga is not None and gb is not None
+        tga = ga if acc else torch.empty(R, K, dtype=dy2.dtype, device=dy2.device)
+        tgb = gb if acc else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
+        native().lora_grads(x2, dy2, dya[:, N:], xa[:, K:], tga, tgb, list(splits), r, acc)
+        if acc:
+            mark_ready(ctx.lora_a)
+            mark_ready(ctx.lora_b)
+        else:
+            da, db = tga, tgb
+    else:
+        if need_a:
+            if ga is not None:
+                ga.addmm_(g.t(), x2)
+                mark_ready(ctx.lora_a)
+            else:
+                da = torch.mm(g.t(), x2)
+        if need_b:
+            tgt = gb if gb is not None else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
+            off = 0
+            for i, n_i in enumerate(splits):
+                tgt[off:off + n_i, i * r:(i + 1) * r].addmm_(dy2[:, off:off + n_i].t(), st[:, i * r:(i + 1) * r],
+                                                            beta=1.0 if gb is not None else 0.0)
+                off += n_i
+            if gb is not None:
+                mark_ready(ctx.lora_b)
+            else:
+                db = tgt
+    if tr:  # [W; A]^T is the leading K rows of the transposed buffer: TN form
+        dx = gemm.mm("tn", dya, wbuf[:K, :])
+    elif ctx.wxt is not None:  # reduction-contiguous image of [W; A]: hipBLASLt "TN"
+        dx = gemm.mm("tn", dya, ctx.wxt)
+    else:  # the n-contiguous weight itself ("NN": gemm8 where it wins, csrc/kernels/gemm8.hip)
+        dx = gemm.mm("nn", dya, wbuf[:, :K])
+    return dx.view(xshape), da, db
+
+
 class _LoRAAugFn(torch.autograd.Function):
     """LoRA projection as ONE augmented GEMM per direction (FusedLinear, models/llama.py).
 
@@ -164,59 +223,9 @@ class _LoRAAugFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xa, wbuf = ctx.saved_tensors
-        N, K, s, splits, r, pad, xshape, nat, tr = ctx.dims
-        R = r * len(splits)
-        dy2 = dy.reshape(-1, N)
-        dya = _padded_rows(dy2, pad) if ctx.dy_tail else None
-        if dya is None:  # ``dy_tail``: the SwiGLU backward already wrote s dy B into the pad columns
-            dya = _augment(dy2, pad)
-            if nat:
-                native().lora_xwt(dy2, ctx.wbt, dya[:, N:], s, len(splits) * r)  # g = s dy B, zero in the pad columns
-            else:
-                bmat = wbuf[K:, :N].t() if tr else wbuf[:N, K:]  # B [N, pad]
-                dya[:, N:].addmm_(dy2, bmat, beta=0.0, alpha=s)
-        g = dya[:, N:N + R]
-        x2, st = xa[:, :K], xa[:, K:K + R]
-        da = db = None
-        need_a, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
-        ga = direct_grad(ctx.lora_a) if need_a else None
-        gb = direct_grad(ctx.lora_b) if need_b else None
-        if nat and need_a and need_b:
-            # dA and every diagonal dB_i in one launch, straight into the flat grads when present
-            acc = ga is not None and gb is not None
-            tga = ga if acc else torch.empty(R, K, dtype=dy2.dtype, device=dy2.device)
-            tgb = gb if acc else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
-            native().lora_grads(x2, dy2, dya[:, N:], xa[:, K:], tga, tgb, list(splits), r, acc)
-            if acc:
-                mark_ready(ctx.lora_a)
-                mark_ready(ctx.lora_b)
-            else:
-                da, db = tga, tgb
-        else:
-            if need_a:
-                if ga is not None:
-                    ga.addmm_(g.t(), x2)
-                    mark_ready(ctx.lora_a)
-                else:
-                    da = torch.mm(g.t(), x2)
-            if need_b:
-                tgt = gb if gb is not None else torch.zeros(N, R, dtype=dy2.dtype, device=dy2.device)
-                off = 0
-                for i, n_i in enumerate(splits):
-                    tgt[off:off + n_i, i * r:(i + 1) * r].addmm_(dy2[:, off:off + n_i].t(), st[:, i * r:(i + 1) * r],
-                                                                beta=1.0 if gb is not None else 0.0)
-                    off += n_i
-                if gb is not None:
-                    mark_ready(ctx.lora_b)
-                else:
-                    db = tgt
-        if tr:  # [W; A]^T is the leading K rows of the transposed buffer: TN form
-            dx = gemm.mm("tn", dya, wbuf[:K, :])
-        elif ctx.wxt is not None:  # reduction-contiguous image of [W; A]: hipBLASLt "TN"
-            dx = gemm.mm("tn", dya, ctx.wxt)
-        else:  # the n-contiguous weight itself ("NN": gemm8 where it wins, csrc/kernels/gemm8.hip)
-            dx = gemm.mm("nn", dya, wbuf[:, :K])
-        return dx.view(xshape), da, db, None, None, None, None, None, None, None, None, None, None
+        dx, da, db = _lora_aug_backward(ctx, xa, wbuf, dy, ctx.dy_tail, ctx.needs_input_grad[1],
+                                        ctx.needs_input_grad[2])
+        return dx, da, db, None, None, None, None, None, None, None, None, None, None
 
 
 def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: torch.Tensor, splits: Sequence[int],
@@ -231,6 +240,94 @@ def lora_linear_aug(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, wbuf: tor
     tensor arrives in its padded buffer, recomputed otherwise."""
     r = a.shape[0] // len(splits)
     return _LoRAAugFn.apply(x, a, b, wbuf, scaling, tuple(splits), r, pad, wbt, wxt, wa, bool(x_tail), bool(dy_tail))
+
+
+_LORA_QKV_ROPE = os.environ.get("MXLLM_LORA_QKV_ROPE", "1") != "0"  # A/B switch
+
+
+def lora_qkv_attention_at(x: torch.Tensor, lin, B: int, S: int, Hq: int, Hkv: int, D: int) -> int:
+    """The tail-balanced split column ``at`` (> 0) when the LoRA q/k/v projection ``lin`` (a FusedLinear
+    with an augmented, non-transposed buffer) can run as ``lora_qkv_attention``: exactly when its
+    unfused forward GEMM would run the tail-balanced gemm8 launch (the dispatch table's ``tail``
+    entry for the augmented shape), whose RoPE variant then replaces GEMM + rope_split; 0 otherwise."""
+    from .fused import _g8_operands_ok
+
+    if not (_LORA_QKV_ROPE and lin.lora_r > 0 and lin.augmented() and not lin.transposed and D == 128
+            and S % 256 == 0 and use_native(x) and x.dtype == torch.bfloat16 and not gemm.deterministic()):
+        return 0
+    N, K, pad = sum(lin.splits), lin.in_features, lin.pad
+    x2 = x.reshape(-1, x.shape[-1])
+    if N != (Hq + 2 * Hkv) * D or x2.shape[0] != B * S or x2.shape[1] != K:
+        return 0
+    xa = _padded_rows(x2, pad)
+    if xa is None or not _g8_operands_ok(xa, lin.wbuf[:N, :]):
+        return 0
+    key = ("tn", B * S, N, K + pad, "bf16")
+    if not gemm.schedule("tn", B * S, N, K + pad, torch.bfloat16):
+        return 0
+    gemm._table()
+    at = gemm._TAIL.get(key, 0)
+    return at if at > 0 else 0
+
+
+def _lora_aug_input(x2, a, wbuf, amat, scaling, N, K, pad, nat):
+    """x_aug = [x | s x A^T] in x's padded row buffer (see _LoRAAugFn)."""
+    xa = _augment(x2, pad)
+    if nat:
+        native().lora_xwt(x2, amat, xa[:, K:], scaling, a.shape[0])  # s t, zero in the pad columns
+    else:
+        xa[:, K:].addmm_(x2, amat.t(), beta=0.0, alpha=scaling)
+    return xa
+
+
+class _LoRAQKVAttnFn(torch.autograd.Function):
+    """LoRA q/k/v projection + RoPE + head split + flash attention in one autograd node.  The augmented
+    GEMM of ``_LoRAAugFn`` runs as the tail-balanced gemm8 launch with the RoPE epilogue
+    (csrc/kernels/gemm8.hip ``mx_gemm8_rope_tail``: q / k / v written head-major by the plain part's
+    epilogue and by the split part's sum pass), so neither the [T, N] qkv activation nor the
+    rope_split pass touches HBM -- bitwise the GEMM + rope_split it replaces.  Backward: the attention
+    backward writes d(qkv) (inverse RoPE applied) into a buffer padded for the LoRA tail, then the
+    LoRA backward of ``_LoRAAugFn``."""
+
+    @staticmethod
+    def forward(ctx, x, a, b, wbuf, scaling, splits, r, pad, wbt, wxt, cos, sin, B, S, Hq, Hkv, D, causal, out_pad,
+                at):
+        N, K = wbuf.shape[0] - pad, wbuf.shape[1] - pad
+        x2 = x.reshape(-1, K)
+        nat = _lora_native(x2, N, K, splits, r, wbt)
+        xa = _lora_aug_input(x2, a, wbuf, wbuf[N:, :K], scaling, N, K, pad, nat)
+        ops = native()
+        q = torch.empty(B, Hq, S, D, dtype=x.dtype, device=x.device)
+        k = torch.empty(B, Hkv, S, D, dtype=x.dtype, device=x.device)
+        v = torch.empty_like(k)
+        if not ops.gemm8_rope_tail(xa, wbuf[:N, :], cos, sin, B, S, Hq, Hkv, q, k, v, at):
+            q, k, v = ops.rope_split(gemm.mm("tn", xa, wbuf[:N, :]), cos, sin, B, S, Hq, Hkv, D)
+        o, lse = ops.attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D), out_pad)
+        ctx.save_for_backward(xa, wbuf, q, k, v, o, lse, cos, sin)
+        ctx.lora_a, ctx.lora_b, ctx.wbt, ctx.wxt = a, b, wbt, wxt
+        ctx.dims = (N, K, scaling, tuple(splits), r, pad, x.shape, nat, False)
+        ctx.causal = causal
+        return o.view(B * S, Hq * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        from .attention import backward_dqkv
+
+        xa, wbuf, q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        pad = ctx.dims[5]
+        dqkv = backward_dqkv(do, q, k, v, o, lse, cos, sin, ctx.causal, pad)  # left part of [T, N + pad]
+        del q, k, v, o, lse
+        dx, da, db = _lora_aug_backward(ctx, xa, wbuf, dqkv, False, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        return (dx, da, db) + (None,) * 17
+
+
+def lora_qkv_attention(x: torch.Tensor, lin, cos: torch.Tensor, sin: torch.Tensor, B: int, S: int, Hq: int,
+                       Hkv: int, D: int, at: int, causal: bool = True, out_pad: int = 0) -> torch.Tensor:
+    """attention(rope(split(lora_qkv(x)))) -> [B*S, Hq*D] for the LoRA FusedLinear ``lin`` (callers take
+    ``at`` from ``lora_qkv_attention_at``)."""
+    r = lin.lora_a.shape[0] // len(lin.splits)
+    return _LoRAQKVAttnFn.apply(x, lin.lora_a, lin.lora_b, lin.wbuf, lin.scaling, tuple(lin.splits), r, lin.pad,
+                                lin.wbt, getattr(lin, "wxt", None), cos, sin, B, S, Hq, Hkv, D, causal, out_pad, at)
 
 
 def transpose2d(t: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:

@@ -49,14 +49,12 @@ def test_gemm8_rope_epilogue(gpu, B, S, Hq, Hkv, K):
     for got, want in ((q, qr), (k, kr), (v, vr)):
         assert _rel(got, want) < 5e-3
         assert (got.float() - want).abs().max().item() < 0.05 * want.abs().max().item()
-    # the unfused path on the same GEMM: gemm8 (4-phase) -> rope_split, near-bitwise
+    # the unfused path on the same GEMM: gemm8 (4-phase) -> rope_split, bitwise (the rotation's fma
+    # contraction is pinned in both kernels: common.h rope_lo / rope_hi)
     qkv = torch.empty(B * S, N, device=gpu, dtype=torch.bfloat16)
     assert _ops().gemm8(x, True, w, True, qkv, 0.0, None, 1.0, 4)
     q2, k2, v2 = _ops().rope_split(qkv, cos, sin, B, S, Hq, Hkv, D)
-    assert torch.equal(v, v2)  # no rotation: the identical GEMM result
-    for a, b in ((q, q2), (k, k2)):
-        d = (a.float() - b.float()).abs()
-        assert d.max().item() <= 2 ** -6 * max(1.0, b.abs().max().item())  # one bf16 ulp (fma contraction)
+    assert torch.equal(v, v2) and torch.equal(q, q2) and torch.equal(k, k2)
 
 
 @pytest.mark.parametrize("T,F,K", [(256, 128, 512), (512, 1024, 1024), (4096, 14336, 4096)])
@@ -192,5 +190,70 @@ def test_fused_mlp_recompute_m_bitwise(gpu, monkeypatch):
         assert not calls, "the recompute path must not run the standalone SwiGLU"
     (l1, g1), (l0, g0) = res["1"], res["0"]
     assert l1 == l0
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,K,at", [(2, 256, 4, 2, 576, 512), (1, 512, 8, 4, 1088, 1024),
+                                              (2, 2048, 64, 8, 8256, 8192)])
+def test_gemm8_rope_tail_bitwise(gpu, B, S, Hq, Hkv, K, at):
+    """The tail-balanced qkv GEMM with RoPE fused (plain part through the epilogue, split part's sum
+    pass rotating and scattering) writes bitwise the q / k / v of gemm8_tail(at) + rope_split --
+    the LoRA augmented qkv forward it replaces (K = in + pad, 70B shape included)."""
+    from mxllm.ops.reference import rope_tables
+
+    N = (Hq + 2 * Hkv) * 128
+    x = _mat(B * S, K, gpu, 1)
+    w = _mat(N, K, gpu, 2)
+    cos, sin = (t.to(gpu).float().contiguous() for t in rope_tables(S, 128, 500000.0, None))
+    qkv = torch.empty(B * S, N, dtype=torch.bfloat16, device=gpu)
+    assert _ops().gemm8_tail(x, True, w, True, qkv, at, False, 4)
+    q0, k0, v0 = _ops().rope_split(qkv, cos, sin, B, S, Hq, Hkv, 128)
+    q = torch.full((B, Hq, S, 128), float("nan"), dtype=torch.bfloat16, device=gpu)
+    k = torch.full((B, Hkv, S, 128), float("nan"), dtype=torch.bfloat16, device=gpu)
+    v = torch.full_like(k, float("nan"))
+    assert _ops().gemm8_rope_tail(x, w, cos, sin, B, S, Hq, Hkv, q, k, v, at)
+    assert torch.equal(q, q0) and torch.equal(k, k0) and torch.equal(v, v0)
+
+
+def test_lora_qkv_attention_matches_unfused(gpu, monkeypatch):
+    """A 2-layer LoRA model (head dim 128) whose q/k/v projection takes the tail-balanced launch:
+    loss and every adapter gradient bitwise equal with the RoPE-fused LoRA qkv path
+    (ops.lora_qkv_attention) and without it (augmented GEMM -> rope_split -> attention)."""
+    from mxllm.models import Llama, get_config
+    import importlib
+
+    from mxllm.ops import gemm
+
+    lin_mod = importlib.import_module("mxllm.ops.linear")  # the module (mxllm.ops.linear is also a function name)
+
+    monkeypatch.setenv("MXLLM_GEMM8", "all")
+    cfg = get_config("tiny-d128").replace(n_layers=2, vocab_size=512)
+    B, S = 2, 256
+    gemm._table()
+    key = ("tn", B * S, (cfg.n_heads + 2 * cfg.n_kv_heads) * 128, cfg.hidden + 64, "bf16")
+    monkeypatch.setitem(gemm._TAIL, key, 512)  # the unfused forward takes the same tail-balanced launch
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=gpu, generator=torch.Generator(device=gpu).manual_seed(6))
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(lin_mod, "_LORA_QKV_ROPE", on)
+        calls = []
+        real = lin_mod._LoRAQKVAttnFn.apply
+        monkeypatch.setattr(lin_mod._LoRAQKVAttnFn, "apply", lambda *a, _r=real: (calls.append(1), _r(*a))[1])
+        model = Llama(cfg, device=gpu, dtype=torch.bfloat16, seed=3, lora_r=16)
+        with torch.no_grad():
+            for i, mod in enumerate(model.modules()):
+                if getattr(mod, "lora_r", 0):
+                    for blk in mod.lora_b_blocks():
+                        blk.copy_(torch.randn(blk.shape, generator=torch.Generator().manual_seed(i)) * 0.02)
+        model.sync_adapters_()
+        loss = model(ids, ids)
+        loss.backward()
+        res[on] = (float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None})
+        assert (len(calls) == cfg.n_layers) == on, calls
+        monkeypatch.setattr(lin_mod._LoRAQKVAttnFn, "apply", real)
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert l1 == l0
+    assert set(g1) == set(g0) and g0
     for n in g0:
         assert torch.equal(g1[n], g0[n]), n
