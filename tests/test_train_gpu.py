@@ -309,8 +309,16 @@ def test_bucketed_grad_norm_overlap(gpu, gdt, accum, monkeypatch):
 
 def test_fused_grad_norm_matches_full_pass(gpu, monkeypatch):
     """The clip norm from the dW GEMMs' per-tile partials (gemm8_sq) plus a direct pass over the other
-    gradients equals the full pass over the flat gradient to fp32 rounding, every armed GEMM weight
-    took the fused path, and training stays on the same trajectory."""
+    gradients equals the full pass over the SAME flat gradient to fp32 rounding at every step, every armed
+    GEMM weight took the fused path, and the first step's gradients and update match the full-pass trainer.
+
+    Only the first step is compared across the two trainers: the two norms differ in their last fp32 bits
+    (different summation order), so the clip coefficients do, and from the second step on a master value
+    sitting on a bf16 rounding boundary can round the other way -- after that the runs are different
+    (equally valid) trajectories (scripts/diag/fused_norm_diag.py: step-0 gradients bitwise equal, step-1
+    gradients ~1 bf16 ulp apart)."""
+    from mxllm import ops
+
     monkeypatch.setenv("MXLLM_GEMM8", "all")  # the tiny shapes on gemm8 (the table holds real ones)
     cfg = _cfg()
     g = torch.Generator(device=gpu).manual_seed(3)
@@ -319,19 +327,22 @@ def test_fused_grad_norm_matches_full_pass(gpu, monkeypatch):
     for fused in ("1", "0"):
         monkeypatch.setenv("MXLLM_FUSED_GRAD_NORM", fused)
         tr = _ddp_trainer(gpu, cfg, 5)
-        norms = []
-        for b in batches:
-            tr.train_step([(b, b)])
-            norms.append(float(tr.last_grad_norm))
+        tr.train_step([(batches[0], batches[0])])
+        res[fused] = (float(tr.last_grad_norm), tr.flat.grads.clone(), _masters(tr))
         if fused == "1":
+            for i, b in enumerate(batches):
+                if i:
+                    tr.train_step([(b, b)])
+                got = float(tr.last_grad_norm)
+                ref = float(ops.sq_norm(tr.flat.grads).sqrt())
+                assert abs(got - ref) <= 1e-6 * ref, (i, got, ref)
             done = [n for n, p in tr.model.named_parameters() if getattr(p, "_mx_sq_done", None) is True]
             assert tr._sq_params and any("wgu" in n for n in done) and any("wd" in n for n in done), done
             assert not any("tok_emb" in n for n in done)  # the embedding gradient is summed directly
         else:
             assert not tr._sq_params
-        res[fused] = (norms, _masters(tr))
-    (n1, m1), (n0, m0) = res["1"], res["0"]
-    for a, b in zip(n1, n0):
-        assert abs(a - b) <= 1e-5 * b, (n1, n0)
+    (n1, g1, m1), (n0, g0, m0) = res["1"], res["0"]
+    assert abs(n1 - n0) <= 1e-6 * n0, (n1, n0)
+    assert torch.equal(g1, g0)  # the fused dW GEMMs store the same gradient bits
     for k in m0:
         assert torch.allclose(m1[k].float(), m0[k].float(), rtol=0, atol=1e-6), k
