@@ -109,11 +109,20 @@ class Trainer:
         self._chunks: list[tuple[int, int]] | None = None
         self._pending: list = []
         self._hold = None
+        lora = bool(getattr(model, "lora", False))
         if overlap_optimizer is None:
             overlap_optimizer = (_overlap_default() and self.flat.device.type == "cuda" and self.zero1 is None
-                                 and not getattr(model, "lora", False))
+                                 and (not lora or os.environ.get("MXLLM_LORA_OVERLAP_ADAMW", "0") == "1"))
+        # LoRA: opt-in -- the headline measured 1.5 ms/step SLOWER overlapped (860.5 / 861.5 vs 858.7 /
+        # 860.4 ms same box, profiles/r6m/): the update is 2.6 ms of HBM streaming that time-shares the
+        # CUs of the forward's GEMMs instead of hiding under them
+        self._chunk_copies: list | None = None  # LoRA: per chunk, the adapter -> wbuf copy launch
         if overlap_optimizer and self.zero1 is None and getattr(model, "param_wait", "absent") is None:
             self._chunks = self._forward_chunks()
+            if self._chunks is not None and lora:
+                self._chunk_copies = self._adapter_chunk_copies()
+                if self._chunk_copies is None:
+                    self._chunks = None
             if self._chunks is not None:
                 self._side = torch.cuda.Stream(self.flat.device) if self.flat.device.type == "cuda" else None
                 cus = os.environ.get("MXLLM_ADAMW_CUS", "")
@@ -242,6 +251,39 @@ class Trainer:
             return None
         return chunks
 
+    def _adapter_chunk_copies(self) -> list | None:
+        """LoRA with the overlapped update: per forward chunk, ONE batched copy (csrc/kernels/misc.hip
+        ``copy2d_batched``) of the chunk's adapters into their augmented GEMM buffers, issued on the
+        side stream right after the chunk's AdamW, so the next forward's wait before layer i also
+        covers its GEMM buffers (the one end-of-step copy of every adapter would have to wait for the
+        whole update).  None when an augmented projection's adapters are not inside one chunk."""
+        from ..models.llama import FusedLinear
+        from ..ops.linear import copy2d_plan
+
+        if not ops.native_available() or self.flat.device.type != "cuda":
+            return None
+        chunk_of = {}
+        for g in self.model._wait_groups():
+            k = self._group_chunk.get(id(g))
+            if k is not None:
+                for p in g:
+                    chunk_of.setdefault(id(p), k)
+        per: list[list] = [[] for _ in self._chunks]
+        for mod in self.model.modules():
+            if isinstance(mod, FusedLinear) and mod.augmented():
+                ka, kb = chunk_of.get(id(mod.lora_a)), chunk_of.get(id(mod.lora_b))
+                if ka is None or ka != kb:
+                    return None
+                per[ka].extend(mod.adapter_copies())
+        out = []
+        for pairs in per:
+            if not pairs:
+                out.append(None)
+                continue
+            rows, total = copy2d_plan(pairs)
+            out.append((torch.tensor(rows, dtype=torch.int64, device=self.flat.device), total))
+        return out
+
     def _param_wait(self, group):
         """``Llama.param_wait``: the compute stream waits for the update of the
         chunk holding ``group`` (no host synchronisation)."""
@@ -299,6 +341,9 @@ class Trainer:
         ops.adamw_step_(self.flat.master[lo:hi], self.flat.grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
                         None if lowp is None else lowp[lo:hi], grad_scale=gscale,
                         zero_grad=not self.fresh_grads, **kw)
+        if self._chunk_copies is not None and self._chunk_copies[k] is not None:
+            desc, blocks = self._chunk_copies[k]  # this chunk's adapters -> their GEMM buffers
+            ops.native().copy2d_batched(desc, blocks)
         ev = torch.cuda.Event()
         ev.record(side)
         self._pending[k] = ev
@@ -431,7 +476,8 @@ class Trainer:
                             beta1=o.beta1, beta2=o.beta2, eps=o.eps, weight_decay=o.weight_decay,
                             step=self.step_num, grad_scale=gscale,
                             zero_grad=not self.fresh_grads)  # else grads cleared in the same pass
-        self._sync_adapters()
+        if self._chunk_copies is None or self._side is None:
+            self._sync_adapters()  # (overlapped LoRA on GPU: each chunk copies its adapters after its update)
         self.flat.attach_grads()
 
     def _fused_sq(self):

@@ -73,6 +73,45 @@ def test_overlapped_adamw_bitwise(gpu, gdt, sched, monkeypatch):
         assert torch.equal(w, out[True][1][n]), n
 
 
+@pytest.mark.parametrize("cfg_name", ["tiny-d128", "tiny"])
+def test_lora_overlapped_adamw_bitwise(gpu, cfg_name, monkeypatch):
+    """LoRA with the overlapped update (MXLLM_LORA_OVERLAP_ADAMW=1, opt-in): each forward chunk's
+    AdamW runs on the side stream followed by the copy of its adapters into their augmented GEMM
+    buffers, and the next forward waits per layer.  Same losses and masters bit for bit as the
+    one-launch update + one end-of-step copy, and every GEMM buffer holds the updated adapters."""
+    from mxllm.models import Llama, get_config
+    from mxllm.models.llama import FusedLinear
+    from mxllm.parallel.runtime import DistEnv
+    from mxllm.train.trainer import OptimConfig, Trainer
+
+    cfg = get_config(cfg_name).replace(n_layers=3, vocab_size=1024)
+    g = torch.Generator(device=gpu).manual_seed(5)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 256), device=gpu, generator=g) for _ in range(3)]
+    out = {}
+    for ovl in ("0", "1"):
+        monkeypatch.setenv("MXLLM_LORA_OVERLAP_ADAMW", ovl)
+        model = Llama(cfg, device=gpu, seed=2, lora_r=16)
+        with torch.no_grad():  # non-zero B: every adapter gets a gradient
+            for i, mod in enumerate(model.modules()):
+                if getattr(mod, "lora_r", 0):
+                    for blk in mod.lora_b_blocks():
+                        blk.normal_(0, 0.02, generator=torch.Generator(device=gpu).manual_seed(i))
+        tr = Trainer(model, DistEnv(device=gpu, backend="nccl"), OptimConfig(lr=1e-3, weight_decay=0.01))
+        assert tr.overlap_optimizer == (ovl == "1")
+        if ovl == "1":
+            assert tr._chunk_copies is not None and sum(c is not None for c in tr._chunk_copies) == 3
+        losses = [float(tr.train_step([(b, b)])) for b in batches]
+        tr.params_ready()
+        for mod in model.modules():
+            if isinstance(mod, FusedLinear) and mod.augmented():
+                for src, dst in mod.adapter_copies():
+                    assert torch.equal(src, dst)
+        out[ovl] = (losses, _masters(tr))
+    assert out["0"][0] == out["1"][0]
+    for n, w in out["0"][1].items():
+        assert torch.equal(w, out["1"][1][n]), n
+
+
 def test_overlap_is_default_for_full_finetune(gpu):
     tr = _ddp_trainer(gpu, _cfg(), 3)
     assert tr.overlap_optimizer and len(tr._chunks) == 5  # embedding, 3 layers, head
